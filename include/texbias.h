@@ -1,0 +1,147 @@
+/* texbias.h -- C ABI of the MI355X (gfx950) k-space / spatial texture-filter library.
+ *
+ * This is the drop-in boundary for the hot path of yanielc/medical-vision-textural-bias:
+ * the filters of source_code/filters_and_operators.py and the in-model layers of
+ * source_code/stylization_layers.py, applied to batched [B][C][H][W][D] float32 volumes
+ * resident in HBM.  Plain C types only (no torch), caller-owned device memory,
+ * stream-ordered, no allocation or host synchronisation inside the launch functions
+ * (graph-capturable).  Every function returns TB_OK (0) or a TB_ERR_* code.
+ *
+ * Reference interfaces each entry point replaces (file:line under the reference root):
+ *   tb_kspace_filter_f32   Fourier.shift_fourier/inv_shift_fourier  filters_and_operators.py:594-632
+ *                          + the k-space body of RandFourierDiskMaskd.__call__         :236-252
+ *                          + RandPlaneWaves_ellipsoid.__call__                         :370-393
+ *                          + WrapArtifact.__call__                                     :503-515
+ *                          + GibbsNoise.__call__ / _apply_mask                         :663-705
+ *                          + KSpaceSpikeNoise.__call__ / _set_spike                    :906-983
+ *                          + GibbsNoiseLayer.forward / _apply_mask   stylization_layers.py:79-116
+ *                          (one fused forward-FFT -> op program -> inverse-FFT round trip)
+ *   tb_salt_pepper_f32     SaltAndPepper.salt_and_pepper             filters_and_operators.py:465-482
+ *   tb_minmax_f32          the x.max()/2, x.min()/2 of SaltAndPepper                   :476
+ *   tb_disk_mask_f32       disk_mask.binary_mask_2d / binary_mask_3d                   :136-197
+ *   tb_kspace_logabs_mean_f32  the default spike log-intensity 2.5*mean(log(|k|+1e-10)) :927-933, 1125-1131
+ */
+#ifndef TEXBIAS_H
+#define TEXBIAS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TB_VERSION 1
+
+/* error codes */
+#define TB_OK 0
+#define TB_ERR_INVALID_ARG 1
+#define TB_ERR_UNSUPPORTED_SIZE 2 /* an FFT length with a prime factor > 31, or a slab above LDS */
+#define TB_ERR_HIP 3              /* a HIP runtime call failed; tb_last_hip_error() has the code */
+#define TB_ERR_WORKSPACE 4        /* workspace smaller than tb_workspace_bytes() */
+
+/* k-space op kinds (applied in program order to every half-spectrum coefficient) */
+#define TB_OP_NONE 0
+#define TB_OP_DISK 1  /* i[0]=int radius?, i[1]=inside_off, f[0]=fl32(r*r) or l=r*r (int)     */
+#define TB_OP_GIBBS 2 /* l = integer threshold T4 on sum (2s-(n-1))^2 (float64 geometry)        */
+#define TB_OP_LAYER 3 /* f[0] = alpha * max_dist (float32 geometry of GibbsNoiseLayer)          */
+#define TB_OP_WRAP 4  /* f[0] = alpha                                                           */
+#define TB_OP_SPIKE 5 /* i[0..2] = UNSHIFTED (kh,kw,kd); f[0] = exp(log-intensity);
+                         f[1] = phase override or NaN (keep own phase); f[2],f[3] = cos,sin(f[1]);
+                         reserved = 1: same KSpaceSpikeNoise call as the previous SPIKE op (all
+                         spikes of one call read the spectrum from before the call)          */
+
+#define TB_MAX_OPS 6
+#define TB_MAX_BATCH 8 /* samples per launch group; larger batches are split by the library */
+
+typedef struct tb_op {
+  int32_t kind;
+  int32_t chan; /* channel selector, -1 = all channels */
+  int32_t i[3];
+  int32_t reserved;
+  int64_t l;
+  float f[4];
+} tb_op;
+
+typedef struct tb_sample_ops {
+  int32_t n; /* number of ops used */
+  int32_t reserved[3];
+  tb_op op[TB_MAX_OPS];
+} tb_sample_ops;
+
+/* transform geometry: spatial (H, W, D) after squeezing size-1 axes; D is contiguous */
+typedef struct tb_plan tb_plan;
+
+int tb_version(void);
+const char* tb_error_string(int code);
+int tb_last_hip_error(void);
+
+/* Device id of the calling thread's current HIP device is used for the plan tables. */
+int tb_plan_create(int H, int W, int D, tb_plan** out);
+int tb_plan_destroy(tb_plan* plan);
+/* Bytes of workspace needed for `bc` volume-channels (the half spectrum). */
+size_t tb_workspace_bytes(const tb_plan* plan, int bc);
+/* The FFT factorisation chosen for axis a (0=H,1=W,2=D): writes up to 8 radices, returns count. */
+int tb_plan_radices(const tb_plan* plan, int axis, int* radices);
+
+/*
+ * y = Re(IFFT( ops_b,c( FFT(x) ) ))  for every sample b < B and channel c < C.
+ *   x  : device, element (b,c,h,w,d) at x[(b*C+c)*xs[0] + h*xs[1] + w*xs[2] + d]
+ *   y  : device, same indexing with ys[]; d in [D, D+y_pad) is written with 0
+ *        (fuses the U-Net's D padding into the filter's store).  y may alias x.
+ *   ws : device workspace of >= tb_workspace_bytes(plan, B*C) bytes
+ *   ops: HOST array of B programs (copied into the launch arguments)
+ *   minmax: optional DEVICE uint32[B][2] receiving the order-preserving keys of the
+ *        per-sample min and max of y (the salt-and-pepper MIN/MAX), or NULL.
+ */
+int tb_kspace_filter_f32(const tb_plan* plan, const float* x, const int64_t* xs, float* y, const int64_t* ys,
+                         int y_pad, void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops,
+                         uint32_t* minmax, void* stream);
+
+/*
+ * Salt and pepper over B samples of `rows` rows of `len` floats (row pitch `ld`, sample pitch `sb`):
+ *   u = u_in[...] if u_in else Philox4x32-10(seed; counter = offset + b*rows*len + row*len + d)
+ *   cls = u <= thr[b][0] ? 1 (MIN) : u <= thr[b][1] ? 2 (MAX) : 0 (keep)
+ *   y = cls==1 ? min_b/2 : cls==2 ? max_b/2 : x     (min_b/max_b from minmax keys)
+ * When x == y only the changed voxels are stored.  cls (int8, same indexing as x) may be NULL.
+ * thr is a HOST float[B][2].
+ */
+int tb_salt_pepper_f32(const float* x, float* y, int8_t* cls, const float* u_in, uint64_t seed, uint64_t offset,
+                       const float* thr, const uint32_t* minmax, int B, int64_t rows, int len, int64_t ld,
+                       int64_t sb, void* stream);
+
+/* per-sample min/max keys of x (same row geometry as tb_salt_pepper_f32) into DEVICE uint32[B][2] */
+int tb_minmax_f32(const float* x, uint32_t* minmax, int B, int64_t rows, int len, int64_t ld, int64_t sb,
+                  void* stream);
+
+/* decode an order-preserving key back to float (host helper) */
+float tb_key_to_float(uint32_t key);
+
+/* float32 binary disk/sphere mask of disk_mask (dim = 2 or 3 trailing axes), written for
+ * `outer` repetitions of the n0 x n1 x n2 grid (n0 = 1 for dim 2).  int_r: compare in int64
+ * against r2i; else float32 against r2f. */
+int tb_disk_mask_f32(float* mask, int64_t outer, int n0, int n1, int n2, int int_r, int64_t r2i, float r2f,
+                     int inside_off, void* stream);
+
+/*
+ * out[bc] = sum over the FULL spectrum of log(|FFT(x)| + 1e-10) (float64 accumulation),
+ * after the first `n_pre` ops of each sample's program (the spike's own op excluded by the
+ * caller).  Used for KSpaceSpikeNoise's default intensity 2.5*mean(...).  out: DEVICE double[B*C].
+ */
+int tb_kspace_logabs_sum_f32(const tb_plan* plan, const float* x, const int64_t* xs, void* ws, size_t ws_bytes,
+                             int B, int C, const tb_sample_ops* ops, double* out, void* stream);
+
+/*
+ * Per-pass device timing for measurement: while enabled, every launch function records HIP
+ * events around each of its kernels on the caller's stream.  tb_get_pass_times_ms synchronises
+ * on them and returns the summed milliseconds per pass -- [0] slab forward (A), [1] k-space
+ * pencil pass (B), [2] slab inverse (C), [3] salt-and-pepper / minmax -- and the launch counts,
+ * then clears the record.  Disabled by default (no events, graph-capturable).
+ */
+int tb_set_pass_timing(int enable);
+int tb_get_pass_times_ms(float* ms_sum4, int* count4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TEXBIAS_H */

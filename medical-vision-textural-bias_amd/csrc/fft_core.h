@@ -1,0 +1,670 @@
+// fft_core.h -- the per-workgroup bodies of the texbias k-space filter passes.
+//
+// Shared by the gfx950 kernels (texbias.hip) and by the serial host emulator
+// used ONLY by the CPU test-suite (tests/emu/emu.cpp).  Every body is written
+// as barrier-separated phases; inside a phase the work items are independent
+// (each in-place butterfly owns its r LDS slots), so the emulator runs a block
+// with one "thread" and a no-op barrier and computes bit-for-bit the same
+// schedule of arithmetic per element.
+//
+// Reference being restated (file:line under /root/reference):
+//   Fourier.shift_fourier / inv_shift_fourier   source_code/filters_and_operators.py:594-632
+//   disk_mask                                    source_code/filters_and_operators.py:105-206
+//   RandPlaneWaves_ellipsoid                     source_code/filters_and_operators.py:370-414
+//   WrapArtifact                                 source_code/filters_and_operators.py:503-515
+//   GibbsNoise._apply_mask                       source_code/filters_and_operators.py:678-705
+//   KSpaceSpikeNoise                             source_code/filters_and_operators.py:906-983
+//   GibbsNoiseLayer._apply_mask                  source_code/stylization_layers.py:91-116
+//
+// Transform layout (DESIGN.md "Data layout in HBM"):
+//   image   x[bc][h][w][d]   float32, d contiguous (D = last spatial axis)
+//   spectrum S[bc][h][w'][kd] complex64, kd in [0, D/2]  (real-input half spectrum)
+//     h and w' are in DIGIT-REVERSED order (in-place mixed-radix DIF output);
+//     the inverse DIT consumes that order directly, so no permutation pass exists.
+#pragma once
+
+#include <stdint.h>
+#include "texbias.h"
+
+#if defined(__HIPCC__)
+#define TB_HD __host__ __device__ __forceinline__
+#else
+#define TB_HD inline
+#endif
+
+#define TB_MAX_STAGES 8
+
+namespace tb {
+
+struct alignas(8) cf {
+  float x, y;
+};
+
+// one FFT axis: length and its in-place DIF stage radices
+struct tb_axis {
+  int n, nst;
+  int radix[TB_MAX_STAGES];
+};
+
+// device-visible plan (passed by value in the launch arguments)
+struct tb_plan_dev {
+  int H, W, D, pad;
+  tb_axis ax[3];        // 0 = H, 1 = W, 2 = D
+  const cf* tw[3];      // tw[a][t] = exp(-2 pi i t / n_a)
+  const int* rev_d;     // D: frequency -> DIF slot
+  const int* irev_h;    // H: DIF slot -> frequency
+  const int* irev_w;    // W: DIF slot -> frequency
+};
+
+TB_HD cf mk(float a, float b) { cf r; r.x = a; r.y = b; return r; }
+TB_HD cf add(cf a, cf b) { return mk(a.x + b.x, a.y + b.y); }
+TB_HD cf sub(cf a, cf b) { return mk(a.x - b.x, a.y - b.y); }
+TB_HD cf mul(cf a, cf b) { return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+TB_HD cf mulc(cf a, cf b) { return mk(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y); }  // a * conj(b)
+TB_HD cf conj(cf a) { return mk(a.x, -a.y); }
+TB_HD cf scl(cf a, float s) { return mk(a.x * s, a.y * s); }
+// multiply by -i (forward) or +i (inverse)
+template <bool FWD> TB_HD cf rot90(cf a) { return FWD ? mk(a.y, -a.x) : mk(-a.y, a.x); }
+
+// ---------------------------------------------------------------- constants
+// constexpr trig (compile-time butterfly constants for the odd-prime radices)
+constexpr double kPi = 3.14159265358979323846264338327950288;
+constexpr double csin_series(double x) {
+  double term = x, sum = x;
+  for (int i = 1; i < 30; ++i) { term *= -x * x / ((2 * i) * (2 * i + 1)); sum += term; }
+  return sum;
+}
+constexpr double cred(double x) {  // reduce to [-pi, pi]
+  while (x > kPi) x -= 2 * kPi;
+  while (x < -kPi) x += 2 * kPi;
+  return x;
+}
+constexpr double csin(double x) { return csin_series(cred(x)); }
+constexpr double ccos(double x) { return csin(x + kPi / 2); }
+// cos/sin(2 pi m / R) as a constexpr table: indexed with unrolled (constant) m the values
+// fold into literals -- a direct constexpr call is NOT folded by hipcc for large R.
+template <int R> struct TrigTab {
+  float c[R], s[R];
+  constexpr TrigTab() : c(), s() {
+    for (int m = 0; m < R; ++m) {
+      c[m] = (float)ccos(2.0 * kPi * m / R);
+      s[m] = (float)csin(2.0 * kPi * m / R);
+    }
+  }
+};
+template <int R> struct Trig { static constexpr TrigTab<R> tab{}; };
+
+// ------------------------------------------------------------- small DFTs
+// In-register DFT of size R.  FWD: X[k] = sum_p a[p] e^{-2 pi i pk/R};
+// inverse (unnormalised) uses e^{+...}.
+template <int R, bool FWD> struct Dft;
+
+template <bool FWD> struct Dft<2, FWD> {
+  TB_HD static void run(cf* a) { cf t = a[1]; a[1] = sub(a[0], t); a[0] = add(a[0], t); }
+};
+
+template <bool FWD> struct Dft<3, FWD> {
+  TB_HD static void run(cf* a) {
+    const float c = -0.5f, s = 0.86602540378443864676f;
+    cf t1 = add(a[1], a[2]), t2 = sub(a[1], a[2]);
+    cf m = add(a[0], scl(t1, c));
+    cf r = rot90<FWD>(scl(t2, s));  // -i*s*(a1-a2) forward
+    a[0] = add(a[0], t1);
+    a[1] = add(m, r);
+    a[2] = sub(m, r);
+  }
+};
+
+template <bool FWD> struct Dft<4, FWD> {
+  TB_HD static void run(cf* a) {
+    cf t0 = add(a[0], a[2]), t1 = sub(a[0], a[2]);
+    cf t2 = add(a[1], a[3]), t3 = rot90<FWD>(sub(a[1], a[3]));
+    a[0] = add(t0, t2);
+    a[2] = sub(t0, t2);
+    a[1] = add(t1, t3);
+    a[3] = sub(t1, t3);
+  }
+};
+
+// generic odd prime: conjugate-pair symmetric direct DFT (R-1)^2/4 complex*real pairs
+template <int R, bool FWD> struct DftOdd {
+  TB_HD static void run(cf* a) {
+    constexpr int M = (R - 1) / 2;
+    cf s[M + 1], d[M + 1];
+    cf y0 = a[0];
+#pragma unroll
+    for (int p = 1; p <= M; ++p) {
+      s[p] = add(a[p], a[R - p]);
+      d[p] = sub(a[p], a[R - p]);
+      y0 = add(y0, s[p]);
+    }
+    cf out[R];
+    out[0] = y0;
+#pragma unroll
+    for (int k = 1; k <= M; ++k) {
+      cf A = a[0], B = mk(0.f, 0.f);
+#pragma unroll
+      for (int p = 1; p <= M; ++p) {
+        const int m = (p * k) % R;
+        const float c = Trig<R>::tab.c[m];
+        const float sn = Trig<R>::tab.s[m];
+        A.x += s[p].x * c; A.y += s[p].y * c;
+        B.x += d[p].x * sn; B.y += d[p].y * sn;
+      }
+      // forward: y[k] = A - i B, y[R-k] = A + i B ; inverse: swapped
+      cf iB = mk(-B.y, B.x);
+      out[k] = FWD ? sub(A, iB) : add(A, iB);
+      out[R - k] = FWD ? add(A, iB) : sub(A, iB);
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) a[k] = out[k];
+  }
+};
+template <bool FWD> struct Dft<5, FWD> : DftOdd<5, FWD> {};
+template <bool FWD> struct Dft<7, FWD> : DftOdd<7, FWD> {};
+template <bool FWD> struct Dft<11, FWD> : DftOdd<11, FWD> {};
+template <bool FWD> struct Dft<13, FWD> : DftOdd<13, FWD> {};
+template <bool FWD> struct Dft<17, FWD> : DftOdd<17, FWD> {};
+template <bool FWD> struct Dft<19, FWD> : DftOdd<19, FWD> {};
+template <bool FWD> struct Dft<23, FWD> : DftOdd<23, FWD> {};
+template <bool FWD> struct Dft<29, FWD> : DftOdd<29, FWD> {};
+template <bool FWD> struct Dft<31, FWD> : DftOdd<31, FWD> {};
+
+// composite R = R1*R2 in registers (Cooley-Tukey, constant twiddles):
+// a[n1 + R1*n2] -> X[k2 + R2*k1]
+template <int R1, int R2, bool FWD> struct DftComp {
+  TB_HD static void run(cf* a) {
+    constexpr int R = R1 * R2;
+    cf t[R];
+    // R1 DFTs of size R2 over n2 for each n1
+#pragma unroll
+    for (int n1 = 0; n1 < R1; ++n1) {
+      cf v[R2];
+#pragma unroll
+      for (int n2 = 0; n2 < R2; ++n2) v[n2] = a[n1 + R1 * n2];
+      Dft<R2, FWD>::run(v);
+#pragma unroll
+      for (int k2 = 0; k2 < R2; ++k2) {
+        const int m = (n1 * k2) % R;
+        if (m == 0) {
+          t[n1 + R1 * k2] = v[k2];
+        } else {
+          const float c = Trig<R>::tab.c[m];
+          const float sn = FWD ? -Trig<R>::tab.s[m] : Trig<R>::tab.s[m];
+          t[n1 + R1 * k2] = mul(v[k2], mk(c, sn));
+        }
+      }
+    }
+    // R2 DFTs of size R1 over n1 for each k2
+#pragma unroll
+    for (int k2 = 0; k2 < R2; ++k2) {
+      cf v[R1];
+#pragma unroll
+      for (int n1 = 0; n1 < R1; ++n1) v[n1] = t[n1 + R1 * k2];
+      Dft<R1, FWD>::run(v);
+#pragma unroll
+      for (int k1 = 0; k1 < R1; ++k1) a[k2 + R2 * k1] = v[k1];
+    }
+  }
+};
+template <bool FWD> struct Dft<8, FWD> : DftComp<2, 4, FWD> {};
+template <bool FWD> struct Dft<16, FWD> : DftComp<4, 4, FWD> {};
+template <bool FWD> struct Dft<6, FWD> : DftComp<2, 3, FWD> {};
+template <bool FWD> struct Dft<9, FWD> : DftComp<3, 3, FWD> {};
+template <bool FWD> struct Dft<10, FWD> : DftComp<2, 5, FWD> {};
+template <bool FWD> struct Dft<12, FWD> : DftComp<4, 3, FWD> {};
+template <bool FWD> struct Dft<15, FWD> : DftComp<3, 5, FWD> {};
+
+// ------------------------------------------------------------ addressing
+// A pencil's element i lives at lds[base + (i>>1)*pitch + (i&1)*odd] when
+// "paired", else lds[base + i*stride].  One form covers all passes.
+struct Pencil {
+  int base, pitch, odd;  // paired form
+};
+
+// ------------------------------------------------------ in-place stages
+// Mixed-radix in-place DIF (Sande-Tukey).  Stage s (radix r, block length Lb,
+// P = n/Lb = product of previous radices, L = Lb/r):
+//   butterfly (blk, j): positions blk*Lb + j + q*L, q < r
+//   y = DFT_r(x);  y[q] *= w_n^{j*q*P}
+// After all stages position  sum_s q_s * L_s  holds X[q_1 + r_1 (q_2 + r_2 (...))].
+// The inverse DIT runs the stages in reverse order with conj twiddles first.
+template <class Ctx, int R, bool FWD, class AddrF>
+TB_HD void stage_r(Ctx& ctx, cf* lds, const cf* tw, int Lb, int P, int npen, int nb, AddrF addr,
+                   bool pencil_fast) {
+  const int L = Lb / R;
+  const int total = npen * nb;
+  for (int t = ctx.tid; t < total; t += ctx.nthreads) {
+    int p, u;
+    if (pencil_fast) { u = t / npen; p = t - u * npen; }
+    else { p = t / nb; u = t - p * nb; }
+    const int blk = u / L, j = u - blk * L;
+    const int base = blk * Lb + j;
+    cf a[R];
+    int ad[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) { ad[q] = addr(p, base + q * L); a[q] = lds[ad[q]]; }
+    if (FWD) {
+      Dft<R, true>::run(a);
+      if (j) {
+#pragma unroll
+        for (int q = 1; q < R; ++q) a[q] = mul(a[q], tw[j * q * P]);
+      }
+    } else {
+      if (j) {
+#pragma unroll
+        for (int q = 1; q < R; ++q) a[q] = mulc(a[q], tw[j * q * P]);
+      }
+      Dft<R, false>::run(a);
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) lds[ad[q]] = a[q];
+  }
+}
+
+// Radix sets compiled into a kernel: RS 0 = {2..10, 12, 15, 16} (small register
+// footprint), RS 1 adds the primes 11..31 (needed e.g. for D = 155 = 5 * 31).
+template <class Ctx, bool FWD, int RS, class AddrF>
+TB_HD void stage(Ctx& ctx, cf* lds, const cf* tw, int r, int Lb, int P, int npen, int n, AddrF addr,
+                 bool pencil_fast) {
+  const int nb = n / r;
+  switch (r) {
+#define TB_CASE(R) case R: stage_r<Ctx, R, FWD>(ctx, lds, tw, Lb, P, npen, nb, addr, pencil_fast); break;
+    TB_CASE(2) TB_CASE(3) TB_CASE(4) TB_CASE(5) TB_CASE(6) TB_CASE(7) TB_CASE(8) TB_CASE(9)
+    TB_CASE(10) TB_CASE(12) TB_CASE(15) TB_CASE(16)
+    default:
+      if constexpr (RS == 1) {
+        switch (r) {
+          TB_CASE(11) TB_CASE(13) TB_CASE(17) TB_CASE(19) TB_CASE(23) TB_CASE(29) TB_CASE(31)
+          default: break;
+        }
+      }
+      break;  // anything else is rejected at plan time
+#undef TB_CASE
+  }
+}
+
+// forward DIF over all stages (natural in -> digit-reversed out)
+template <class Ctx, int RS, class AddrF>
+TB_HD void fft_dif(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen, AddrF addr, bool pencil_fast) {
+  int P = 1;
+  for (int s = 0; s < ax.nst; ++s) {
+    const int r = ax.radix[s];
+    const int Lb = ax.n / P;
+    stage<Ctx, true, RS>(ctx, lds, tw, r, Lb, P, npen, ax.n, addr, pencil_fast);
+    ctx.sync();
+    P *= r;
+  }
+}
+
+// inverse DIT over all stages (digit-reversed in -> natural out), unnormalised
+template <class Ctx, int RS, class AddrF>
+TB_HD void fft_dit(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen, AddrF addr, bool pencil_fast) {
+  int P = ax.n;
+  for (int s = ax.nst - 1; s >= 0; --s) {
+    const int r = ax.radix[s];
+    P /= r;
+    const int Lb = ax.n / P;
+    stage<Ctx, false, RS>(ctx, lds, tw, r, Lb, P, npen, ax.n, addr, pencil_fast);
+    ctx.sync();
+  }
+}
+
+// ------------------------------------------------------------- k-space ops
+// Frequency bookkeeping per axis: unshifted index k in [0,n); the reference's
+// fftshift-ed index is s = (k + n/2) mod n (n/2 floored).
+TB_HD int shifted(int k, int n) { int s = k + n / 2; return s >= n ? s - n : s; }
+TB_HD int negk(int k, int n) { return k == 0 ? 0 : n - k; }
+
+// disk_mask (filters_and_operators.py:176-195): centre floor(n/2) of the shifted grid = DC;
+// integer sum of squares compared strictly (< r^2) in float32, or in int64 for an int r.
+TB_HD float disk_value(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
+  const int64_t dh = shifted(kh, H) - H / 2, dw = shifted(kw, W) - W / 2, dd = shifted(kd, D) - D / 2;
+  const int64_t s = dh * dh + dw * dw + dd * dd;
+  bool in;
+  if (op.i[0]) in = s < op.l;               // int radius: exact integer compare
+  else in = (float)s < op.f[0];             // float radius: float32 compare (s < 2^24 exact)
+  if (op.i[1]) in = !in;                    // inside_off
+  return in ? 1.f : 0.f;
+}
+
+// GibbsNoise mask (filters_and_operators.py:686-698): float64 geometry, centre (n-1)/2,
+// dist <= r.  4*(s-c)^2 = (2s-(n-1))^2 is an exact integer; the host turns
+// fl64(sqrt(t/4)) <= r into the integer threshold t <= T4 (op.l).
+TB_HD bool gibbs_in(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
+  const int64_t eh = 2 * shifted(kh, H) - (H - 1), ew = 2 * shifted(kw, W) - (W - 1),
+                ed = 2 * shifted(kd, D) - (D - 1);
+  return eh * eh + ew * ew + ed * ed <= op.l;
+}
+
+// GibbsNoiseLayer mask (stylization_layers.py:99-109): float32 geometry, centre (n-1)/2,
+// norm_dist = dist / (alpha * max dist); mask = !(norm_dist > 1)  (NaN -> 1, inf -> 0)
+// correctly rounded IEEE float32 division / square root (bit-exact mask geometry)
+TB_HD float f32_div(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __fdiv_rn(a, b);
+#else
+  return a / b;
+#endif
+}
+TB_HD float f32_sqrt(float a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __fsqrt_rn(a);
+#else
+  return __builtin_sqrtf(a);
+#endif
+}
+TB_HD bool layer_in(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
+  const float eh = (float)shifted(kh, H) - (float)(H - 1) * 0.5f;
+  const float ew = (float)shifted(kw, W) - (float)(W - 1) * 0.5f;
+  const float ed = (float)shifted(kd, D) - (float)(D - 1) * 0.5f;
+  const float d2 = (eh * eh + ew * ew) + ed * ed;   // exact: quarter-integers < 2^22
+  const float nd = f32_div(f32_sqrt(d2), op.f[0]);
+  return !(nd > 1.f);
+}
+
+// wrap (filters_and_operators.py:509-511): alpha per axis whose shifted index is odd
+TB_HD float wrap_value(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
+  float m = 1.f;
+  if (shifted(kh, H) & 1) m *= op.f[0];
+  if (shifted(kw, W) & 1) m *= op.f[0];
+  if (shifted(kd, D) & 1) m *= op.f[0];
+  return m;
+}
+
+// The target value of a spike: |k| := amp (= exp(intensity)), phase kept
+// (filters_and_operators.py:383-390, 927-942) or overridden (parity hook).
+TB_HD cf spike_target(const tb_op& op, cf kf) {
+  float ph = op.f[1];
+  if (ph != ph) {  // NaN -> keep the coefficient's own phase (angle(0) = 0)
+    const float m2 = kf.x * kf.x + kf.y * kf.y;
+    if (m2 > 0.f) {
+      const float inv = 1.f / f32_sqrt(m2);
+      return mk(op.f[0] * kf.x * inv, op.f[0] * kf.y * inv);
+    }
+    return mk(op.f[0], 0.f);
+  }
+  return mk(op.f[0] * op.f[2], op.f[0] * op.f[3]);  // host passes cos/sin of the override
+}
+
+// Apply a sample's op program to one stored half-spectrum coefficient.
+// Every op is followed by the reference's `.real` (G4: Hermitian symmetrisation);
+// on a half spectrum that is exact for symmetric masks, needs (M(f)+M(-f))/2 for
+// the off-centre Gibbs masks, and splits a spike into +Delta/2 at f and
+// +conj(Delta)/2 at -f.  Consecutive SPIKE ops flagged `reserved = 1` belong to one
+// KSpaceSpikeNoise call: they are all measured against the spectrum BEFORE the group
+// (the reference writes every location into one log-amplitude array, :936-942).
+TB_HD cf apply_ops(const tb_sample_ops& so, int chan, cf v, int kh, int kw, int kd, int H, int W, int D) {
+  const int nkh = negk(kh, H), nkw = negk(kw, W), nkd = negk(kd, D);
+  cf gbase = v;
+  bool in_group = false;
+  for (int o = 0; o < so.n; ++o) {
+    const tb_op& op = so.op[o];
+    if (op.kind == TB_OP_SPIKE) {
+      if (!in_group || op.reserved != 1) gbase = v;
+      in_group = true;
+    } else {
+      in_group = false;
+    }
+    if (op.chan >= 0 && op.chan != chan) continue;
+    switch (op.kind) {
+      case TB_OP_DISK:
+        v = scl(v, disk_value(op, kh, kw, kd, H, W, D));
+        break;
+      case TB_OP_GIBBS: {
+        const float m = 0.5f * ((gibbs_in(op, kh, kw, kd, H, W, D) ? 1.f : 0.f) +
+                                (gibbs_in(op, nkh, nkw, nkd, H, W, D) ? 1.f : 0.f));
+        v = scl(v, m);
+      } break;
+      case TB_OP_LAYER: {
+        const float m = 0.5f * ((layer_in(op, kh, kw, kd, H, W, D) ? 1.f : 0.f) +
+                                (layer_in(op, nkh, nkw, nkd, H, W, D) ? 1.f : 0.f));
+        v = scl(v, m);
+      } break;
+      case TB_OP_WRAP:
+        v = scl(v, wrap_value(op, kh, kw, kd, H, W, D));
+        break;
+      case TB_OP_SPIKE: {
+        if (kh == op.i[0] && kw == op.i[1] && kd == op.i[2]) {        // this coefficient is f
+          const cf d = sub(spike_target(op, gbase), gbase);
+          v = add(v, scl(d, 0.5f));
+        }
+        if (nkh == op.i[0] && nkw == op.i[1] && nkd == op.i[2]) {     // this coefficient is -f
+          const cf kf = conj(gbase);
+          const cf d = sub(spike_target(op, kf), kf);
+          v = add(v, scl(conj(d), 0.5f));
+        }
+      } break;
+      default: break;
+    }
+  }
+  return v;
+}
+
+// ---------------------------------------------------------- pass geometry
+// LDS carve of the slab passes (A forward, C inverse), in cf units:
+//   [0, NP*PR)          pair rows: z = x[2p] + i x[2p+1], D slots each
+//   C0 [W], CN [W]      the real-valued kd=0 / kd=D/2 columns
+//   twW [W], twD [D]    twiddle tables
+//   posA, posB [Dh]     int: digit-reversed slots of k and D-k
+struct SlabGeo {
+  int NP, PR, off_c0, off_cn, off_tww, off_twd, off_pos, total_cf;
+};
+
+TB_HD SlabGeo slab_geo(int W, int D) {
+  SlabGeo g;
+  g.NP = (W + 1) / 2;
+  g.PR = D;
+  g.off_c0 = g.NP * g.PR;
+  g.off_cn = g.off_c0 + W;
+  g.off_tww = g.off_cn + ((D % 2 == 0) ? W : 0);
+  g.off_twd = g.off_tww + W;
+  g.off_pos = g.off_twd + D;
+  const int Dh = D / 2 + 1;
+  g.total_cf = g.off_pos + (2 * Dh + 1) / 2 + 1;  // ints packed two per cf
+  return g;
+}
+
+// pass B carve: tile [H][T] + twH[H] + irevH[H] (ints)
+struct TileGeo {
+  int T, off_tw, off_irev, total_cf;
+};
+TB_HD TileGeo tile_geo(int H, int T) {
+  TileGeo g;
+  g.T = T;
+  g.off_tw = H * T;
+  g.off_irev = g.off_tw + H;
+  g.total_cf = g.off_irev + (H + 1) / 2 + 1;
+  return g;
+}
+
+// column addressing of the W-axis FFT inside the slab
+struct ColAddr {
+  const int* posA;
+  const int* posB;
+  int PR, off_c0, off_cn, Dn, D;  // Dn = D/2 if D even else -1
+  TB_HD int base(int kd) const { return kd == 0 ? off_c0 : (kd == Dn ? off_cn : posA[kd]); }
+  TB_HD int operator()(int kd, int w) const {
+    if (kd == 0) return off_c0 + w;
+    if (kd == Dn) return off_cn + w;
+    return (w >> 1) * PR + ((w & 1) ? posB[kd] : posA[kd]);
+  }
+};
+struct RowAddr {  // pair pencils along D
+  int PR;
+  TB_HD int operator()(int p, int d) const { return p * PR + d; }
+};
+struct TileAddr {  // H pencils of the pass-B tile
+  int T;
+  TB_HD int operator()(int c, int h) const { return h * T + c; }
+};
+
+// --------------------------------------------------------------- pass A
+// forward: real slab x[bc][h][:][:] -> half spectrum S[bc][h][w'][kd]
+template <class Ctx, int RS>
+TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __restrict__ x, int64_t sx_bc,
+                       int64_t sx_h, int64_t sx_w, cf* __restrict__ S, int bc, int h) {
+  const int W = pl.W, D = pl.D, Dh = D / 2 + 1;
+  const SlabGeo g = slab_geo(W, D);
+  cf* tww = lds + g.off_tww;
+  cf* twd = lds + g.off_twd;
+  int* pos = reinterpret_cast<int*>(lds + g.off_pos);
+  int* posA = pos;
+  int* posB = pos + Dh;
+  for (int i = ctx.tid; i < W; i += ctx.nthreads) tww[i] = pl.tw[1][i];
+  for (int i = ctx.tid; i < D; i += ctx.nthreads) twd[i] = pl.tw[2][i];
+  for (int i = ctx.tid; i < Dh; i += ctx.nthreads) {
+    posA[i] = pl.rev_d[i];
+    posB[i] = pl.rev_d[i == 0 ? 0 : D - i];
+  }
+  // load pair rows
+  const float* xb = x + bc * sx_bc + h * sx_h;
+  const int nload = g.NP * D;
+  for (int t = ctx.tid; t < nload; t += ctx.nthreads) {
+    const int p = t / D, d = t - p * D;
+    const int w0 = 2 * p;
+    const float a = xb[w0 * sx_w + d];
+    const float b = (w0 + 1 < W) ? xb[(w0 + 1) * sx_w + d] : 0.f;
+    lds[p * g.PR + d] = mk(a, b);
+  }
+  ctx.sync();
+  fft_dif<Ctx, RS>(ctx, lds, twd, pl.ax[2], g.NP, RowAddr{g.PR}, false);
+  // unpack the pair spectra in place (each unit owns the two slots it reads)
+  const int Dn = (D % 2 == 0) ? D / 2 : -1;
+  const int nun = g.NP * Dh;
+  for (int t = ctx.tid; t < nun; t += ctx.nthreads) {
+    const int p = t / Dh, k = t - p * Dh;
+    cf* row = lds + p * g.PR;
+    const int w0 = 2 * p;
+    if (k == 0 || k == Dn) {
+      const cf z = row[posA[k]];
+      cf* col = lds + (k == 0 ? g.off_c0 : g.off_cn);
+      col[w0] = mk(z.x, 0.f);
+      if (w0 + 1 < W) col[w0 + 1] = mk(z.y, 0.f);
+    } else {
+      const cf zk = row[posA[k]], zm = conj(row[posB[k]]);
+      const cf xa = scl(add(zk, zm), 0.5f);
+      const cf dd = scl(sub(zk, zm), 0.5f);
+      row[posA[k]] = xa;
+      row[posB[k]] = mk(dd.y, -dd.x);  // (zk - zm) / (2i)
+    }
+  }
+  ctx.sync();
+  ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
+  fft_dif<Ctx, RS>(ctx, lds, tww, pl.ax[1], Dh, ca, true);
+  // store S[bc][h][w'*Dh + kd]
+  cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
+  const int nst = W * Dh;
+  for (int t = ctx.tid; t < nst; t += ctx.nthreads) {
+    const int w = t / Dh, kd = t - w * Dh;
+    Sb[t] = lds[ca(kd, w)];
+  }
+}
+
+// --------------------------------------------------------------- pass B
+template <class Ctx, int RS>
+TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict__ S, int bc, int tile, int T,
+                       const tb_sample_ops& so, int chan) {
+  const int H = pl.H, W = pl.W, D = pl.D, Dh = D / 2 + 1;
+  const int ncols_all = W * Dh;
+  const int j0 = tile * T;
+  const int nc = (ncols_all - j0) < T ? (ncols_all - j0) : T;
+  const TileGeo g = tile_geo(H, T);
+  cf* tw = lds + g.off_tw;
+  int* irev = reinterpret_cast<int*>(lds + g.off_irev);
+  for (int i = ctx.tid; i < H; i += ctx.nthreads) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
+  cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
+  const int nl = H * nc;
+  for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
+    const int hh = t / nc, c = t - hh * nc;
+    lds[hh * T + c] = Sb[(int64_t)hh * ncols_all + c];
+  }
+  ctx.sync();
+  const TileAddr ta{T};
+  fft_dif<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
+  for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
+    const int hp = t / nc, c = t - hp * nc;
+    const int j = j0 + c;
+    const int wp = j / Dh, kd = j - wp * Dh;
+    const int kh = irev[hp], kw = pl.irev_w[wp];
+    cf& v = lds[hp * T + c];
+    v = apply_ops(so, chan, v, kh, kw, kd, H, W, D);
+  }
+  ctx.sync();
+  fft_dit<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
+  for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
+    const int hh = t / nc, c = t - hh * nc;
+    Sb[(int64_t)hh * ncols_all + c] = lds[hh * T + c];
+  }
+}
+
+// --------------------------------------------------------------- pass C
+// inverse: S[bc][h] -> y[bc][h][:][:] (scaled 1/N), pad columns [D, ldy) zeroed,
+// optional running (min, max) of the written values for salt-and-pepper.
+template <class Ctx, int RS>
+TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __restrict__ S, float* __restrict__ y,
+                       int64_t sy_bc, int64_t sy_h, int64_t sy_w, int ldy_pad, int bc, int h, float scale,
+                       float* vmin, float* vmax) {
+  const int W = pl.W, D = pl.D, Dh = D / 2 + 1;
+  const SlabGeo g = slab_geo(W, D);
+  cf* tww = lds + g.off_tww;
+  cf* twd = lds + g.off_twd;
+  int* pos = reinterpret_cast<int*>(lds + g.off_pos);
+  int* posA = pos;
+  int* posB = pos + Dh;
+  for (int i = ctx.tid; i < W; i += ctx.nthreads) tww[i] = pl.tw[1][i];
+  for (int i = ctx.tid; i < D; i += ctx.nthreads) twd[i] = pl.tw[2][i];
+  for (int i = ctx.tid; i < Dh; i += ctx.nthreads) {
+    posA[i] = pl.rev_d[i];
+    posB[i] = pl.rev_d[i == 0 ? 0 : D - i];
+  }
+  ctx.sync();
+  const int Dn = (D % 2 == 0) ? D / 2 : -1;
+  ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
+  const cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
+  const int nst = W * Dh;
+  for (int t = ctx.tid; t < nst; t += ctx.nthreads) {
+    const int w = t / Dh, kd = t - w * Dh;
+    lds[ca(kd, w)] = Sb[t];
+  }
+  ctx.sync();
+  fft_dit<Ctx, RS>(ctx, lds, tww, pl.ax[1], Dh, ca, true);
+  // repack rows (2p, 2p+1) into the pair spectrum z = X_a + i X_b (digit-reversed slots)
+  const int nun = g.NP * Dh;
+  for (int t = ctx.tid; t < nun; t += ctx.nthreads) {
+    const int p = t / Dh, k = t - p * Dh;
+    cf* row = lds + p * g.PR;
+    const int w0 = 2 * p;
+    const bool has_b = (w0 + 1 < W);
+    if (k == 0 || k == Dn) {
+      const cf* col = lds + (k == 0 ? g.off_c0 : g.off_cn);
+      row[posA[k]] = mk(col[w0].x, has_b ? col[w0 + 1].x : 0.f);   // c2r keeps Re of DC/Nyquist
+    } else {
+      const cf xa = row[posA[k]];
+      const cf xb = has_b ? row[posB[k]] : mk(0.f, 0.f);
+      row[posA[k]] = mk(xa.x - xb.y, xa.y + xb.x);         // xa + i xb
+      row[posB[k]] = mk(xa.x + xb.y, -xa.y + xb.x);        // conj(xa) + i conj(xb)
+    }
+  }
+  ctx.sync();
+  fft_dit<Ctx, RS>(ctx, lds, twd, pl.ax[2], g.NP, RowAddr{g.PR}, false);
+  float* yb = y + bc * sy_bc + h * sy_h;
+  const int ldw = D + ldy_pad;
+  const int nout = W * ldw;
+  float lo = 3.402823466e38f, hi = -3.402823466e38f;
+  for (int t = ctx.tid; t < nout; t += ctx.nthreads) {
+    const int w = t / ldw, d = t - w * ldw;
+    float v = 0.f;
+    if (d < D) {
+      const cf z = lds[(w >> 1) * g.PR + d];
+      v = ((w & 1) ? z.y : z.x) * scale;
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
+    yb[w * sy_w + d] = v;
+  }
+  *vmin = lo;
+  *vmax = hi;
+}
+
+}  // namespace tb

@@ -1,0 +1,604 @@
+// texbias.hip -- gfx950 kernels and the C ABI (include/texbias.h) of the texbias library.
+//
+// Pass plan of one k-space filter call (DESIGN.md "Kernels"):
+//   A  k_slab_fwd   per (bc, h) slab: real rows -> pair-packed R2C along D -> C2C along W,
+//                   in one 150 KB LDS slab; stores the half spectrum (digit-reversed W).
+//   B  k_kspace     per (bc, tile of T spectrum columns): C2C along H (DIF), the sample's
+//                   op program on every coefficient, inverse along H (DIT).
+//   C  k_slab_inv   per (bc, h) slab: inverse W, C2R along D, scale 1/N, zero D-padding,
+//                   per-sample min/max epilogue.
+//   D  k_salt_pepper  Philox u, class, sparse in-place MIN/MAX scatter.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "fft_core.h"
+#include "plan_host.h"
+#include "sap_core.h"
+
+using namespace tb;
+
+namespace {
+
+struct DevCtx {
+  int tid, nthreads;
+  __device__ __forceinline__ void sync() { __syncthreads(); }
+};
+
+enum { RS_SMALL = 0, RS_ALL = 1 };
+
+struct BatchOps {
+  tb_sample_ops s[TB_MAX_BATCH];
+};
+
+thread_local int g_last_hip = 0;
+
+inline int hip_fail(hipError_t e) {
+  g_last_hip = (int)e;
+  return TB_ERR_HIP;
+}
+#define TB_HIP(call)                              \
+  do {                                            \
+    hipError_t e_ = (call);                       \
+    if (e_ != hipSuccess) return hip_fail(e_);    \
+  } while (0)
+
+// ------------------------------------------------------------------ timing
+struct TimingRec {
+  hipEvent_t a, b;
+  int slot;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimingRec> g_recs;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t ev_get() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+struct Timer {  // records [begin, end) of one pass when timing is enabled
+  hipEvent_t a = nullptr, b = nullptr;
+  int slot;
+  hipStream_t st;
+  Timer(int s, hipStream_t stream) : slot(s), st(stream) {
+    if (!g_timing) return;
+    std::lock_guard<std::mutex> lk(g_tmu);
+    a = ev_get();
+    b = ev_get();
+    if (a) hipEventRecord(a, st);
+  }
+  ~Timer() {
+    if (!a || !b) return;
+    hipEventRecord(b, st);
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_recs.push_back({a, b, slot});
+  }
+};
+
+// ---------------------------------------------------------------- kernels
+template <int NT, int RS>
+__global__ __launch_bounds__(NT) void k_slab_fwd(tb_plan_dev pl, const float* __restrict__ x, int64_t sbc,
+                                                 int64_t sh, int64_t sw, cf* __restrict__ S, int bc0) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  DevCtx ctx{(int)threadIdx.x, NT};
+  pass_a_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), pl, x, sbc, sh, sw, S, bc0 + (int)blockIdx.y, (int)blockIdx.x);
+}
+
+template <int NT, int RS>
+__global__ __launch_bounds__(NT) void k_kspace(tb_plan_dev pl, cf* __restrict__ S, int bc0, int C, int T,
+                                               BatchOps ops) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  DevCtx ctx{(int)threadIdx.x, NT};
+  const int bcl = (int)blockIdx.y;
+  pass_b_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), pl, S, bc0 + bcl, (int)blockIdx.x, T, ops.s[bcl / C], bcl % C);
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block min/max -> atomic keys (uses the first 2*NT/64 floats of smem after a barrier)
+template <int NT>
+__device__ __forceinline__ void block_minmax_atomic(float lo, float hi, float* red, uint32_t* mm) {
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    red[wid] = lo;
+    red[NT / 64 + wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < NT / 64; ++w) {
+      lo = fminf(lo, red[w]);
+      hi = fmaxf(hi, red[NT / 64 + w]);
+    }
+    atomicMin(&mm[0], f2key(lo));
+    atomicMax(&mm[1], f2key(hi));
+  }
+}
+
+template <int NT, int RS>
+__global__ __launch_bounds__(NT) void k_slab_inv(tb_plan_dev pl, const cf* __restrict__ S, float* __restrict__ y,
+                                                 int64_t sbc, int64_t sh, int64_t sw, int ypad, int bc0, int C,
+                                                 float scale, uint32_t* __restrict__ mm) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  DevCtx ctx{(int)threadIdx.x, NT};
+  const int bc = bc0 + (int)blockIdx.y;
+  float lo, hi;
+  pass_c_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), pl, S, y, sbc, sh, sw, ypad, bc, (int)blockIdx.x, scale, &lo, &hi);
+  if (mm) block_minmax_atomic<NT>(lo, hi, reinterpret_cast<float*>(smem), mm + 2 * (bc / C));
+}
+
+__global__ void k_minmax_init(uint32_t* mm, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    mm[2 * i] = 0xffffffffu;
+    mm[2 * i + 1] = 0u;
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_minmax(const float* __restrict__ x, uint32_t* __restrict__ mm, int64_t rows,
+                                               int len, int64_t ld, int64_t sb) {
+  __shared__ float red[2 * NT / 64];
+  const int b = blockIdx.y;
+  const float* xb = x + b * sb;
+  const int64_t n = rows * len;
+  float lo = 3.402823466e38f, hi = -3.402823466e38f;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int64_t r = i / len;
+    const float v = xb[r * ld + (i - r * len)];
+    lo = fminf(lo, v);
+    hi = fmaxf(hi, v);
+  }
+  block_minmax_atomic<NT>(lo, hi, red, mm + 2 * b);
+}
+
+struct SapThr {
+  float lo[TB_MAX_BATCH], hi[TB_MAX_BATCH];
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_salt_pepper(const float* __restrict__ x, float* __restrict__ y,
+                                                    int8_t* __restrict__ cls, const float* __restrict__ uin,
+                                                    uint64_t seed, uint64_t offset, SapThr thr,
+                                                    const uint32_t* __restrict__ mm, int b0, int64_t rows, int len,
+                                                    int64_t ld, int64_t sb, int sparse) {
+  const int bl = blockIdx.y;
+  const int b = b0 + bl;
+  const int64_t n = rows * len;
+  const float vmin = key2f(mm[2 * b]) * 0.5f, vmax = key2f(mm[2 * b + 1]) * 0.5f;
+  const float lo = thr.lo[bl], hi = thr.hi[bl];
+  const int64_t lin0 = (int64_t)b * n;  // logical (unpadded) voxel index of this sample
+  const int64_t ngroups = (n + 3) / 4;
+  for (int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x; g < ngroups; g += (int64_t)gridDim.x * NT) {
+    u32x4 r;
+    if (!uin) r = philox((uint64_t)(lin0 / 4 + g), offset, seed);  // n % 4 handled below
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i = 4 * g + q;
+      if (i >= n) break;
+      const int64_t row = i / len;
+      const int64_t off = b * sb + row * ld + (i - row * len);
+      float u;
+      if (uin) u = uin[off];
+      else {
+        // counter of logical voxel L = lin0 + i: the group index and lane of L itself, so the
+        // stream is independent of how samples are batched when n % 4 == 0 (the usual case)
+        if ((lin0 & 3) == 0) u = u01(r.v[q]);
+        else {
+          const int64_t L = lin0 + i;
+          u = u01(philox((uint64_t)(L >> 2), offset, seed).v[L & 3]);
+        }
+      }
+      const int c = sap_class(u, lo, hi);
+      if (cls) cls[off] = (int8_t)c;
+      if (sparse) {
+        if (c) y[off] = c == 1 ? vmin : vmax;
+      } else {
+        y[off] = c == 0 ? x[off] : (c == 1 ? vmin : vmax);
+      }
+    }
+  }
+}
+
+__global__ void k_disk_mask(float* __restrict__ m, int64_t outer, int n0, int n1, int n2, int int_r, int64_t r2i,
+                            float r2f, int inside_off) {
+  const int64_t per = (int64_t)n0 * n1 * n2;
+  const int64_t total = outer * per;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i % per;
+    const int i2 = (int)(r % n2);
+    r /= n2;
+    const int i1 = (int)(r % n1);
+    const int i0 = (int)(r / n1);
+    const int64_t d0 = i0 - n0 / 2, d1 = i1 - n1 / 2, d2 = i2 - n2 / 2;
+    const int64_t s = d0 * d0 + d1 * d1 + d2 * d2;
+    bool in = int_r ? (s < r2i) : ((float)s < r2f);
+    if (inside_off) in = !in;
+    m[i] = in ? 1.f : 0.f;
+  }
+}
+
+// log-abs statistics of the op-processed spectrum (default spike intensity)
+template <int NT, int RS>
+__global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* __restrict__ S, int bc0, int C, int T,
+                                                     BatchOps ops, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cf* lds = reinterpret_cast<cf*>(smem);
+  DevCtx ctx{(int)threadIdx.x, NT};
+  const int bcl = (int)blockIdx.y, bc = bc0 + bcl;
+  const int H = pl.H, W = pl.W, D = pl.D, Dh = D / 2 + 1;
+  const int ncols_all = W * Dh;
+  const int j0 = (int)blockIdx.x * T;
+  const int nc = (ncols_all - j0) < T ? (ncols_all - j0) : T;
+  const TileGeo g = tile_geo(H, T);
+  cf* tw = lds + g.off_tw;
+  int* irev = reinterpret_cast<int*>(lds + g.off_irev);
+  for (int i = threadIdx.x; i < H; i += NT) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
+  const cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
+  const int nl = H * nc;
+  for (int t = threadIdx.x; t < nl; t += NT) {
+    const int hh = t / nc, c = t - hh * nc;
+    lds[hh * T + c] = Sb[(int64_t)hh * ncols_all + c];
+  }
+  __syncthreads();
+  fft_dif<DevCtx, RS>(ctx, lds, tw, pl.ax[0], nc, TileAddr{T}, true);
+  double acc = 0.0;
+  const tb_sample_ops& so = ops.s[bcl / C];
+  const int chan = bcl % C;
+  const int Dtop = (D % 2 == 0) ? D / 2 : -1;
+  for (int t = threadIdx.x; t < nl; t += NT) {
+    const int hp = t / nc, c = t - hp * nc;
+    const int j = j0 + c;
+    const int wp = j / Dh, kd = j - wp * Dh;
+    const cf v = apply_ops(so, chan, lds[hp * T + c], irev[hp], pl.irev_w[wp], kd, H, W, D);
+    const float la = logf(f32_sqrt(v.x * v.x + v.y * v.y) + 1e-10f);
+    acc += (kd == 0 || kd == Dtop) ? (double)la : 2.0 * (double)la;
+  }
+  // block reduce in double
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(smem);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < NT / 64; ++w) acc += red[w];
+    atomicAdd(&out[bc], acc);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- plan
+struct tb_plan {
+  tb_plan_dev dev;
+  PlanTables host;
+  void* dmem = nullptr;
+  int rset = RS_ALL;
+  int lds_max = 65536;
+};
+
+namespace {
+
+constexpr int NT_SLAB = 512;
+constexpr int NT_TILE = 256;
+constexpr int NT_SAP = 256;
+
+int rset_of(const PlanTables& pt) {
+  int mr = 1;
+  for (int a = 0; a < 3; ++a)
+    for (int s = 0; s < pt.ax[a].nst; ++s)
+      if (pt.ax[a].radix[s] > 10 && pt.ax[a].radix[s] != 12 && pt.ax[a].radix[s] != 15 &&
+          pt.ax[a].radix[s] != 16)
+        mr = pt.ax[a].radix[s];
+  return mr > 1 ? RS_ALL : RS_SMALL;
+}
+
+int pick_tile(int H, int lds_max) {
+  // ~64 KB tiles: two workgroups per CU, >= 256 B contiguous per row segment when H <= 256
+  int T = 65536 / (H * 8);
+  if (T > 64) T = 64;
+  if (T < 4) T = 4;
+  while (tile_geo(H, T).total_cf * 8 > lds_max && T > 1) --T;
+  return T;
+}
+
+template <class K>
+int set_lds(K kern, size_t bytes) {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  TB_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes));
+  return TB_OK;
+}
+
+}  // namespace
+
+// Exported functions: C linkage comes from their declarations in texbias.h.
+int tb_version(void) { return TB_VERSION; }
+
+const char* tb_error_string(int code) {
+  switch (code) {
+    case TB_OK: return "ok";
+    case TB_ERR_INVALID_ARG: return "invalid argument";
+    case TB_ERR_UNSUPPORTED_SIZE: return "unsupported transform size (prime factor > 31 or slab exceeds LDS)";
+    case TB_ERR_HIP: return "HIP runtime error";
+    case TB_ERR_WORKSPACE: return "workspace too small";
+    default: return "unknown error";
+  }
+}
+
+int tb_last_hip_error(void) { return g_last_hip; }
+
+int tb_plan_create(int H, int W, int D, tb_plan** out) {
+  if (!out) return TB_ERR_INVALID_ARG;
+  *out = nullptr;
+  tb_plan* p = new tb_plan();
+  int rc = build_tables(H, W, D, p->host);
+  if (rc != TB_OK) { delete p; return rc; }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { delete p; return hip_fail(hipGetLastError()); }
+  int lds = 0;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && lds > 0)
+    p->lds_max = lds;
+  const SlabGeo sg = slab_geo(W, D);
+  if ((size_t)sg.total_cf * 8 > (size_t)p->lds_max) { delete p; return TB_ERR_UNSUPPORTED_SIZE; }
+  // device tables: tw[H], tw[W], tw[D] (cf) + rev_d[D], irev_h[H], irev_w[W] (int)
+  const size_t ncf = (size_t)H + W + D, nint = (size_t)D + H + W;
+  const size_t bytes = ncf * sizeof(cf) + nint * sizeof(int);
+  std::vector<char> buf(bytes);
+  char* q = buf.data();
+  size_t off_tw[3], off_i[3];
+  size_t o = 0;
+  const int n[3] = {H, W, D};
+  for (int a = 0; a < 3; ++a) {
+    off_tw[a] = o;
+    std::memcpy(q + o, p->host.tw[a].data(), n[a] * sizeof(cf));
+    o += n[a] * sizeof(cf);
+  }
+  const std::vector<int>* iv[3] = {&p->host.rev_d, &p->host.irev_h, &p->host.irev_w};
+  for (int a = 0; a < 3; ++a) {
+    off_i[a] = o;
+    std::memcpy(q + o, iv[a]->data(), iv[a]->size() * sizeof(int));
+    o += iv[a]->size() * sizeof(int);
+  }
+  if (hipMalloc(&p->dmem, bytes) != hipSuccess) { delete p; return hip_fail(hipGetLastError()); }
+  if (hipMemcpy(p->dmem, buf.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(p->dmem);
+    delete p;
+    return hip_fail(hipGetLastError());
+  }
+  char* d = static_cast<char*>(p->dmem);
+  p->dev.H = H; p->dev.W = W; p->dev.D = D; p->dev.pad = 0;
+  for (int a = 0; a < 3; ++a) {
+    p->dev.ax[a] = p->host.ax[a];
+    p->dev.tw[a] = reinterpret_cast<const cf*>(d + off_tw[a]);
+  }
+  p->dev.rev_d = reinterpret_cast<const int*>(d + off_i[0]);
+  p->dev.irev_h = reinterpret_cast<const int*>(d + off_i[1]);
+  p->dev.irev_w = reinterpret_cast<const int*>(d + off_i[2]);
+  p->rset = rset_of(p->host);
+  *out = p;
+  return TB_OK;
+}
+
+int tb_plan_destroy(tb_plan* plan) {
+  if (!plan) return TB_OK;
+  if (plan->dmem) hipFree(plan->dmem);
+  delete plan;
+  return TB_OK;
+}
+
+size_t tb_workspace_bytes(const tb_plan* plan, int bc) {
+  if (!plan || bc < 0) return 0;
+  return (size_t)bc * plan->dev.H * plan->dev.W * (plan->dev.D / 2 + 1) * sizeof(cf);
+}
+
+int tb_plan_radices(const tb_plan* plan, int axis, int* radices) {
+  if (!plan || axis < 0 || axis > 2 || !radices) return -1;
+  const tb_axis& a = plan->dev.ax[axis];
+  for (int s = 0; s < a.nst; ++s) radices[s] = a.radix[s];
+  return a.nst;
+}
+
+template <int RS>
+static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, cf* S, int bc0, int nbc,
+                           hipStream_t st) {
+  const size_t lds = (size_t)slab_geo(p->dev.W, p->dev.D).total_cf * sizeof(cf);
+  int rc = set_lds(k_slab_fwd<NT_SLAB, RS>, lds);
+  if (rc) return rc;
+  hipLaunchKernelGGL((k_slab_fwd<NT_SLAB, RS>), dim3(p->dev.H, nbc), dim3(NT_SLAB), lds, st, p->dev, x, xs[0],
+                     xs[1], xs[2], S, bc0);
+  TB_HIP(hipGetLastError());
+  return TB_OK;
+}
+
+template <int RS>
+static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
+                         void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops, uint32_t* minmax,
+                         void* stream) {
+  if (!p || !x || !y || !xs || !ys || !ops || B < 1 || C < 1 || y_pad < 0) return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb_workspace_bytes(p, B * C) || !ws) return TB_ERR_WORKSPACE;
+  for (int b = 0; b < B; ++b)
+    if (ops[b].n < 0 || ops[b].n > TB_MAX_OPS) return TB_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  cf* S = static_cast<cf*>(ws);
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  const float scale = (float)(1.0 / ((double)H * (double)W * (double)D));
+  if (minmax) {
+    hipLaunchKernelGGL(k_minmax_init, dim3((B + 255) / 256), dim3(256), 0, st, minmax, B);
+    TB_HIP(hipGetLastError());
+  }
+  const int T = pick_tile(H, p->lds_max);
+  const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
+  const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
+  const size_t lds_s = (size_t)slab_geo(W, D).total_cf * sizeof(cf);
+  int rc = set_lds(k_kspace<NT_TILE, RS>, lds_b);
+  if (rc) return rc;
+  rc = set_lds(k_slab_inv<NT_SLAB, RS>, lds_s);
+  if (rc) return rc;
+  // launch groups of <= TB_MAX_BATCH samples (the op programs travel in the kernel arguments)
+  for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
+    const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
+    BatchOps bo;
+    std::memset(&bo, 0, sizeof(bo));
+    for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
+    {
+      Timer t(0, st);
+      rc = launch_slab_fwd<RS>(p, x, xs, S, b0 * C, nb * C, st);
+      if (rc) return rc;
+    }
+    {
+      Timer t(1, st);
+      hipLaunchKernelGGL((k_kspace<NT_TILE, RS>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C, T,
+                         bo);
+      TB_HIP(hipGetLastError());
+    }
+    {
+      Timer t(2, st);
+      hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RS>), dim3(H, nb * C), dim3(NT_SLAB), lds_s, st, p->dev, S, y, ys[0], ys[1],
+                         ys[2], y_pad, b0 * C, C, scale, minmax);
+      TB_HIP(hipGetLastError());
+    }
+  }
+  return TB_OK;
+}
+
+template <int RS>
+static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, void* ws, size_t ws_bytes, int B,
+                             int C, const tb_sample_ops* ops, double* out, void* stream) {
+  if (!p || !x || !xs || !ops || !out || B < 1 || C < 1) return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb_workspace_bytes(p, B * C) || !ws) return TB_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  cf* S = static_cast<cf*>(ws);
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  const int T = pick_tile(H, p->lds_max);
+  const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
+  const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
+  int rc = set_lds(k_kspace_stats<NT_TILE, RS>, lds_b);
+  if (rc) return rc;
+  TB_HIP(hipMemsetAsync(out, 0, sizeof(double) * B * C, st));
+  for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
+    const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
+    BatchOps bo;
+    std::memset(&bo, 0, sizeof(bo));
+    for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
+    rc = launch_slab_fwd<RS>(p, x, xs, S, b0 * C, nb * C, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_kspace_stats<NT_TILE, RS>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C,
+                       T, bo, out);
+    TB_HIP(hipGetLastError());
+  }
+  return TB_OK;
+}
+
+int tb_kspace_filter_f32(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
+                         void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops, uint32_t* minmax,
+                         void* stream) {
+  if (!p) return TB_ERR_INVALID_ARG;
+  return p->rset == RS_SMALL ? kspace_filter<RS_SMALL>(p, x, xs, y, ys, y_pad, ws, ws_bytes, B, C, ops, minmax, stream)
+                             : kspace_filter<RS_ALL>(p, x, xs, y, ys, y_pad, ws, ws_bytes, B, C, ops, minmax, stream);
+}
+
+int tb_kspace_logabs_sum_f32(const tb_plan* p, const float* x, const int64_t* xs, void* ws, size_t ws_bytes, int B,
+                             int C, const tb_sample_ops* ops, double* out, void* stream) {
+  if (!p) return TB_ERR_INVALID_ARG;
+  return p->rset == RS_SMALL ? kspace_stats<RS_SMALL>(p, x, xs, ws, ws_bytes, B, C, ops, out, stream)
+                             : kspace_stats<RS_ALL>(p, x, xs, ws, ws_bytes, B, C, ops, out, stream);
+}
+
+int tb_minmax_f32(const float* x, uint32_t* mm, int B, int64_t rows, int len, int64_t ld, int64_t sb, void* stream) {
+  if (!x || !mm || B < 1 || rows < 1 || len < 1 || ld < len) return TB_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  Timer t(3, st);
+  hipLaunchKernelGGL(k_minmax_init, dim3((B + 255) / 256), dim3(256), 0, st, mm, B);
+  const int64_t n = rows * len;
+  int64_t blocks = (n + 256 * 8 - 1) / (256 * 8);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_minmax<256>, dim3((unsigned)blocks, B), dim3(256), 0, st, x, mm, rows, len, ld, sb);
+  TB_HIP(hipGetLastError());
+  return TB_OK;
+}
+
+int tb_salt_pepper_f32(const float* x, float* y, int8_t* cls, const float* u_in, uint64_t seed, uint64_t offset,
+                       const float* thr, const uint32_t* mm, int B, int64_t rows, int len, int64_t ld, int64_t sb,
+                       void* stream) {
+  if (!x || !y || !thr || !mm || B < 1 || rows < 1 || len < 1 || ld < len) return TB_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int sparse = (x == y && !cls && !u_in) ? 1 : 0;
+  const int64_t n = rows * len;
+  int64_t blocks = ((n + 3) / 4 + NT_SAP - 1) / NT_SAP;
+  if (blocks > 2048) blocks = 2048;
+  Timer t(3, st);
+  for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
+    const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
+    SapThr th;
+    for (int i = 0; i < TB_MAX_BATCH; ++i) {
+      th.lo[i] = i < nb ? thr[2 * (b0 + i)] : 0.f;
+      th.hi[i] = i < nb ? thr[2 * (b0 + i) + 1] : 0.f;
+    }
+    hipLaunchKernelGGL(k_salt_pepper<NT_SAP>, dim3((unsigned)blocks, nb), dim3(NT_SAP), 0, st, x, y, cls, u_in, seed,
+                       offset, th, mm, b0, rows, len, ld, sb, sparse);
+    TB_HIP(hipGetLastError());
+  }
+  return TB_OK;
+}
+
+float tb_key_to_float(uint32_t key) { return key2f(key); }
+
+int tb_disk_mask_f32(float* mask, int64_t outer, int n0, int n1, int n2, int int_r, int64_t r2i, float r2f,
+                     int inside_off, void* stream) {
+  if (!mask || outer < 1 || n0 < 1 || n1 < 1 || n2 < 1) return TB_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = outer * n0 * n1 * n2;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_disk_mask, dim3((unsigned)blocks), dim3(256), 0, st, mask, outer, n0, n1, n2, int_r, r2i, r2f,
+                     inside_off);
+  TB_HIP(hipGetLastError());
+  return TB_OK;
+}
+
+int tb_set_pass_timing(int enable) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_timing = enable != 0;
+  for (auto& r : g_recs) { g_pool.push_back(r.a); g_pool.push_back(r.b); }
+  g_recs.clear();
+  return TB_OK;
+}
+
+int tb_get_pass_times_ms(float* ms, int* cnt) {
+  if (!ms || !cnt) return TB_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(g_tmu);
+  for (int i = 0; i < 4; ++i) { ms[i] = 0.f; cnt[i] = 0; }
+  for (auto& r : g_recs) {
+    TB_HIP(hipEventSynchronize(r.b));
+    float t = 0.f;
+    TB_HIP(hipEventElapsedTime(&t, r.a, r.b));
+    ms[r.slot] += t;
+    cnt[r.slot] += 1;
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  g_recs.clear();
+  return TB_OK;
+}
