@@ -44,7 +44,8 @@ extern "C" {
 #define TB_OP_NONE 0
 #define TB_OP_DISK 1  /* i[0]=int radius?, i[1]=inside_off, f[0]=fl32(r*r) or l=r*r (int)     */
 #define TB_OP_GIBBS 2 /* l = integer threshold T4 on sum (2s-(n-1))^2 (float64 geometry)        */
-#define TB_OP_LAYER 3 /* f[0] = alpha * max_dist (float32 geometry of GibbsNoiseLayer)          */
+#define TB_OP_LAYER 3 /* f[0] = alpha * max_dist (float32 geometry of GibbsNoiseLayer), or, when
+                         l != 0, l = DEVICE address of a float alpha and f[1] = max_dist        */
 #define TB_OP_WRAP 4  /* f[0] = alpha                                                           */
 #define TB_OP_SPIKE 5 /* i[0..2] = UNSHIFTED (kh,kw,kd); f[0] = exp(log-intensity);
                          f[1] = phase override or NaN (keep own phase); f[2],f[3] = cos,sin(f[1]);

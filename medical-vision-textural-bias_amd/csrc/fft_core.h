@@ -359,7 +359,10 @@ TB_HD bool layer_in(const tb_op& op, int kh, int kw, int kd, int H, int W, int D
   const float ew = (float)shifted(kw, W) - (float)(W - 1) * 0.5f;
   const float ed = (float)shifted(kd, D) - (float)(D - 1) * 0.5f;
   const float d2 = (eh * eh + ew * ew) + ed * ed;   // exact: quarter-integers < 2^22
-  const float nd = f32_div(f32_sqrt(d2), op.f[0]);
+  // alpha * max_dist: from the launch arguments, or (op.l != 0) from the layer's device-resident
+  // alpha buffer times max_dist in f[1] -- no host round trip for the alpha of Gibbs_GD updates
+  const float an = op.l ? (*reinterpret_cast<const float*>(op.l)) * op.f[1] : op.f[0];
+  const float nd = f32_div(f32_sqrt(d2), an);
   return !(nd > 1.f);
 }
 

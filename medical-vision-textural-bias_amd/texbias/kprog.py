@@ -134,9 +134,15 @@ def layer_alpha_norm(alpha: float, spatial: Sequence[int]) -> np.float32:
     return np.float32(np.float32(alpha) * np.sqrt(np.float32(s)))
 
 
-def layer_op(alpha: float, spatial: Sequence[int]) -> TbOp:
+def layer_op(alpha: float, spatial: Sequence[int], alpha_ptr: int = 0) -> TbOp:
+    """GibbsNoiseLayer mask.  With ``alpha_ptr`` (device address of a float32 alpha) the kernel
+    reads alpha itself, so a layer whose alpha lives on the device never syncs the host."""
     op = _op(TB_OP_LAYER)
-    op.f[0] = layer_alpha_norm(alpha, spatial)
+    if alpha_ptr:
+        op.l = int(alpha_ptr)
+        op.f[1] = layer_alpha_norm(1.0, spatial)   # = max dist
+    else:
+        op.f[0] = layer_alpha_norm(alpha, spatial)
     return op
 
 

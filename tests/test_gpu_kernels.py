@@ -1,0 +1,184 @@
+"""GPU parity of the HIP kernels (through the C ABI via texbias.runtime) against the
+reference's golden fixtures and the numpy oracle.
+
+Tolerances: filtered outputs  max|y - y_ref| / max|y_ref| <= 1e-5 (north_star);
+salt-and-pepper class maps and mask counts bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _golden import load_cases, relerr
+from oracle import filters_oracle as O
+from texbias import kprog as K
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def rt(gpu):
+    from texbias import runtime
+    return runtime
+
+
+def run(rt, x, n_dims, prog, pad=0):
+    lead = x.shape[:-n_dims]
+    chans = int(np.prod(lead))
+    xb = torch.from_numpy(np.ascontiguousarray(x)).cuda().reshape((1, chans) + x.shape[-n_dims:])
+    mm = torch.empty((1, 2), dtype=torch.int32, device="cuda")
+    y = rt.kspace_filter(xb, n_dims, [prog], chans, pad=pad, minmax=mm)
+    torch.cuda.synchronize()
+    return y.cpu().numpy().reshape(x.shape[:-1] + (x.shape[-1] + pad,)), rt.keys_to_float(mm)[0]
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 16, 16), (1, 240, 240, 155), (4, 128, 128, 64), (1, 31, 17, 37 - 7),
+                                   (3, 1, 1, 64), (2, 1, 256, 256), (1, 60, 1, 15)])
+def test_identity_roundtrip(rt, shape):
+    x = np.random.default_rng(7).standard_normal(shape).astype(np.float32)
+    y, mm = run(rt, x, 3, [])
+    assert relerr(y, x) < 2e-6
+    assert mm[0] == x.min() or abs(mm[0] - x.min()) < 1e-5
+    assert abs(mm[1] - x.max()) < 1e-5
+
+
+@pytest.mark.parametrize("name,case", sorted(load_cases("disk").items()))
+def test_disk(rt, name, case):
+    meta, a = case
+    r = meta["r"]
+    r = float("inf") if r == "inf" else (meta["r_used"] if isinstance(r, list) else r)
+    y, _ = run(rt, a["x"], 3, [K.disk_op(r, meta["inside_off"])])
+    assert relerr(y, a["y"]) < TOL
+
+
+@pytest.mark.parametrize("name,case", sorted(load_cases("wrap").items()))
+def test_wrap(rt, name, case):
+    meta, a = case
+    y, _ = run(rt, a["x"], 3, [K.wrap_op(meta["alpha"])])
+    assert relerr(y, a["y"]) < TOL
+
+
+@pytest.mark.parametrize("name,case", sorted((k, v) for k, v in load_cases("gibbs").items() if k != "gibbs_known"))
+def test_gibbs(rt, name, case):
+    meta, a = case
+    x = a["x"]
+    y, _ = run(rt, x, x.ndim - 1, [K.gibbs_op(meta["alpha"], x.shape[1:])])
+    assert relerr(y, a["y"]) < TOL
+
+
+@pytest.mark.parametrize("name,case", sorted(load_cases("planes").items()))
+def test_planes(rt, name, case):
+    meta, a = case
+    geo = K.geometry(a["x"].shape[1:])
+    y, _ = run(rt, a["x"], 3, [K.spike_op(meta["idx"], geo, meta["intensity"])])
+    assert relerr(y, a["y"]) < TOL
+
+
+@pytest.mark.parametrize("name,case", sorted((k, v) for k, v in load_cases("glayer").items() if k != "glayer_known"))
+def test_gibbs_layer_device_alpha(rt, name, case):
+    meta, a = case
+    x = torch.from_numpy(a["x"]).cuda()
+    alpha = torch.tensor([meta["alpha"]], dtype=torch.float32, device="cuda")
+    progs = [[K.layer_op(0.0, x.shape[1:], alpha_ptr=alpha.data_ptr())] for _ in range(x.shape[0])]
+    y = rt.kspace_filter(x[:, None], 4, progs, 1)
+    assert relerr(y[:, 0].cpu().numpy(), a["y"]) < TOL
+
+
+@pytest.mark.parametrize("name,case", sorted(load_cases("chain").items()))
+def test_chain_fused_with_sap(rt, name, case):
+    meta, a = case
+    x = a["x"]
+    geo = K.geometry(x.shape[1:])
+    prog = [K.disk_op(meta["r"], False)]
+    prog += [K.spike_op(meta["idx"], geo, meta["intensity"], phase=float(p), chan=c) for c, p in enumerate(a["phase"])]
+    for op in prog[2:]:
+        op.reserved = 1
+    prog += [K.wrap_op(meta["alpha"])]
+    xb = torch.from_numpy(x).cuda()[None]
+    mm = torch.empty((1, 2), dtype=torch.int32, device="cuda")
+    y3 = rt.kspace_filter(xb, 3, [prog], x.shape[0], minmax=mm)
+    assert relerr(y3[0].cpu().numpy(), a["y3"]) < TOL
+    # salt & pepper on the fused output with the reference's own u field
+    u = torch.from_numpy(a["u"]).cuda()[None]
+    cls = torch.empty(xb.shape, dtype=torch.int8, device="cuda")
+    p = meta["p"]
+    z = rt.salt_and_pepper(y3, 4, [(np.float32(p / 2), np.float32(p))], mm, u=u, cls=cls)
+    zh = z[0].cpu().numpy()
+    refz, refc = O.salt_and_pepper(y3[0].cpu().numpy(), p, a["u"])
+    np.testing.assert_array_equal(cls[0].cpu().numpy(), refc)
+    np.testing.assert_array_equal(zh, refz)
+    assert relerr(zh, a["y"]) < TOL
+
+
+@pytest.mark.parametrize("name,case", sorted(load_cases("sap").items()))
+def test_sap_golden(rt, name, case):
+    meta, a = case
+    x = torch.from_numpy(a["x"]).cuda()[None]
+    mm = rt.minmax_keys(x, 4)
+    p = meta["p_used"]
+    cls = torch.empty(x.shape, dtype=torch.int8, device="cuda")
+    y = rt.salt_and_pepper(x, 4, [(np.float32(p / 2), np.float32(p))], mm, u=torch.from_numpy(a["u"]).cuda()[None],
+                           cls=cls)
+    np.testing.assert_array_equal(cls[0].cpu().numpy(), a["cls"])
+    np.testing.assert_array_equal(y[0].cpu().numpy(), a["y"])
+
+
+def test_sap_philox_sparse_inplace(rt):
+    """Sparse in-place scatter == dense out-of-place with the same Philox stream; rate ~ p."""
+    x = torch.randn((2, 4, 64, 60, 31), device="cuda")
+    mm = rt.minmax_keys(x, 4)
+    thr = [(np.float32(0.05), np.float32(0.1))] * 2
+    cls = torch.empty(x.shape, dtype=torch.int8, device="cuda")
+    dense = rt.salt_and_pepper(x, 4, thr, mm, cls=cls, seed=1234, offset=7)
+    inplace = x.clone()
+    rt.salt_and_pepper(inplace, 4, thr, mm, out=inplace, seed=1234, offset=7)
+    torch.testing.assert_close(inplace, dense, rtol=0, atol=0)
+    frac1 = (cls == 1).float().mean().item()
+    frac2 = (cls == 2).float().mean().item()
+    assert abs(frac1 - 0.05) < 0.003 and abs(frac2 - 0.05) < 0.003
+    mmf = rt.keys_to_float(mm)
+    xs = x.reshape(2, -1)
+    assert np.allclose(mmf[:, 0], xs.min(1).values.cpu().numpy()) and np.allclose(mmf[:, 1], xs.max(1).values.cpu().numpy())
+
+
+def test_disk_mask_counts(rt):
+    m = rt.disk_mask_tensor((1, 64, 64, 64), 12.5, 3, False, torch.device("cuda"))
+    assert int(m.sum().item()) == 8217
+    m2 = rt.disk_mask_tensor((1, 256, 256), 40, 2, False, torch.device("cuda"))
+    assert int(m2.sum().item()) == 5013
+    meta, a = load_cases("diskmask")["diskmask_counts"]
+    m3 = rt.disk_mask_tensor((2, 20, 17), 6.5, 2, True, torch.device("cuda"))
+    np.testing.assert_array_equal(m3.cpu().numpy(), a["mask2d_20x17"])
+
+
+def test_full_size_c3_properties(rt):
+    """BASELINE config 3 geometry 2 x 4 x 240 x 240 x 155: parity of one channel vs the oracle,
+    linearity of the fused filter, zero D-padding to 160, identity at r = inf / alpha = 1."""
+    torch.manual_seed(0)
+    x = torch.randn((2, 4, 240, 240, 155), device="cuda")
+    geo = K.geometry((240, 240, 155))
+    prog = [K.disk_op(12.5, False), K.spike_op((70, 137, 71), geo, 15.0, phase=0.3), K.wrap_op(0.5)]
+    y = rt.kspace_filter(x, 3, [prog, prog], 4, pad=5)
+    assert y.shape == (2, 4, 240, 240, 160)
+    assert torch.all(y[..., 155:] == 0)
+    x0 = x[1, 2].cpu().numpy()
+    ref = O.wrap_artifact(O.plane_waves(O.fourier_disk(x0[None], 12.5), (70, 137, 71), 15.0, phase=[0.3]), 0.5)[0]
+    assert relerr(y[1, 2, ..., :155].cpu().numpy(), ref) < TOL
+    # linearity of the mask part
+    progm = [K.disk_op(20.0, False), K.wrap_op(0.25)]
+    a, b = 0.75, -1.5
+    x2 = torch.randn_like(x)
+    lhs = rt.kspace_filter(a * x + b * x2, 3, [progm] * 2, 4)
+    rhs = a * rt.kspace_filter(x, 3, [progm] * 2, 4) + b * rt.kspace_filter(x2, 3, [progm] * 2, 4)
+    assert (lhs - rhs).abs().max().item() / rhs.abs().max().item() < 2e-6
+    ident = rt.kspace_filter(x, 3, [[K.disk_op(float("inf"), False), K.wrap_op(1.0)]] * 2, 4)
+    assert (ident - x).abs().max().item() / x.abs().max().item() < 2e-6
+
+
+def test_default_intensity_stats(rt):
+    meta, a = load_cases("kspike")["kspike_3"]
+    x = torch.from_numpy(a["x"]).cuda()[None]
+    s = rt.logabs_sums(x, 3, [[]], x.shape[1]).cpu().numpy()
+    n = np.prod(a["x"].shape[1:])
+    dflt = s / n * 2.5
+    np.testing.assert_allclose(dflt, O.kspace_default_intensity(a["x"]), rtol=2e-3)
