@@ -1,0 +1,147 @@
+"""Batched device-side augmentation: a list of the reference's transforms compiled into
+fused k-space passes over a collated [B, C, *spatial] batch.
+
+The reference applies its transforms per sample in DataLoader workers, one full FFT round
+trip per filter (e.g. 127_.../..._3modalities.py:171-174: disk -> planes -> wrap -> S&P).
+``FusedChain`` keeps the same transform objects -- so every host RNG draw (prob draws, sampled
+radius / alpha, the ellipsoid point) happens in the same order as a sequential Compose over
+each sample -- but runs each maximal run of k-space transforms as ONE forward-FFT -> op program
+-> inverse-FFT pass (``.real`` between filters is a Hermitian symmetrisation, which
+the half-spectrum program reproduces exactly), then salt-and-pepper as a sparse in-place
+scatter.  The k-space pass also writes the U-Net's zero D-padding and the per-sample min/max
+salt-and-pepper needs, so the batch is read from HBM once per pass.
+
+Salt-and-pepper draws its uniform field from a device Philox stream keyed per call from
+torch's global generator (the reference uses ``torch.rand`` on the CPU, :472).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import kprog as K
+from . import runtime as rt
+
+
+def _kind(t) -> str:
+    return type(t).__name__
+
+
+KSPACE = {"RandFourierDiskMaskd", "RandPlaneWaves_ellipsoid", "WrapArtifactd", "WrapArtifact", "GibbsNoise",
+          "RandGibbsNoise", "RandGibbsNoised", "KSpaceSpikeNoise"}
+POINTWISE = {"SaltAndPepper"}
+
+
+class FusedChain:
+    """Compile ``transforms`` (instances from filters_and_operators) for batched device execution.
+
+    ``__call__(x, pad=0)``: x [B, C, *spatial] float32 on a HIP device (spatial = 3 axes);
+    returns [B, C, *spatial[:-1], spatial[-1] + pad].  ``rngs``: optional per-sample list of
+    transform lists (independent RandomStates per sample, e.g. per rank); by default the same
+    transform objects draw for every sample in turn, exactly like a per-sample Compose.
+    """
+
+    def __init__(self, transforms: Sequence, key: str = "image"):
+        for t in transforms:
+            if _kind(t) not in KSPACE | POINTWISE:
+                raise TypeError(f"{_kind(t)} is not a fusable texbias transform")
+        self.transforms = list(transforms)
+        self.key = key
+        self._mm: Optional[torch.Tensor] = None
+
+    # --- host side: one sample's draws, in Compose order --------------------------------
+    def _sample_plan(self, spatial) -> List:
+        """Returns a list of stages: ('k', program) or ('sap', p) for one sample."""
+        stages: List = []
+        prog: List = []
+        seg = False   # the current segment holds a k-space transform (structure, not draws)
+        for t in self.transforms:
+            k = _kind(t)
+            seg = seg or k in KSPACE
+            if k == "RandFourierDiskMaskd":
+                t.randomize()
+                if t._do_transform:
+                    prog += t.program()
+            elif k == "RandPlaneWaves_ellipsoid":
+                t.randomize(None)
+                if t._do_transform:
+                    prog += t.program_for(spatial)
+            elif k == "WrapArtifactd":
+                prog += t.transform.program()
+            elif k == "WrapArtifact":
+                prog += t.program()
+            elif k == "GibbsNoise":
+                prog += t.program(spatial)
+            elif k in ("RandGibbsNoise", "RandGibbsNoised"):
+                t._randomize(None)
+                if t._do_transform:
+                    prog += [K.gibbs_op(t.sampled_alpha, spatial)]
+            elif k == "KSpaceSpikeNoise":
+                if t.k_intensity is None:
+                    raise ValueError("FusedChain needs explicit k_intensity (the default is data dependent)")
+                prog += t.program(torch.empty((1,) + tuple(spatial), device="meta"))
+            elif k == "SaltAndPepper":
+                t.randomize(None)
+                if seg:
+                    stages.append(("k", prog))
+                    prog, seg = [], False
+                stages.append(("sap", t.p if t._do_transform else None))
+        if seg:
+            stages.append(("k", prog))
+        return stages
+
+    def plan(self, B: int, spatial) -> List[List]:
+        return [self._sample_plan(spatial) for _ in range(B)]
+
+    # --- device side --------------------------------------------------------------------
+    def __call__(self, x: torch.Tensor, pad: int = 0, plans: Optional[List[List]] = None) -> torch.Tensor:
+        rt.require_hip(x, "FusedChain")
+        if x.dim() != 5:
+            raise ValueError("FusedChain expects [B, C, H, W, D]")
+        B, C = x.shape[:2]
+        spatial = tuple(x.shape[2:])
+        plans = plans if plans is not None else self.plan(B, spatial)
+        nst = len(plans[0])
+        if any(len(p) != nst or [s[0] for s in p] != [s[0] for s in plans[0]] for p in plans):
+            raise ValueError("all samples of a batch must share the stage structure")
+        if self._mm is None or self._mm.shape[0] < B or self._mm.device != x.device:
+            self._mm = torch.empty((max(B, 8), 2), dtype=torch.int32, device=x.device)
+        mm = self._mm[:B]
+        cur = x
+        padded = False
+        mm_valid = False
+        for si in range(nst):
+            kind = plans[0][si][0]
+            if kind == "k":
+                progs = [p[si][1] for p in plans]
+                if not any(progs):
+                    continue   # every sample drew "no transform": identity
+                out_pad = pad if not padded else 0
+                if padded:   # filter the padded buffer in place (pass A reads all before C writes)
+                    view = cur[..., : spatial[-1]]
+                    rt.kspace_filter(view, 3, progs, C, out=view, minmax=mm)
+                else:
+                    cur = rt.kspace_filter(cur, 3, progs, C, pad=out_pad, minmax=mm)
+                    padded = out_pad > 0
+                mm_valid = True
+            else:
+                ps = [p[si][1] for p in plans]
+                if all(v is None for v in ps):
+                    continue
+                if cur is x:
+                    cur = x.clone() if not pad else torch.nn.functional.pad(x, (0, pad))
+                    padded = padded or pad > 0
+                view = cur[..., : spatial[-1]] if padded else cur
+                if not mm_valid:
+                    rt.minmax_keys(view, 4, out=mm)
+                thr = [((np.float32(p / 2), np.float32(p)) if p is not None else (-1.0, -1.0)) for p in ps]
+                seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+                rt.salt_and_pepper(view, 4, thr, mm, out=view, seed=seed)
+                mm_valid = False
+        if cur is x:
+            cur = x.clone() if not pad else torch.nn.functional.pad(x, (0, pad))
+        elif pad and not padded:
+            cur = torch.nn.functional.pad(cur, (0, pad))
+        return cur
