@@ -133,6 +133,17 @@ int tb_kspace_logabs_sum_f32(const tb_plan* plan, const float* x, const int64_t*
                              int B, int C, const tb_sample_ops* ops, double* out, void* stream);
 
 /*
+ * Weight gradient of a 3x3x3 Conv3d / ConvTranspose3d (stride 1 or 2, padding `pad`), f32:
+ *   dW[m][c][tz][ty][tx] = sum_n,z,y,x G[n][m][z][y][x] * X[n][c][s z+tz-pad][s y+ty-pad][s x+tx-pad]
+ * G [N][M][Do][Ho][Wo] and X [N][Cc][Di][Hi][Wi] contiguous (device); dW [M][Cc][27] (device,
+ * overwritten).  Conv3d: G = grad_out, X = input.  ConvTranspose3d: G = input, X = grad_out.
+ * Replaces MIOpen's backward-weights for the U-Net's full-resolution layers (train step of
+ * 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:232-243).
+ */
+int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
+                        int Hi, int Wi, int stride, int pad, void* stream);
+
+/*
  * Per-pass device timing for measurement: while enabled, every launch function records HIP
  * events around each of its kernels on the caller's stream.  tb_get_pass_times_ms synchronises
  * on them and returns the summed milliseconds per pass -- [0] slab forward (A), [1] k-space

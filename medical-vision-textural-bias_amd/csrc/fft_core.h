@@ -215,11 +215,39 @@ template <bool FWD> struct Dft<10, FWD> : DftComp<2, 5, FWD> {};
 template <bool FWD> struct Dft<12, FWD> : DftComp<4, 3, FWD> {};
 template <bool FWD> struct Dft<15, FWD> : DftComp<3, 5, FWD> {};
 
+// ------------------------------------------------------------ integer helpers
+// Division by a runtime-constant divisor for 0 <= t < 2^22: one float multiply + one correction
+// (the exact integer division sequence costs ~25 VALU ops; it sits in every work loop).
+struct FastDiv {
+  int d;
+  float inv;
+  TB_HD static FastDiv make(int dv) { FastDiv f; f.d = dv > 0 ? dv : 1; f.inv = 1.0f / (float)f.d; return f; }
+  TB_HD int div(int t) const {
+    int q = (int)((float)t * inv);
+    const int r = t - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+  }
+};
+
 // ------------------------------------------------------------ addressing
-// A pencil's element i lives at lds[base + (i>>1)*pitch + (i&1)*odd] when
-// "paired", else lds[base + i*stride].  One form covers all passes.
-struct Pencil {
-  int base, pitch, odd;  // paired form
+// pen(p) binds pencil p once per butterfly; pen(i) is then one multiply-add per element.
+struct RowAddr {  // pair pencils along D: element d of pair p at p*PR + d
+  int PR;
+  struct Pen {
+    int b;
+    TB_HD int operator()(int i) const { return b + i; }
+  };
+  TB_HD Pen pen(int p) const { return Pen{p * PR}; }
+};
+struct TileAddr {  // H pencils of the pass-B tile: element h of column c at h*T + c
+  int T;
+  struct Pen {
+    int c, T;
+    TB_HD int operator()(int h) const { return h * T + c; }
+  };
+  TB_HD Pen pen(int c) const { return Pen{c, T}; }
 };
 
 // ------------------------------------------------------ in-place stages
@@ -229,36 +257,84 @@ struct Pencil {
 //   y = DFT_r(x);  y[q] *= w_n^{j*q*P}
 // After all stages position  sum_s q_s * L_s  holds X[q_1 + r_1 (q_2 + r_2 (...))].
 // The inverse DIT runs the stages in reverse order with conj twiddles first.
+
+// odd-prime butterfly that stores each output pair as soon as it is formed (keeps ~R+8 live
+// complex registers instead of ~3R for the radix-31 stage of D = 155)
+template <int R, bool FWD, class Store>
+TB_HD void dft_odd_stream(cf* a, Store st) {
+  constexpr int M = (R - 1) / 2;
+  cf y0 = a[0];
+#pragma unroll
+  for (int p = 1; p <= M; ++p) {
+    const cf s = add(a[p], a[R - p]), d = sub(a[p], a[R - p]);
+    a[p] = s;
+    a[R - p] = d;
+    y0 = add(y0, s);
+  }
+  st(0, y0);
+#pragma unroll
+  for (int k = 1; k <= M; ++k) {
+    cf A = a[0], B = mk(0.f, 0.f);
+#pragma unroll
+    for (int p = 1; p <= M; ++p) {
+      const int m = (p * k) % R;
+      const float c = Trig<R>::tab.c[m], sn = Trig<R>::tab.s[m];
+      A.x += a[p].x * c; A.y += a[p].y * c;
+      B.x += a[R - p].x * sn; B.y += a[R - p].y * sn;
+    }
+    const cf iB = mk(-B.y, B.x);
+    st(k, FWD ? sub(A, iB) : add(A, iB));
+    st(R - k, FWD ? add(A, iB) : sub(A, iB));
+  }
+}
+
+// the streamed symmetric form is used for the odd primes >= 11 only (composites go through DftComp)
+template <int R> struct IsStreamed {
+  static constexpr bool value = (R == 11 || R == 13 || R == 17 || R == 19 || R == 23 || R == 29 || R == 31);
+};
+
 template <class Ctx, int R, bool FWD, class AddrF>
 TB_HD void stage_r(Ctx& ctx, cf* lds, const cf* tw, int Lb, int P, int npen, int nb, AddrF addr,
                    bool pencil_fast) {
   const int L = Lb / R;
   const int total = npen * nb;
+  const FastDiv dpen = FastDiv::make(npen), dnb = FastDiv::make(nb), dL = FastDiv::make(L);
   for (int t = ctx.tid; t < total; t += ctx.nthreads) {
     int p, u;
-    if (pencil_fast) { u = t / npen; p = t - u * npen; }
-    else { p = t / nb; u = t - p * nb; }
-    const int blk = u / L, j = u - blk * L;
+    if (pencil_fast) { u = dpen.div(t); p = t - u * npen; }
+    else { p = dnb.div(t); u = t - p * nb; }
+    const int blk = dL.div(u), j = u - blk * L;
     const int base = blk * Lb + j;
+    const auto pen = addr.pen(p);
     cf a[R];
-    int ad[R];
 #pragma unroll
-    for (int q = 0; q < R; ++q) { ad[q] = addr(p, base + q * L); a[q] = lds[ad[q]]; }
-    if (FWD) {
-      Dft<R, true>::run(a);
-      if (j) {
-#pragma unroll
-        for (int q = 1; q < R; ++q) a[q] = mul(a[q], tw[j * q * P]);
-      }
-    } else {
-      if (j) {
+    for (int q = 0; q < R; ++q) a[q] = lds[pen(base + q * L)];
+    if constexpr (IsStreamed<R>::value) {
+      if (!FWD && j) {
 #pragma unroll
         for (int q = 1; q < R; ++q) a[q] = mulc(a[q], tw[j * q * P]);
       }
-      Dft<R, false>::run(a);
-    }
+      dft_odd_stream<R, FWD>(a, [&](int q, cf v) {
+        if (FWD && j && q) v = mul(v, tw[j * q * P]);
+        lds[pen(base + q * L)] = v;
+      });
+    } else {
+      if (FWD) {
+        Dft<R, true>::run(a);
+        if (j) {
 #pragma unroll
-    for (int q = 0; q < R; ++q) lds[ad[q]] = a[q];
+          for (int q = 1; q < R; ++q) a[q] = mul(a[q], tw[j * q * P]);
+        }
+      } else {
+        if (j) {
+#pragma unroll
+          for (int q = 1; q < R; ++q) a[q] = mulc(a[q], tw[j * q * P]);
+        }
+        Dft<R, false>::run(a);
+      }
+#pragma unroll
+      for (int q = 0; q < R; ++q) lds[pen(base + q * L)] = a[q];
+    }
   }
 }
 
@@ -481,25 +557,21 @@ TB_HD TileGeo tile_geo(int H, int T) {
   return g;
 }
 
-// column addressing of the W-axis FFT inside the slab
+// column addressing of the W-axis FFT inside the slab: element w of column kd
 struct ColAddr {
   const int* posA;
   const int* posB;
   int PR, off_c0, off_cn, Dn, D;  // Dn = D/2 if D even else -1
-  TB_HD int base(int kd) const { return kd == 0 ? off_c0 : (kd == Dn ? off_cn : posA[kd]); }
-  TB_HD int operator()(int kd, int w) const {
-    if (kd == 0) return off_c0 + w;
-    if (kd == Dn) return off_cn + w;
-    return (w >> 1) * PR + ((w & 1) ? posB[kd] : posA[kd]);
+  struct Pen {
+    int e, o, pitch;
+    TB_HD int operator()(int w) const { return (w >> 1) * pitch + ((w & 1) ? o : e); }
+  };
+  TB_HD Pen pen(int kd) const {
+    if (kd == 0) return Pen{off_c0, off_c0 + 1, 2};
+    if (kd == Dn) return Pen{off_cn, off_cn + 1, 2};
+    return Pen{posA[kd], posB[kd], PR};
   }
-};
-struct RowAddr {  // pair pencils along D
-  int PR;
-  TB_HD int operator()(int p, int d) const { return p * PR + d; }
-};
-struct TileAddr {  // H pencils of the pass-B tile
-  int T;
-  TB_HD int operator()(int c, int h) const { return h * T + c; }
+  TB_HD int operator()(int kd, int w) const { return pen(kd)(w); }
 };
 
 // --------------------------------------------------------------- pass A
@@ -523,8 +595,9 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
   // load pair rows
   const float* xb = x + bc * sx_bc + h * sx_h;
   const int nload = g.NP * D;
+  const FastDiv fD = FastDiv::make(D), fDh = FastDiv::make(Dh);
   for (int t = ctx.tid; t < nload; t += ctx.nthreads) {
-    const int p = t / D, d = t - p * D;
+    const int p = fD.div(t), d = t - p * D;
     const int w0 = 2 * p;
     const float a = xb[w0 * sx_w + d];
     const float b = (w0 + 1 < W) ? xb[(w0 + 1) * sx_w + d] : 0.f;
@@ -536,7 +609,7 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
   const int Dn = (D % 2 == 0) ? D / 2 : -1;
   const int nun = g.NP * Dh;
   for (int t = ctx.tid; t < nun; t += ctx.nthreads) {
-    const int p = t / Dh, k = t - p * Dh;
+    const int p = fDh.div(t), k = t - p * Dh;
     cf* row = lds + p * g.PR;
     const int w0 = 2 * p;
     if (k == 0 || k == Dn) {
@@ -559,7 +632,7 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
   cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
   const int nst = W * Dh;
   for (int t = ctx.tid; t < nst; t += ctx.nthreads) {
-    const int w = t / Dh, kd = t - w * Dh;
+    const int w = fDh.div(t), kd = t - w * Dh;
     Sb[t] = lds[ca(kd, w)];
   }
 }
@@ -578,17 +651,18 @@ TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict_
   for (int i = ctx.tid; i < H; i += ctx.nthreads) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
   cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
   const int nl = H * nc;
+  const FastDiv fnc = FastDiv::make(nc), fDh = FastDiv::make(Dh);
   for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
-    const int hh = t / nc, c = t - hh * nc;
+    const int hh = fnc.div(t), c = t - hh * nc;
     lds[hh * T + c] = Sb[(int64_t)hh * ncols_all + c];
   }
   ctx.sync();
   const TileAddr ta{T};
   fft_dif<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
   for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
-    const int hp = t / nc, c = t - hp * nc;
+    const int hp = fnc.div(t), c = t - hp * nc;
     const int j = j0 + c;
-    const int wp = j / Dh, kd = j - wp * Dh;
+    const int wp = fDh.div(j), kd = j - wp * Dh;
     const int kh = irev[hp], kw = pl.irev_w[wp];
     cf& v = lds[hp * T + c];
     v = apply_ops(so, chan, v, kh, kw, kd, H, W, D);
@@ -596,7 +670,7 @@ TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict_
   ctx.sync();
   fft_dit<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
   for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
-    const int hh = t / nc, c = t - hh * nc;
+    const int hh = fnc.div(t), c = t - hh * nc;
     Sb[(int64_t)hh * ncols_all + c] = lds[hh * T + c];
   }
 }
@@ -626,8 +700,9 @@ TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __res
   ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
   const cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
   const int nst = W * Dh;
+  const FastDiv fDh = FastDiv::make(Dh);
   for (int t = ctx.tid; t < nst; t += ctx.nthreads) {
-    const int w = t / Dh, kd = t - w * Dh;
+    const int w = fDh.div(t), kd = t - w * Dh;
     lds[ca(kd, w)] = Sb[t];
   }
   ctx.sync();
@@ -635,7 +710,7 @@ TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __res
   // repack rows (2p, 2p+1) into the pair spectrum z = X_a + i X_b (digit-reversed slots)
   const int nun = g.NP * Dh;
   for (int t = ctx.tid; t < nun; t += ctx.nthreads) {
-    const int p = t / Dh, k = t - p * Dh;
+    const int p = fDh.div(t), k = t - p * Dh;
     cf* row = lds + p * g.PR;
     const int w0 = 2 * p;
     const bool has_b = (w0 + 1 < W);
@@ -654,9 +729,10 @@ TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __res
   float* yb = y + bc * sy_bc + h * sy_h;
   const int ldw = D + ldy_pad;
   const int nout = W * ldw;
+  const FastDiv fld = FastDiv::make(ldw);
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
   for (int t = ctx.tid; t < nout; t += ctx.nthreads) {
-    const int w = t / ldw, d = t - w * ldw;
+    const int w = fld.div(t), d = t - w * ldw;
     float v = 0.f;
     if (d < D) {
       const cf z = lds[(w >> 1) * g.PR + d];

@@ -256,8 +256,9 @@ __global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* _
   for (int i = threadIdx.x; i < H; i += NT) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
   const cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
   const int nl = H * nc;
+  const FastDiv fnc = FastDiv::make(nc), fDh = FastDiv::make(Dh);
   for (int t = threadIdx.x; t < nl; t += NT) {
-    const int hh = t / nc, c = t - hh * nc;
+    const int hh = fnc.div(t), c = t - hh * nc;
     lds[hh * T + c] = Sb[(int64_t)hh * ncols_all + c];
   }
   __syncthreads();
@@ -267,9 +268,9 @@ __global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* _
   const int chan = bcl % C;
   const int Dtop = (D % 2 == 0) ? D / 2 : -1;
   for (int t = threadIdx.x; t < nl; t += NT) {
-    const int hp = t / nc, c = t - hp * nc;
+    const int hp = fnc.div(t), c = t - hp * nc;
     const int j = j0 + c;
-    const int wp = j / Dh, kd = j - wp * Dh;
+    const int wp = fDh.div(j), kd = j - wp * Dh;
     const cf v = apply_ops(so, chan, lds[hp * T + c], irev[hp], pl.irev_w[wp], kd, H, W, D);
     const float la = logf(f32_sqrt(v.x * v.x + v.y * v.y) + 1e-10f);
     acc += (kd == 0 || kd == Dtop) ? (double)la : 2.0 * (double)la;
@@ -293,7 +294,8 @@ struct tb_plan {
   tb_plan_dev dev;
   PlanTables host;
   void* dmem = nullptr;
-  int rset = RS_ALL;
+  int rset_h = RS_ALL;   // radix set of the H axis (pass B)
+  int rset_wd = RS_ALL;  // radix set of the W and D axes (passes A, C)
   int lds_max = 65536;
 };
 
@@ -303,14 +305,12 @@ constexpr int NT_SLAB = 512;
 constexpr int NT_TILE = 256;
 constexpr int NT_SAP = 256;
 
-int rset_of(const PlanTables& pt) {
-  int mr = 1;
-  for (int a = 0; a < 3; ++a)
-    for (int s = 0; s < pt.ax[a].nst; ++s)
-      if (pt.ax[a].radix[s] > 10 && pt.ax[a].radix[s] != 12 && pt.ax[a].radix[s] != 15 &&
-          pt.ax[a].radix[s] != 16)
-        mr = pt.ax[a].radix[s];
-  return mr > 1 ? RS_ALL : RS_SMALL;
+bool needs_all(const tb_axis& ax) {
+  for (int s = 0; s < ax.nst; ++s) {
+    const int r = ax.radix[s];
+    if (r > 10 && r != 12 && r != 15 && r != 16) return true;
+  }
+  return false;
 }
 
 int pick_tile(int H, int lds_max) {
@@ -396,7 +396,8 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   p->dev.rev_d = reinterpret_cast<const int*>(d + off_i[0]);
   p->dev.irev_h = reinterpret_cast<const int*>(d + off_i[1]);
   p->dev.irev_w = reinterpret_cast<const int*>(d + off_i[2]);
-  p->rset = rset_of(p->host);
+  p->rset_h = needs_all(p->host.ax[0]) ? RS_ALL : RS_SMALL;
+  p->rset_wd = (needs_all(p->host.ax[1]) || needs_all(p->host.ax[2])) ? RS_ALL : RS_SMALL;
   *out = p;
   return TB_OK;
 }
@@ -432,7 +433,7 @@ static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, 
   return TB_OK;
 }
 
-template <int RS>
+template <int RA, int RB>
 static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
                          void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops, uint32_t* minmax,
                          void* stream) {
@@ -452,9 +453,9 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
   const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
   const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
   const size_t lds_s = (size_t)slab_geo(W, D).total_cf * sizeof(cf);
-  int rc = set_lds(k_kspace<NT_TILE, RS>, lds_b);
+  int rc = set_lds(k_kspace<NT_TILE, RB>, lds_b);
   if (rc) return rc;
-  rc = set_lds(k_slab_inv<NT_SLAB, RS>, lds_s);
+  rc = set_lds(k_slab_inv<NT_SLAB, RA>, lds_s);
   if (rc) return rc;
   // launch groups of <= TB_MAX_BATCH samples (the op programs travel in the kernel arguments)
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
@@ -464,18 +465,18 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
     {
       Timer t(0, st);
-      rc = launch_slab_fwd<RS>(p, x, xs, S, b0 * C, nb * C, st);
+      rc = launch_slab_fwd<RA>(p, x, xs, S, b0 * C, nb * C, st);
       if (rc) return rc;
     }
     {
       Timer t(1, st);
-      hipLaunchKernelGGL((k_kspace<NT_TILE, RS>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C, T,
+      hipLaunchKernelGGL((k_kspace<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C, T,
                          bo);
       TB_HIP(hipGetLastError());
     }
     {
       Timer t(2, st);
-      hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RS>), dim3(H, nb * C), dim3(NT_SLAB), lds_s, st, p->dev, S, y, ys[0], ys[1],
+      hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RA>), dim3(H, nb * C), dim3(NT_SLAB), lds_s, st, p->dev, S, y, ys[0], ys[1],
                          ys[2], y_pad, b0 * C, C, scale, minmax);
       TB_HIP(hipGetLastError());
     }
@@ -483,7 +484,7 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
   return TB_OK;
 }
 
-template <int RS>
+template <int RA, int RB>
 static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, void* ws, size_t ws_bytes, int B,
                              int C, const tb_sample_ops* ops, double* out, void* stream) {
   if (!p || !x || !xs || !ops || !out || B < 1 || C < 1) return TB_ERR_INVALID_ARG;
@@ -494,7 +495,7 @@ static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, voi
   const int T = pick_tile(H, p->lds_max);
   const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
   const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
-  int rc = set_lds(k_kspace_stats<NT_TILE, RS>, lds_b);
+  int rc = set_lds(k_kspace_stats<NT_TILE, RB>, lds_b);
   if (rc) return rc;
   TB_HIP(hipMemsetAsync(out, 0, sizeof(double) * B * C, st));
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
@@ -502,9 +503,9 @@ static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, voi
     BatchOps bo;
     std::memset(&bo, 0, sizeof(bo));
     for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
-    rc = launch_slab_fwd<RS>(p, x, xs, S, b0 * C, nb * C, st);
+    rc = launch_slab_fwd<RA>(p, x, xs, S, b0 * C, nb * C, st);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_kspace_stats<NT_TILE, RS>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C,
+    hipLaunchKernelGGL((k_kspace_stats<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C,
                        T, bo, out);
     TB_HIP(hipGetLastError());
   }
@@ -515,15 +516,21 @@ int tb_kspace_filter_f32(const tb_plan* p, const float* x, const int64_t* xs, fl
                          void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops, uint32_t* minmax,
                          void* stream) {
   if (!p) return TB_ERR_INVALID_ARG;
-  return p->rset == RS_SMALL ? kspace_filter<RS_SMALL>(p, x, xs, y, ys, y_pad, ws, ws_bytes, B, C, ops, minmax, stream)
-                             : kspace_filter<RS_ALL>(p, x, xs, y, ys, y_pad, ws, ws_bytes, B, C, ops, minmax, stream);
+#define TB_ARGS p, x, xs, y, ys, y_pad, ws, ws_bytes, B, C, ops, minmax, stream
+  if (p->rset_wd == RS_SMALL)
+    return p->rset_h == RS_SMALL ? kspace_filter<RS_SMALL, RS_SMALL>(TB_ARGS) : kspace_filter<RS_SMALL, RS_ALL>(TB_ARGS);
+  return p->rset_h == RS_SMALL ? kspace_filter<RS_ALL, RS_SMALL>(TB_ARGS) : kspace_filter<RS_ALL, RS_ALL>(TB_ARGS);
+#undef TB_ARGS
 }
 
 int tb_kspace_logabs_sum_f32(const tb_plan* p, const float* x, const int64_t* xs, void* ws, size_t ws_bytes, int B,
                              int C, const tb_sample_ops* ops, double* out, void* stream) {
   if (!p) return TB_ERR_INVALID_ARG;
-  return p->rset == RS_SMALL ? kspace_stats<RS_SMALL>(p, x, xs, ws, ws_bytes, B, C, ops, out, stream)
-                             : kspace_stats<RS_ALL>(p, x, xs, ws, ws_bytes, B, C, ops, out, stream);
+#define TB_ARGS p, x, xs, ws, ws_bytes, B, C, ops, out, stream
+  if (p->rset_wd == RS_SMALL)
+    return p->rset_h == RS_SMALL ? kspace_stats<RS_SMALL, RS_SMALL>(TB_ARGS) : kspace_stats<RS_SMALL, RS_ALL>(TB_ARGS);
+  return p->rset_h == RS_SMALL ? kspace_stats<RS_ALL, RS_SMALL>(TB_ARGS) : kspace_stats<RS_ALL, RS_ALL>(TB_ARGS);
+#undef TB_ARGS
 }
 
 int tb_minmax_f32(const float* x, uint32_t* mm, int B, int64_t rows, int len, int64_t ld, int64_t sb, void* stream) {

@@ -15,7 +15,9 @@ Blocks (MONAI 0.5 semantics):
   conv, 1^3 conv when only the channel count changes, else identity), summed;
 * ``SkipConnection`` = cat([x, sub(x)], dim=1).
 
-It runs on PyTorch-ROCm (MIOpen convolutions); nothing here is a custom kernel.
+It runs on PyTorch-ROCm (MIOpen/CK forward and input-gradient convolutions); the weight
+gradient of the long-reduction 3x3x3 layers runs on the texbias split-K MFMA kernel
+(``texbias.conv``), the one U-Net op where MIOpen has no usable gfx950 path.
 """
 from __future__ import annotations
 
@@ -23,6 +25,8 @@ from typing import Sequence
 
 import torch
 import torch.nn as nn
+
+from .conv import Conv3d, ConvTranspose3d
 
 
 class ADN(nn.Sequential):
@@ -39,9 +43,9 @@ class Convolution(nn.Sequential):
         super().__init__()
         pad = (kernel_size - 1) // 2
         if is_transposed:
-            conv = nn.ConvTranspose3d(cin, cout, kernel_size, stride=strides, padding=pad, output_padding=strides - 1)
+            conv = ConvTranspose3d(cin, cout, kernel_size, stride=strides, padding=pad, output_padding=strides - 1)
         else:
-            conv = nn.Conv3d(cin, cout, kernel_size, stride=strides, padding=pad)
+            conv = Conv3d(cin, cout, kernel_size, stride=strides, padding=pad)
         self.add_module("conv", conv)
         if not conv_only:
             self.add_module("adn", ADN(cout, dropout))
@@ -61,7 +65,7 @@ class ResidualUnit(nn.Module):
             sch, sst = cout, 1
         if strides != 1 or cin != cout:
             k, p = (kernel_size, (kernel_size - 1) // 2) if strides != 1 else (1, 0)
-            self.residual = nn.Conv3d(cin, cout, k, stride=strides, padding=p)
+            self.residual = Conv3d(cin, cout, k, stride=strides, padding=p)
         else:
             self.residual = nn.Identity()
 
