@@ -1,2 +1,6 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 1000 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --cudnn-benchmark > gpurun_out/bench_cb.json 2> gpurun_out/bench_cb.err; echo cb rc=$?
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu4.log 2>&1; echo pytest rc=$?
+for tb in 65536 32768 16384; do
+TEXBIAS_TILE_BYTES=$tb timeout -k 10 300 python bench.py --filter-only --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/bench_filter_t$tb.json 2> gpurun_out/bench_filter_t$tb.err || exit 1
+done
+echo done

@@ -231,6 +231,27 @@ struct FastDiv {
   }
 };
 
+// ------------------------------------------------------------ batched copies
+// Global <-> LDS copies issue U independent loads per thread before their first use, so a
+// workgroup keeps U * nthreads requests in flight instead of waiting out HBM latency per element.
+template <int U, class Ctx, class LoadF, class StoreF>
+TB_HD void copy_batched(Ctx& ctx, int n, LoadF ld, StoreF st) {
+  for (int b0 = ctx.tid; b0 < n; b0 += ctx.nthreads * U) {
+    cf v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = b0 + u * ctx.nthreads;
+      if (t < n) v[u] = ld(t);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = b0 + u * ctx.nthreads;
+      if (t < n) st(t, v[u]);
+    }
+  }
+}
+constexpr int kCopyUnroll = 8;
+
 // ------------------------------------------------------------ addressing
 // pen(p) binds pencil p once per butterfly; pen(i) is then one multiply-add per element.
 struct RowAddr {  // pair pencils along D: element d of pair p at p*PR + d
@@ -596,13 +617,19 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
   const float* xb = x + bc * sx_bc + h * sx_h;
   const int nload = g.NP * D;
   const FastDiv fD = FastDiv::make(D), fDh = FastDiv::make(Dh);
-  for (int t = ctx.tid; t < nload; t += ctx.nthreads) {
-    const int p = fD.div(t), d = t - p * D;
-    const int w0 = 2 * p;
-    const float a = xb[w0 * sx_w + d];
-    const float b = (w0 + 1 < W) ? xb[(w0 + 1) * sx_w + d] : 0.f;
-    lds[p * g.PR + d] = mk(a, b);
-  }
+  copy_batched<kCopyUnroll>(
+      ctx, nload,
+      [&](int t) {
+        const int p = fD.div(t), d = t - p * D;
+        const int w0 = 2 * p;
+        const float a = xb[w0 * sx_w + d];
+        const float b = (w0 + 1 < W) ? xb[(w0 + 1) * sx_w + d] : 0.f;
+        return mk(a, b);
+      },
+      [&](int t, cf v) {
+        const int p = fD.div(t);
+        lds[p * g.PR + (t - p * D)] = v;
+      });
   ctx.sync();
   fft_dif<Ctx, RS>(ctx, lds, twd, pl.ax[2], g.NP, RowAddr{g.PR}, false);
   // unpack the pair spectra in place (each unit owns the two slots it reads)
@@ -631,10 +658,13 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
   // store S[bc][h][w'*Dh + kd]
   cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
   const int nst = W * Dh;
-  for (int t = ctx.tid; t < nst; t += ctx.nthreads) {
-    const int w = fDh.div(t), kd = t - w * Dh;
-    Sb[t] = lds[ca(kd, w)];
-  }
+  copy_batched<kCopyUnroll>(
+      ctx, nst,
+      [&](int t) {
+        const int w = fDh.div(t), kd = t - w * Dh;
+        return lds[ca(kd, w)];
+      },
+      [&](int t, cf v) { Sb[t] = v; });
 }
 
 // --------------------------------------------------------------- pass B
@@ -652,10 +682,16 @@ TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict_
   cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
   const int nl = H * nc;
   const FastDiv fnc = FastDiv::make(nc), fDh = FastDiv::make(Dh);
-  for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
-    const int hh = fnc.div(t), c = t - hh * nc;
-    lds[hh * T + c] = Sb[(int64_t)hh * ncols_all + c];
-  }
+  copy_batched<kCopyUnroll>(
+      ctx, nl,
+      [&](int t) {
+        const int hh = fnc.div(t), c = t - hh * nc;
+        return Sb[(int64_t)hh * ncols_all + c];
+      },
+      [&](int t, cf v) {
+        const int hh = fnc.div(t), c = t - hh * nc;
+        lds[hh * T + c] = v;
+      });
   ctx.sync();
   const TileAddr ta{T};
   fft_dif<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
@@ -669,10 +705,16 @@ TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict_
   }
   ctx.sync();
   fft_dit<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
-  for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
-    const int hh = fnc.div(t), c = t - hh * nc;
-    Sb[(int64_t)hh * ncols_all + c] = lds[hh * T + c];
-  }
+  copy_batched<kCopyUnroll>(
+      ctx, nl,
+      [&](int t) {
+        const int hh = fnc.div(t), c = t - hh * nc;
+        return lds[hh * T + c];
+      },
+      [&](int t, cf v) {
+        const int hh = fnc.div(t), c = t - hh * nc;
+        Sb[(int64_t)hh * ncols_all + c] = v;
+      });
 }
 
 // --------------------------------------------------------------- pass C
@@ -701,10 +743,12 @@ TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __res
   const cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
   const int nst = W * Dh;
   const FastDiv fDh = FastDiv::make(Dh);
-  for (int t = ctx.tid; t < nst; t += ctx.nthreads) {
-    const int w = fDh.div(t), kd = t - w * Dh;
-    lds[ca(kd, w)] = Sb[t];
-  }
+  copy_batched<kCopyUnroll>(
+      ctx, nst, [&](int t) { return Sb[t]; },
+      [&](int t, cf v) {
+        const int w = fDh.div(t), kd = t - w * Dh;
+        lds[ca(kd, w)] = v;
+      });
   ctx.sync();
   fft_dit<Ctx, RS>(ctx, lds, tww, pl.ax[1], Dh, ca, true);
   // repack rows (2p, 2p+1) into the pair spectrum z = X_a + i X_b (digit-reversed slots)
@@ -731,17 +775,23 @@ TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __res
   const int nout = W * ldw;
   const FastDiv fld = FastDiv::make(ldw);
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  for (int t = ctx.tid; t < nout; t += ctx.nthreads) {
-    const int w = fld.div(t), d = t - w * ldw;
-    float v = 0.f;
-    if (d < D) {
-      const cf z = lds[(w >> 1) * g.PR + d];
-      v = ((w & 1) ? z.y : z.x) * scale;
-      lo = v < lo ? v : lo;
-      hi = v > hi ? v : hi;
-    }
-    yb[w * sy_w + d] = v;
-  }
+  copy_batched<kCopyUnroll>(
+      ctx, nout,
+      [&](int t) {
+        const int w = fld.div(t), d = t - w * ldw;
+        float v = 0.f;
+        if (d < D) {
+          const cf z = lds[(w >> 1) * g.PR + d];
+          v = ((w & 1) ? z.y : z.x) * scale;
+          lo = v < lo ? v : lo;
+          hi = v > hi ? v : hi;
+        }
+        return mk(v, 0.f);
+      },
+      [&](int t, cf v) {
+        const int w = fld.div(t), d = t - w * ldw;
+        yb[w * sy_w + d] = v.x;
+      });
   *vmin = lo;
   *vmax = hi;
 }

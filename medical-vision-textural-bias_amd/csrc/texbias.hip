@@ -10,6 +10,7 @@
 //   D  k_salt_pepper  Philox u, class, sparse in-place MIN/MAX scatter.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -315,7 +316,12 @@ bool needs_all(const tb_axis& ax) {
 
 int pick_tile(int H, int lds_max) {
   // ~64 KB tiles: two workgroups per CU, >= 256 B contiguous per row segment when H <= 256
-  int T = 65536 / (H * 8);
+  // (TEXBIAS_TILE_BYTES overrides the budget for tuning)
+  static const int budget = [] {
+    const char* e = std::getenv("TEXBIAS_TILE_BYTES");
+    return e ? std::atoi(e) : 65536;
+  }();
+  int T = budget / (H * 8);
   if (T > 64) T = 64;
   if (T < 4) T = 4;
   while (tile_geo(H, T).total_cf * 8 > lds_max && T > 1) --T;

@@ -24,7 +24,8 @@ def _grads(mod, x):
 @pytest.mark.parametrize("cin,cout,stride,shape", [(4, 16, 2, (2, 24, 20, 36)), (16, 16, 1, (2, 12, 10, 40)),
                                                     (3, 3, 1, (1, 16, 16, 33)), (20, 5, 1, (2, 10, 12, 18)),
                                                     (32, 24, 2, (1, 16, 16, 70))])
-def test_conv3d_wgrad(conv, cin, cout, stride, shape):
+def test_conv3d_wgrad(conv, cin, cout, stride, shape, monkeypatch):
+    monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)
     torch.manual_seed(0)
     ref = nn.Conv3d(cin, cout, 3, stride=stride, padding=1).cuda()
     ours = conv.Conv3d(cin, cout, 3, stride=stride, padding=1).cuda()
@@ -42,22 +43,19 @@ def test_conv3d_wgrad(conv, cin, cout, stride, shape):
     torch.testing.assert_close(gwo, gwr, rtol=1e-4, atol=1e-3 * gwr.abs().max().item())
 
 
-@pytest.mark.parametrize("cin,cout,shape", [(32, 3, (2, 12, 10, 20)), (64, 16, (1, 10, 8, 16))])
-def test_convtranspose3d_wgrad(conv, cin, cout, shape):
+@pytest.mark.parametrize("cin,cout,shape", [(32, 3, (2, 12, 10, 20)), (64, 16, (1, 12, 10, 16))])
+def test_convtranspose3d_wgrad(conv, cin, cout, shape, monkeypatch):
+    monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)
     torch.manual_seed(0)
     ref = nn.ConvTranspose3d(cin, cout, 3, stride=2, padding=1, output_padding=1).cuda()
     ours = conv.ConvTranspose3d(cin, cout, 3, stride=2, padding=1, output_padding=1).cuda()
     ours.load_state_dict(ref.state_dict())
-    conv.MIN_K_PER_OUTPUT, old = 1, conv.MIN_K_PER_OUTPUT
-    try:
-        x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
-        assert conv.fast_wgrad_applies(x, ours.weight, None, ours.stride, ours.padding, True)
-        torch.manual_seed(1)
-        yr, gxr, gwr, gbr = _grads(ref, x)
-        torch.manual_seed(1)
-        yo, gxo, gwo, gbo = _grads(ours, x)
-    finally:
-        conv.MIN_K_PER_OUTPUT = old
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
+    assert conv.fast_wgrad_applies(x, ours.weight, None, ours.stride, ours.padding, True)
+    torch.manual_seed(1)
+    yr, gxr, gwr, gbr = _grads(ref, x)
+    torch.manual_seed(1)
+    yo, gxo, gwo, gbo = _grads(ours, x)
     torch.testing.assert_close(yo, yr)
     torch.testing.assert_close(gxo, gxr)
     torch.testing.assert_close(gwo, gwr, rtol=1e-4, atol=1e-3 * gwr.abs().max().item())
