@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--pad-to", type=int, default=160, help="U-Net D extent (G10: 155 is not /16)")
     ap.add_argument("--random-filters", action="store_true")
     ap.add_argument("--channels-last", action="store_true")
-    ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen find (exhaustive solver search)")
+    ap.add_argument("--no-cudnn-benchmark", action="store_true",
+                    help="skip MIOpen Find (its exhaustive solver search makes the first step slow, the rest fast)")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-vols", type=int, default=1)
@@ -117,7 +118,7 @@ def main():
 
     step_fn = None
     if not args.filter_only:
-        torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
+        torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
         step_fn = TrainStep(reference_model(C, 3), dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb,
                             channels_last=args.channels_last)
 

@@ -271,6 +271,36 @@ struct TileAddr {  // H pencils of the pass-B tile: element h of column c at h*T
   TB_HD Pen pen(int c) const { return Pen{c, T}; }
 };
 
+// Accessors: acc.pen(p) -> {ld(i), st(i, v)} for element i of pencil p.  A stage reads through
+// one accessor and writes through another, so the first stage of an axis can read HBM straight
+// into registers and the last can write HBM from registers (no staging round trip through LDS).
+template <class AddrF>
+struct LdsAcc {
+  cf* lds;
+  AddrF addr;
+  struct Pen {
+    cf* lds;
+    typename AddrF::Pen a;
+    TB_HD cf ld(int i) const { return lds[a(i)]; }
+    TB_HD void st(int i, cf v) const { lds[a(i)] = v; }
+  };
+  TB_HD Pen pen(int p) const { return Pen{lds, addr.pen(p)}; }
+};
+template <class AddrF>
+TB_HD LdsAcc<AddrF> lds_acc(cf* lds, AddrF a) { return LdsAcc<AddrF>{lds, a}; }
+
+struct StridedAcc {  // pencil p: base + p * pstride, element stride estride (complex, global)
+  cf* base;
+  int64_t pstride, estride;
+  struct Pen {
+    cf* b;
+    int64_t es;
+    TB_HD cf ld(int i) const { return b[i * es]; }
+    TB_HD void st(int i, cf v) const { b[i * es] = v; }
+  };
+  TB_HD Pen pen(int p) const { return Pen{base + p * pstride, estride}; }
+};
+
 // ------------------------------------------------------ in-place stages
 // Mixed-radix in-place DIF (Sande-Tukey).  Stage s (radix r, block length Lb,
 // P = n/Lb = product of previous radices, L = Lb/r):
@@ -314,22 +344,45 @@ template <int R> struct IsStreamed {
   static constexpr bool value = (R == 11 || R == 13 || R == 17 || R == 19 || R == 23 || R == 29 || R == 31);
 };
 
-template <class Ctx, int R, bool FWD, class AddrF>
-TB_HD void stage_r(Ctx& ctx, cf* lds, const cf* tw, int Lb, int P, int npen, int nb, AddrF addr,
-                   bool pencil_fast) {
-  const int L = Lb / R;
-  const int total = npen * nb;
-  const FastDiv dpen = FastDiv::make(npen), dnb = FastDiv::make(nb), dL = FastDiv::make(L);
-  for (int t = ctx.tid; t < total; t += ctx.nthreads) {
-    int p, u;
+struct StageGeo {  // butterfly -> (pencil, base position) for one stage
+  int L, Lb, npen, nb;
+  FastDiv dpen, dnb, dL;
+  bool pencil_fast;
+  TB_HD static StageGeo make(int R, int Lb, int npen, int n, bool pf) {
+    StageGeo g;
+    g.Lb = Lb;
+    g.L = Lb / R;
+    g.npen = npen;
+    g.nb = n / R;
+    g.dpen = FastDiv::make(npen);
+    g.dnb = FastDiv::make(g.nb);
+    g.dL = FastDiv::make(g.L);
+    g.pencil_fast = pf;
+    return g;
+  }
+  TB_HD void map(int t, int& p, int& base, int& j) const {
+    int u;
     if (pencil_fast) { u = dpen.div(t); p = t - u * npen; }
     else { p = dnb.div(t); u = t - p * nb; }
-    const int blk = dL.div(u), j = u - blk * L;
-    const int base = blk * Lb + j;
-    const auto pen = addr.pen(p);
+    const int blk = dL.div(u);
+    j = u - blk * L;
+    base = blk * Lb + j;
+  }
+};
+
+template <class Ctx, int R, bool FWD, class Src, class Dst>
+TB_HD void stage_r(Ctx& ctx, Src src, Dst dst, const cf* tw, int Lb, int P, int npen, int n, bool pencil_fast) {
+  const StageGeo g = StageGeo::make(R, Lb, npen, n, pencil_fast);
+  const int L = g.L;
+  const int total = npen * g.nb;
+  for (int t = ctx.tid; t < total; t += ctx.nthreads) {
+    int p, base, j;
+    g.map(t, p, base, j);
+    const auto sp = src.pen(p);
+    const auto dp = dst.pen(p);
     cf a[R];
 #pragma unroll
-    for (int q = 0; q < R; ++q) a[q] = lds[pen(base + q * L)];
+    for (int q = 0; q < R; ++q) a[q] = sp.ld(base + q * L);
     if constexpr (IsStreamed<R>::value) {
       if (!FWD && j) {
 #pragma unroll
@@ -337,7 +390,7 @@ TB_HD void stage_r(Ctx& ctx, cf* lds, const cf* tw, int Lb, int P, int npen, int
       }
       dft_odd_stream<R, FWD>(a, [&](int q, cf v) {
         if (FWD && j && q) v = mul(v, tw[j * q * P]);
-        lds[pen(base + q * L)] = v;
+        dp.st(base + q * L, v);
       });
     } else {
       if (FWD) {
@@ -354,57 +407,98 @@ TB_HD void stage_r(Ctx& ctx, cf* lds, const cf* tw, int Lb, int P, int npen, int
         Dft<R, false>::run(a);
       }
 #pragma unroll
-      for (int q = 0; q < R; ++q) lds[pen(base + q * L)] = a[q];
+      for (int q = 0; q < R; ++q) dp.st(base + q * L, a[q]);
     }
+  }
+}
+
+// last forward stage + per-coefficient ops + first inverse stage, in registers.  The last DIF
+// stage has L = 1 and j = 0 (no twiddles): its butterfly groups are exactly the groups of the
+// first DIT stage, so forward DFT -> ops(position) -> inverse DFT never leaves the thread.
+template <class Ctx, int R, class Src, class Dst, class OpsF>
+TB_HD void stage_mid_r(Ctx& ctx, Src src, Dst dst, int npen, int n, OpsF ops, bool pencil_fast) {
+  const StageGeo g = StageGeo::make(R, R, npen, n, pencil_fast);
+  const int total = npen * g.nb;
+  for (int t = ctx.tid; t < total; t += ctx.nthreads) {
+    int p, base, j;
+    g.map(t, p, base, j);
+    const auto sp = src.pen(p);
+    const auto dp = dst.pen(p);
+    cf a[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) a[q] = sp.ld(base + q);
+    Dft<R, true>::run(a);
+#pragma unroll
+    for (int q = 0; q < R; ++q) a[q] = ops(p, base + q, a[q]);
+    Dft<R, false>::run(a);
+#pragma unroll
+    for (int q = 0; q < R; ++q) dp.st(base + q, a[q]);
   }
 }
 
 // Radix sets compiled into a kernel: RS 0 = {2..10, 12, 15, 16} (small register
 // footprint), RS 1 adds the primes 11..31 (needed e.g. for D = 155 = 5 * 31).
-template <class Ctx, bool FWD, int RS, class AddrF>
-TB_HD void stage(Ctx& ctx, cf* lds, const cf* tw, int r, int Lb, int P, int npen, int n, AddrF addr,
-                 bool pencil_fast) {
-  const int nb = n / r;
-  switch (r) {
-#define TB_CASE(R) case R: stage_r<Ctx, R, FWD>(ctx, lds, tw, Lb, P, npen, nb, addr, pencil_fast); break;
-    TB_CASE(2) TB_CASE(3) TB_CASE(4) TB_CASE(5) TB_CASE(6) TB_CASE(7) TB_CASE(8) TB_CASE(9)
-    TB_CASE(10) TB_CASE(12) TB_CASE(15) TB_CASE(16)
-    default:
-      if constexpr (RS == 1) {
-        switch (r) {
-          TB_CASE(11) TB_CASE(13) TB_CASE(17) TB_CASE(19) TB_CASE(23) TB_CASE(29) TB_CASE(31)
-          default: break;
-        }
-      }
-      break;  // anything else is rejected at plan time
-#undef TB_CASE
+#define TB_SMALL_RADICES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(12) X(15) X(16)
+#define TB_PRIME_RADICES(X) X(11) X(13) X(17) X(19) X(23) X(29) X(31)
+
+template <class Ctx, bool FWD, int RS, class Src, class Dst>
+TB_HD void stage(Ctx& ctx, Src src, Dst dst, const cf* tw, int r, int Lb, int P, int npen, int n, bool pf) {
+#define TB_CASE(R) case R: stage_r<Ctx, R, FWD>(ctx, src, dst, tw, Lb, P, npen, n, pf); return;
+  switch (r) { TB_SMALL_RADICES(TB_CASE) default: break; }
+  if constexpr (RS == 1) {
+    switch (r) { TB_PRIME_RADICES(TB_CASE) default: break; }
   }
+#undef TB_CASE
 }
 
-// forward DIF over all stages (natural in -> digit-reversed out)
-template <class Ctx, int RS, class AddrF>
-TB_HD void fft_dif(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen, AddrF addr, bool pencil_fast) {
+template <class Ctx, int RS, class Src, class Dst, class OpsF>
+TB_HD void stage_mid(Ctx& ctx, Src src, Dst dst, int r, int npen, int n, OpsF ops, bool pf) {
+#define TB_CASE(R) case R: stage_mid_r<Ctx, R>(ctx, src, dst, npen, n, ops, pf); return;
+  switch (r) { TB_SMALL_RADICES(TB_CASE) default: break; }
+  if constexpr (RS == 1) {
+    switch (r) { TB_PRIME_RADICES(TB_CASE) default: break; }
+  }
+#undef TB_CASE
+}
+
+TB_HD int prefix_product(const tb_axis& ax, int s) {
   int P = 1;
-  for (int s = 0; s < ax.nst; ++s) {
+  for (int i = 0; i < s; ++i) P *= ax.radix[i];
+  return P;
+}
+
+// forward DIF stages [s0, s1) in place through `acc`, a barrier after each
+template <class Ctx, int RS, class Acc>
+TB_HD void dif_stages(Ctx& ctx, Acc acc, const cf* tw, const tb_axis& ax, int s0, int s1, int npen, bool pf) {
+  int P = prefix_product(ax, s0);
+  for (int s = s0; s < s1; ++s) {
     const int r = ax.radix[s];
-    const int Lb = ax.n / P;
-    stage<Ctx, true, RS>(ctx, lds, tw, r, Lb, P, npen, ax.n, addr, pencil_fast);
+    stage<Ctx, true, RS>(ctx, acc, acc, tw, r, ax.n / P, P, npen, ax.n, pf);
     ctx.sync();
     P *= r;
   }
 }
 
-// inverse DIT over all stages (digit-reversed in -> natural out), unnormalised
-template <class Ctx, int RS, class AddrF>
-TB_HD void fft_dit(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen, AddrF addr, bool pencil_fast) {
-  int P = ax.n;
-  for (int s = ax.nst - 1; s >= 0; --s) {
+// inverse DIT stages s1-1 down to s0 in place through `acc`, a barrier after each
+template <class Ctx, int RS, class Acc>
+TB_HD void dit_stages(Ctx& ctx, Acc acc, const cf* tw, const tb_axis& ax, int s0, int s1, int npen, bool pf) {
+  int P = prefix_product(ax, s1);
+  for (int s = s1 - 1; s >= s0; --s) {
     const int r = ax.radix[s];
     P /= r;
-    const int Lb = ax.n / P;
-    stage<Ctx, false, RS>(ctx, lds, tw, r, Lb, P, npen, ax.n, addr, pencil_fast);
+    stage<Ctx, false, RS>(ctx, acc, acc, tw, r, ax.n / P, P, npen, ax.n, pf);
     ctx.sync();
   }
+}
+
+// whole-axis transforms through one accessor (used by the stats kernel and the tests)
+template <class Ctx, int RS, class AddrF>
+TB_HD void fft_dif(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen, AddrF addr, bool pf) {
+  dif_stages<Ctx, RS>(ctx, lds_acc(lds, addr), tw, ax, 0, ax.nst, npen, pf);
+}
+template <class Ctx, int RS, class AddrF>
+TB_HD void fft_dit(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen, AddrF addr, bool pf) {
+  dit_stages<Ctx, RS>(ctx, lds_acc(lds, addr), tw, ax, 0, ax.nst, npen, pf);
 }
 
 // ------------------------------------------------------------- k-space ops
@@ -498,7 +592,7 @@ TB_HD cf apply_ops(const tb_sample_ops& so, int chan, cf v, int kh, int kw, int 
   const int nkh = negk(kh, H), nkw = negk(kw, W), nkd = negk(kd, D);
   cf gbase = v;
   bool in_group = false;
-  for (int o = 0; o < so.n; ++o) {
+  for (int o = 0; o < so.n; ++o) {   // op fields come straight from the kernarg segment (scalar loads)
     const tb_op& op = so.op[o];
     if (op.kind == TB_OP_SPIKE) {
       if (!in_group || op.reserved != 1) gbase = v;
@@ -584,54 +678,119 @@ struct ColAddr {
   const int* posB;
   int PR, off_c0, off_cn, Dn, D;  // Dn = D/2 if D even else -1
   struct Pen {
-    int e, o, pitch;
-    TB_HD int operator()(int w) const { return (w >> 1) * pitch + ((w & 1) ? o : e); }
+    int e, d, pitch;  // even-row slot, odd-minus-even offset (arithmetic, not a select: hipcc
+                      // otherwise turns `w&1 ? o : e` into a dynamically indexed stack array)
+    TB_HD int operator()(int w) const { return (w >> 1) * pitch + e + (w & 1) * d; }
   };
   TB_HD Pen pen(int kd) const {
-    if (kd == 0) return Pen{off_c0, off_c0 + 1, 2};
-    if (kd == Dn) return Pen{off_cn, off_cn + 1, 2};
-    return Pen{posA[kd], posB[kd], PR};
+    if (kd == 0) return Pen{off_c0, 1, 2};
+    if (kd == Dn) return Pen{off_cn, 1, 2};
+    const int a = posA[kd];
+    return Pen{a, posB[kd] - a, PR};
   }
   TB_HD int operator()(int kd, int w) const { return pen(kd)(w); }
 };
 
-// --------------------------------------------------------------- pass A
-// forward: real slab x[bc][h][:][:] -> half spectrum S[bc][h][w'][kd]
-template <class Ctx, int RS>
-TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __restrict__ x, int64_t sx_bc,
-                       int64_t sx_h, int64_t sx_w, cf* __restrict__ S, int bc, int h) {
+// real pair rows of the slab as the source of the first D stage: z = x[2p] + i x[2p+1]
+struct PairSrc {
+  const float* xb;
+  int64_t sw;
+  int W;
+  struct Pen {
+    const float* r0;
+    const float* r1;
+    bool has1;
+    TB_HD cf ld(int i) const { return mk(r0[i], has1 ? r1[i] : 0.f); }
+    TB_HD void st(int, cf) const {}
+  };
+  TB_HD Pen pen(int p) const {
+    const float* r0 = xb + (int64_t)(2 * p) * sw;
+    return Pen{r0, r0 + sw, 2 * p + 1 < W};
+  }
+};
+
+// pair rows of the output as the sink of the last inverse D stage: scale, split re/im into
+// rows 2p / 2p+1, track the running min/max (salt-and-pepper MIN/MAX epilogue)
+struct PairDst {
+  float* yb;
+  int64_t sw;
+  int W;
+  float scale;
+  float* lo;
+  float* hi;
+  struct Pen {
+    float* r0;
+    float* r1;
+    bool has1;
+    float scale;
+    float* lo;
+    float* hi;
+    TB_HD cf ld(int) const { return mk(0.f, 0.f); }
+    TB_HD void st(int i, cf v) const {
+      const float a = v.x * scale;
+      r0[i] = a;
+      *lo = a < *lo ? a : *lo;
+      *hi = a > *hi ? a : *hi;
+      if (has1) {
+        const float b = v.y * scale;
+        r1[i] = b;
+        *lo = b < *lo ? b : *lo;
+        *hi = b > *hi ? b : *hi;
+      }
+    }
+  };
+  TB_HD Pen pen(int p) const {
+    float* r0 = yb + (int64_t)(2 * p) * sw;
+    return Pen{r0, r0 + sw, 2 * p + 1 < W, scale, lo, hi};
+  }
+};
+
+template <class Ctx>
+TB_HD void slab_tables(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const SlabGeo& g) {
   const int W = pl.W, D = pl.D, Dh = D / 2 + 1;
-  const SlabGeo g = slab_geo(W, D);
   cf* tww = lds + g.off_tww;
   cf* twd = lds + g.off_twd;
-  int* pos = reinterpret_cast<int*>(lds + g.off_pos);
-  int* posA = pos;
-  int* posB = pos + Dh;
+  int* posA = reinterpret_cast<int*>(lds + g.off_pos);
+  int* posB = posA + Dh;
   for (int i = ctx.tid; i < W; i += ctx.nthreads) tww[i] = pl.tw[1][i];
   for (int i = ctx.tid; i < D; i += ctx.nthreads) twd[i] = pl.tw[2][i];
   for (int i = ctx.tid; i < Dh; i += ctx.nthreads) {
     posA[i] = pl.rev_d[i];
     posB[i] = pl.rev_d[i == 0 ? 0 : D - i];
   }
-  // load pair rows
-  const float* xb = x + bc * sx_bc + h * sx_h;
-  const int nload = g.NP * D;
-  const FastDiv fD = FastDiv::make(D), fDh = FastDiv::make(Dh);
-  copy_batched<kCopyUnroll>(
-      ctx, nload,
-      [&](int t) {
-        const int p = fD.div(t), d = t - p * D;
-        const int w0 = 2 * p;
-        const float a = xb[w0 * sx_w + d];
-        const float b = (w0 + 1 < W) ? xb[(w0 + 1) * sx_w + d] : 0.f;
-        return mk(a, b);
-      },
-      [&](int t, cf v) {
-        const int p = fD.div(t);
-        lds[p * g.PR + (t - p * D)] = v;
-      });
   ctx.sync();
-  fft_dif<Ctx, RS>(ctx, lds, twd, pl.ax[2], g.NP, RowAddr{g.PR}, false);
+}
+
+// --------------------------------------------------------------- pass A
+// forward: real slab x[bc][h][:][:] -> half spectrum S[bc][h][w'][kd]
+//   D stage 0 reads HBM into registers, D stages 1.. in LDS, pair unpack in LDS,
+//   W stages 0..S-2 in LDS, the last W stage writes HBM from registers.
+template <class Ctx, int RS>
+TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __restrict__ x, int64_t sx_bc,
+                       int64_t sx_h, int64_t sx_w, cf* __restrict__ S, int bc, int h) {
+  const int W = pl.W, D = pl.D, Dh = D / 2 + 1;
+  const SlabGeo g = slab_geo(W, D);
+  slab_tables(ctx, lds, pl, g);
+  const cf* tww = lds + g.off_tww;
+  const cf* twd = lds + g.off_twd;
+  const int* posA = reinterpret_cast<const int*>(lds + g.off_pos);
+  const int* posB = posA + Dh;
+  const float* xb = x + bc * sx_bc + h * sx_h;
+  const tb_axis& axd = pl.ax[2];
+  const tb_axis& axw = pl.ax[1];
+  const auto rows = lds_acc(lds, RowAddr{g.PR});
+  const FastDiv fDh = FastDiv::make(Dh);
+  if (axd.nst == 0) {
+    const FastDiv fD = FastDiv::make(D);
+    copy_batched<kCopyUnroll>(
+        ctx, g.NP * D, [&](int t) { return PairSrc{xb, sx_w, W}.pen(fD.div(t)).ld(t - fD.div(t) * D); },
+        [&](int t, cf v) { lds[fD.div(t) * g.PR + (t - fD.div(t) * D)] = v; });
+    ctx.sync();
+  } else {
+    stage<Ctx, true, RS>(ctx, PairSrc{xb, sx_w, W}, rows, twd, axd.radix[0], D, 1, g.NP, D, false);
+    ctx.sync();
+    dif_stages<Ctx, RS>(ctx, rows, twd, axd, 1, axd.nst, g.NP, false);
+  }
   // unpack the pair spectra in place (each unit owns the two slots it reads)
   const int Dn = (D % 2 == 0) ? D / 2 : -1;
   const int nun = g.NP * Dh;
@@ -653,21 +812,24 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
     }
   }
   ctx.sync();
-  ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
-  fft_dif<Ctx, RS>(ctx, lds, tww, pl.ax[1], Dh, ca, true);
-  // store S[bc][h][w'*Dh + kd]
+  const ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
+  const auto cols = lds_acc(lds, ca);
   cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
-  const int nst = W * Dh;
-  copy_batched<kCopyUnroll>(
-      ctx, nst,
-      [&](int t) {
-        const int w = fDh.div(t), kd = t - w * Dh;
-        return lds[ca(kd, w)];
-      },
-      [&](int t, cf v) { Sb[t] = v; });
+  if (axw.nst == 0) {
+    copy_batched<kCopyUnroll>(
+        ctx, W * Dh, [&](int t) { const int w = fDh.div(t); return lds[ca(t - w * Dh, w)]; },
+        [&](int t, cf v) { Sb[t] = v; });
+  } else {
+    dif_stages<Ctx, RS>(ctx, cols, tww, axw, 0, axw.nst - 1, Dh, true);
+    const int sl = axw.nst - 1, P = prefix_product(axw, sl);
+    stage<Ctx, true, RS>(ctx, cols, StridedAcc{Sb, 1, Dh}, tww, axw.radix[sl], W / P, P, Dh, W, true);
+  }
 }
 
 // --------------------------------------------------------------- pass B
+// per (bc, tile of T spectrum columns): H stage 0 from HBM, H stages in LDS, the last forward
+// stage fused with the op program and the first inverse stage in registers, inverse stage 0
+// back to HBM.
 template <class Ctx, int RS>
 TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict__ S, int bc, int tile, int T,
                        const tb_sample_ops& so, int chan) {
@@ -679,78 +841,67 @@ TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict_
   cf* tw = lds + g.off_tw;
   int* irev = reinterpret_cast<int*>(lds + g.off_irev);
   for (int i = ctx.tid; i < H; i += ctx.nthreads) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
-  cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
-  const int nl = H * nc;
-  const FastDiv fnc = FastDiv::make(nc), fDh = FastDiv::make(Dh);
-  copy_batched<kCopyUnroll>(
-      ctx, nl,
-      [&](int t) {
-        const int hh = fnc.div(t), c = t - hh * nc;
-        return Sb[(int64_t)hh * ncols_all + c];
-      },
-      [&](int t, cf v) {
-        const int hh = fnc.div(t), c = t - hh * nc;
-        lds[hh * T + c] = v;
-      });
   ctx.sync();
-  const TileAddr ta{T};
-  fft_dif<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
-  for (int t = ctx.tid; t < nl; t += ctx.nthreads) {
-    const int hp = fnc.div(t), c = t - hp * nc;
+  cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
+  const StridedAcc gacc{Sb, 1, ncols_all};
+  const FastDiv fDh = FastDiv::make(Dh);
+  auto ops = [&](int c, int pos, cf v) {
     const int j = j0 + c;
     const int wp = fDh.div(j), kd = j - wp * Dh;
-    const int kh = irev[hp], kw = pl.irev_w[wp];
-    cf& v = lds[hp * T + c];
-    v = apply_ops(so, chan, v, kh, kw, kd, H, W, D);
+    return apply_ops(so, chan, v, irev[pos], pl.irev_w[wp], kd, H, W, D);
+  };
+  const tb_axis& ax = pl.ax[0];
+  if (ax.nst == 0) {  // H == 1: the op program alone
+    for (int t = ctx.tid; t < nc; t += ctx.nthreads) Sb[t] = ops(t, 0, Sb[t]);
+    return;
   }
+  if (ax.nst == 1) {  // one radix: HBM -> DFT -> ops -> IDFT -> HBM, no LDS round trip
+    stage_mid<Ctx, RS>(ctx, gacc, gacc, ax.radix[0], nc, H, ops, true);
+    return;
+  }
+  const auto la = lds_acc(lds, TileAddr{T});
+  stage<Ctx, true, RS>(ctx, gacc, la, tw, ax.radix[0], H, 1, nc, H, true);
   ctx.sync();
-  fft_dit<Ctx, RS>(ctx, lds, tw, pl.ax[0], nc, ta, true);
-  copy_batched<kCopyUnroll>(
-      ctx, nl,
-      [&](int t) {
-        const int hh = fnc.div(t), c = t - hh * nc;
-        return lds[hh * T + c];
-      },
-      [&](int t, cf v) {
-        const int hh = fnc.div(t), c = t - hh * nc;
-        Sb[(int64_t)hh * ncols_all + c] = v;
-      });
+  dif_stages<Ctx, RS>(ctx, la, tw, ax, 1, ax.nst - 1, nc, true);
+  stage_mid<Ctx, RS>(ctx, la, la, ax.radix[ax.nst - 1], nc, H, ops, true);
+  ctx.sync();
+  dit_stages<Ctx, RS>(ctx, la, tw, ax, 1, ax.nst - 1, nc, true);
+  stage<Ctx, false, RS>(ctx, la, gacc, tw, ax.radix[0], H, 1, nc, H, true);
 }
 
 // --------------------------------------------------------------- pass C
-// inverse: S[bc][h] -> y[bc][h][:][:] (scaled 1/N), pad columns [D, ldy) zeroed,
-// optional running (min, max) of the written values for salt-and-pepper.
+// inverse: S[bc][h] -> y[bc][h][:][:] (scaled 1/N), pad columns [D, D+ypad) zeroed,
+// running (min, max) of the written values for salt-and-pepper.
 template <class Ctx, int RS>
 TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __restrict__ S, float* __restrict__ y,
                        int64_t sy_bc, int64_t sy_h, int64_t sy_w, int ldy_pad, int bc, int h, float scale,
                        float* vmin, float* vmax) {
   const int W = pl.W, D = pl.D, Dh = D / 2 + 1;
   const SlabGeo g = slab_geo(W, D);
-  cf* tww = lds + g.off_tww;
-  cf* twd = lds + g.off_twd;
-  int* pos = reinterpret_cast<int*>(lds + g.off_pos);
-  int* posA = pos;
-  int* posB = pos + Dh;
-  for (int i = ctx.tid; i < W; i += ctx.nthreads) tww[i] = pl.tw[1][i];
-  for (int i = ctx.tid; i < D; i += ctx.nthreads) twd[i] = pl.tw[2][i];
-  for (int i = ctx.tid; i < Dh; i += ctx.nthreads) {
-    posA[i] = pl.rev_d[i];
-    posB[i] = pl.rev_d[i == 0 ? 0 : D - i];
-  }
-  ctx.sync();
+  slab_tables(ctx, lds, pl, g);
+  const cf* tww = lds + g.off_tww;
+  const cf* twd = lds + g.off_twd;
+  const int* posA = reinterpret_cast<const int*>(lds + g.off_pos);
+  const int* posB = posA + Dh;
   const int Dn = (D % 2 == 0) ? D / 2 : -1;
-  ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
-  const cf* Sb = S + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
-  const int nst = W * Dh;
+  const ColAddr ca{posA, posB, g.PR, g.off_c0, g.off_cn, Dn, D};
+  const auto cols = lds_acc(lds, ca);
+  const auto rows = lds_acc(lds, RowAddr{g.PR});
+  cf* Sb = const_cast<cf*>(S) + ((int64_t)bc * pl.H + h) * (int64_t)W * Dh;
+  const tb_axis& axd = pl.ax[2];
+  const tb_axis& axw = pl.ax[1];
   const FastDiv fDh = FastDiv::make(Dh);
-  copy_batched<kCopyUnroll>(
-      ctx, nst, [&](int t) { return Sb[t]; },
-      [&](int t, cf v) {
-        const int w = fDh.div(t), kd = t - w * Dh;
-        lds[ca(kd, w)] = v;
-      });
-  ctx.sync();
-  fft_dit<Ctx, RS>(ctx, lds, tww, pl.ax[1], Dh, ca, true);
+  if (axw.nst == 0) {
+    copy_batched<kCopyUnroll>(
+        ctx, W * Dh, [&](int t) { return Sb[t]; },
+        [&](int t, cf v) { const int w = fDh.div(t); lds[ca(t - w * Dh, w)] = v; });
+    ctx.sync();
+  } else {
+    const int sl = axw.nst - 1, P = prefix_product(axw, sl);
+    stage<Ctx, false, RS>(ctx, StridedAcc{Sb, 1, Dh}, cols, tww, axw.radix[sl], W / P, P, Dh, W, true);
+    ctx.sync();
+    dit_stages<Ctx, RS>(ctx, cols, tww, axw, 0, axw.nst - 1, Dh, true);
+  }
   // repack rows (2p, 2p+1) into the pair spectrum z = X_a + i X_b (digit-reversed slots)
   const int nun = g.NP * Dh;
   for (int t = ctx.tid; t < nun; t += ctx.nthreads) {
@@ -769,29 +920,28 @@ TB_HD void pass_c_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const cf* __res
     }
   }
   ctx.sync();
-  fft_dit<Ctx, RS>(ctx, lds, twd, pl.ax[2], g.NP, RowAddr{g.PR}, false);
   float* yb = y + bc * sy_bc + h * sy_h;
-  const int ldw = D + ldy_pad;
-  const int nout = W * ldw;
-  const FastDiv fld = FastDiv::make(ldw);
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  copy_batched<kCopyUnroll>(
-      ctx, nout,
-      [&](int t) {
-        const int w = fld.div(t), d = t - w * ldw;
-        float v = 0.f;
-        if (d < D) {
-          const cf z = lds[(w >> 1) * g.PR + d];
-          v = ((w & 1) ? z.y : z.x) * scale;
-          lo = v < lo ? v : lo;
-          hi = v > hi ? v : hi;
-        }
-        return mk(v, 0.f);
-      },
-      [&](int t, cf v) {
-        const int w = fld.div(t), d = t - w * ldw;
-        yb[w * sy_w + d] = v.x;
-      });
+  if (axd.nst == 0) {
+    for (int t = ctx.tid; t < W; t += ctx.nthreads) {
+      const cf z = lds[(t >> 1) * g.PR];
+      const float v = ((t & 1) ? z.y : z.x) * scale;
+      yb[t * sy_w] = v;
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
+  } else {
+    dit_stages<Ctx, RS>(ctx, rows, twd, axd, 1, axd.nst, g.NP, false);
+    stage<Ctx, false, RS>(ctx, rows, PairDst{yb, sy_w, W, scale, &lo, &hi}, twd, axd.radix[0], D, 1, g.NP, D,
+                          false);
+  }
+  if (ldy_pad > 0) {
+    const FastDiv fp = FastDiv::make(ldy_pad);
+    for (int t = ctx.tid; t < W * ldy_pad; t += ctx.nthreads) {
+      const int w = fp.div(t);
+      yb[w * sy_w + D + (t - w * ldy_pad)] = 0.f;
+    }
+  }
   *vmin = lo;
   *vmax = hi;
 }

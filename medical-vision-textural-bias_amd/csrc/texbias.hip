@@ -86,21 +86,44 @@ struct Timer {  // records [begin, end) of one pass when timing is enabled
 };
 
 // ---------------------------------------------------------------- kernels
-template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_slab_fwd(tb_plan_dev pl, const float* __restrict__ x, int64_t sbc,
-                                                 int64_t sh, int64_t sw, cf* __restrict__ S, int bc0) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  DevCtx ctx{(int)threadIdx.x, NT};
-  pass_a_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), pl, x, sbc, sh, sw, S, bc0 + (int)blockIdx.y, (int)blockIdx.x);
+// Every kernel takes ONE argument struct and reads it through the kernarg segment pointer:
+// dynamically indexed by-value parameters (the plan's radix lists, a sample's op program)
+// are otherwise copied to per-lane scratch memory (2.4 KB per lane for the op programs).
+template <class A>
+__device__ __forceinline__ const A& kargs() {
+  return *(const A*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
 }
 
+struct SlabFwdArgs {
+  tb_plan_dev pl;
+  const float* x;
+  int64_t sbc, sh, sw;
+  cf* S;
+  int bc0;
+};
 template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_kspace(tb_plan_dev pl, cf* __restrict__ S, int bc0, int C, int T,
-                                               BatchOps ops) {
+__global__ __launch_bounds__(NT) void k_slab_fwd(SlabFwdArgs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SlabFwdArgs& a = kargs<SlabFwdArgs>();
+  DevCtx ctx{(int)threadIdx.x, NT};
+  pass_a_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.x, a.sbc, a.sh, a.sw, a.S,
+                          a.bc0 + (int)blockIdx.y, (int)blockIdx.x);
+}
+
+struct KspaceArgs {
+  tb_plan_dev pl;
+  cf* S;
+  int bc0, C, T, pad;
+  BatchOps ops;
+};
+template <int NT, int RS>
+__global__ __launch_bounds__(NT) void k_kspace(KspaceArgs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const KspaceArgs& a = kargs<KspaceArgs>();
   DevCtx ctx{(int)threadIdx.x, NT};
   const int bcl = (int)blockIdx.y;
-  pass_b_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), pl, S, bc0 + bcl, (int)blockIdx.x, T, ops.s[bcl / C], bcl % C);
+  pass_b_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.S, a.bc0 + bcl, (int)blockIdx.x, a.T,
+                          a.ops.s[bcl / a.C], bcl % a.C);
 }
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -136,16 +159,25 @@ __device__ __forceinline__ void block_minmax_atomic(float lo, float hi, float* r
   }
 }
 
+struct SlabInvArgs {
+  tb_plan_dev pl;
+  const cf* S;
+  float* y;
+  int64_t sbc, sh, sw;
+  int ypad, bc0, C;
+  float scale;
+  uint32_t* mm;
+};
 template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_slab_inv(tb_plan_dev pl, const cf* __restrict__ S, float* __restrict__ y,
-                                                 int64_t sbc, int64_t sh, int64_t sw, int ypad, int bc0, int C,
-                                                 float scale, uint32_t* __restrict__ mm) {
+__global__ __launch_bounds__(NT) void k_slab_inv(SlabInvArgs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SlabInvArgs& a = kargs<SlabInvArgs>();
   DevCtx ctx{(int)threadIdx.x, NT};
-  const int bc = bc0 + (int)blockIdx.y;
+  const int bc = a.bc0 + (int)blockIdx.y;
   float lo, hi;
-  pass_c_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), pl, S, y, sbc, sh, sw, ypad, bc, (int)blockIdx.x, scale, &lo, &hi);
-  if (mm) block_minmax_atomic<NT>(lo, hi, reinterpret_cast<float*>(smem), mm + 2 * (bc / C));
+  pass_c_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.S, a.y, a.sbc, a.sh, a.sw, a.ypad, bc,
+                          (int)blockIdx.x, a.scale, &lo, &hi);
+  if (a.mm) block_minmax_atomic<NT>(lo, hi, reinterpret_cast<float*>(smem), a.mm + 2 * (bc / a.C));
 }
 
 __global__ void k_minmax_init(uint32_t* mm, int n) {
@@ -240,13 +272,22 @@ __global__ void k_disk_mask(float* __restrict__ m, int64_t outer, int n0, int n1
 }
 
 // log-abs statistics of the op-processed spectrum (default spike intensity)
+struct StatsArgs {
+  tb_plan_dev pl;
+  const cf* S;
+  int bc0, C, T, pad;
+  double* out;
+  BatchOps ops;
+};
 template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* __restrict__ S, int bc0, int C, int T,
-                                                     BatchOps ops, double* __restrict__ out) {
+__global__ __launch_bounds__(NT) void k_kspace_stats(StatsArgs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const StatsArgs& a = kargs<StatsArgs>();
+  const tb_plan_dev& pl = a.pl;
   cf* lds = reinterpret_cast<cf*>(smem);
   DevCtx ctx{(int)threadIdx.x, NT};
-  const int bcl = (int)blockIdx.y, bc = bc0 + bcl;
+  const int bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int T = a.T;
   const int H = pl.H, W = pl.W, D = pl.D, Dh = D / 2 + 1;
   const int ncols_all = W * Dh;
   const int j0 = (int)blockIdx.x * T;
@@ -255,7 +296,7 @@ __global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* _
   cf* tw = lds + g.off_tw;
   int* irev = reinterpret_cast<int*>(lds + g.off_irev);
   for (int i = threadIdx.x; i < H; i += NT) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
-  const cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
+  const cf* Sb = a.S + (int64_t)bc * H * ncols_all + j0;
   const int nl = H * nc;
   const FastDiv fnc = FastDiv::make(nc), fDh = FastDiv::make(Dh);
   for (int t = threadIdx.x; t < nl; t += NT) {
@@ -265,8 +306,8 @@ __global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* _
   __syncthreads();
   fft_dif<DevCtx, RS>(ctx, lds, tw, pl.ax[0], nc, TileAddr{T}, true);
   double acc = 0.0;
-  const tb_sample_ops& so = ops.s[bcl / C];
-  const int chan = bcl % C;
+  const tb_sample_ops& so = a.ops.s[bcl / a.C];
+  const int chan = bcl % a.C;
   const int Dtop = (D % 2 == 0) ? D / 2 : -1;
   for (int t = threadIdx.x; t < nl; t += NT) {
     const int hp = fnc.div(t), c = t - hp * nc;
@@ -284,7 +325,7 @@ __global__ __launch_bounds__(NT) void k_kspace_stats(tb_plan_dev pl, const cf* _
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < NT / 64; ++w) acc += red[w];
-    atomicAdd(&out[bc], acc);
+    atomicAdd(&a.out[bc], acc);
   }
 }
 
@@ -315,11 +356,11 @@ bool needs_all(const tb_axis& ax) {
 }
 
 int pick_tile(int H, int lds_max) {
-  // ~64 KB tiles: two workgroups per CU, >= 256 B contiguous per row segment when H <= 256
+  // ~32 KB tiles (measured best of 16/32/64 KB at H = 240: 4 workgroups per CU, 128-B rows)
   // (TEXBIAS_TILE_BYTES overrides the budget for tuning)
   static const int budget = [] {
     const char* e = std::getenv("TEXBIAS_TILE_BYTES");
-    return e ? std::atoi(e) : 65536;
+    return e ? std::atoi(e) : 32768;
   }();
   int T = budget / (H * 8);
   if (T > 64) T = 64;
@@ -433,8 +474,8 @@ static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, 
   const size_t lds = (size_t)slab_geo(p->dev.W, p->dev.D).total_cf * sizeof(cf);
   int rc = set_lds(k_slab_fwd<NT_SLAB, RS>, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL((k_slab_fwd<NT_SLAB, RS>), dim3(p->dev.H, nbc), dim3(NT_SLAB), lds, st, p->dev, x, xs[0],
-                     xs[1], xs[2], S, bc0);
+  SlabFwdArgs a{p->dev, x, xs[0], xs[1], xs[2], S, bc0};
+  hipLaunchKernelGGL((k_slab_fwd<NT_SLAB, RS>), dim3(p->dev.H, nbc), dim3(NT_SLAB), lds, st, a);
   TB_HIP(hipGetLastError());
   return TB_OK;
 }
@@ -476,14 +517,14 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     }
     {
       Timer t(1, st);
-      hipLaunchKernelGGL((k_kspace<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C, T,
-                         bo);
+      KspaceArgs ka{p->dev, S, b0 * C, C, T, 0, bo};
+      hipLaunchKernelGGL((k_kspace<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, ka);
       TB_HIP(hipGetLastError());
     }
     {
       Timer t(2, st);
-      hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RA>), dim3(H, nb * C), dim3(NT_SLAB), lds_s, st, p->dev, S, y, ys[0], ys[1],
-                         ys[2], y_pad, b0 * C, C, scale, minmax);
+      SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, b0 * C, C, scale, minmax};
+      hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RA>), dim3(H, nb * C), dim3(NT_SLAB), lds_s, st, ia);
       TB_HIP(hipGetLastError());
     }
   }
@@ -511,8 +552,8 @@ static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, voi
     for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
     rc = launch_slab_fwd<RA>(p, x, xs, S, b0 * C, nb * C, st);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_kspace_stats<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, p->dev, S, b0 * C, C,
-                       T, bo, out);
+    StatsArgs sa{p->dev, S, b0 * C, C, T, 0, out, bo};
+    hipLaunchKernelGGL((k_kspace_stats<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, sa);
     TB_HIP(hipGetLastError());
   }
   return TB_OK;

@@ -9,6 +9,7 @@ those of ``nn.Conv3d`` / ``nn.ConvTranspose3d``, so state dicts are interchangea
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -16,8 +17,10 @@ import torch.nn.functional as F
 
 from ._lib import check, lib
 
-# use the custom weight gradient when the reduction is long relative to the output tile
+# use the custom weight gradient when the reduction is long relative to the output tile;
+# TEXBIAS_WGRAD=0 leaves every layer to MIOpen (e.g. to compare with MIOpen's Find choice)
 MIN_K_PER_OUTPUT = 64
+ENABLED = os.environ.get("TEXBIAS_WGRAD", "1") != "0"
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -40,7 +43,7 @@ def wgrad(G: torch.Tensor, X: torch.Tensor, w_shape, stride: int, pad: int) -> t
 
 
 def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, padding, transposed: bool) -> bool:
-    if not (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32):
+    if not ENABLED or not (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32):
         return False
     if tuple(w.shape[2:]) != (3, 3, 3) or len(set(stride)) != 1 or stride[0] not in (1, 2) or len(set(padding)) != 1:
         return False
