@@ -428,8 +428,9 @@ TB_HD void stage_mid_r(Ctx& ctx, Src src, Dst dst, int npen, int n, OpsF ops, bo
 #pragma unroll
     for (int q = 0; q < R; ++q) a[q] = sp.ld(base + q);
     Dft<R, true>::run(a);
+    const auto cc = ops.col(p);   // geometry shared by the butterfly's R coefficients
 #pragma unroll
-    for (int q = 0; q < R; ++q) a[q] = ops(p, base + q, a[q]);
+    for (int q = 0; q < R; ++q) a[q] = ops(cc, base + q, a[q]);
     Dft<R, false>::run(a);
 #pragma unroll
     for (int q = 0; q < R; ++q) dp.st(base + q, a[q]);
@@ -507,29 +508,6 @@ TB_HD void fft_dit(Ctx& ctx, cf* lds, const cf* tw, const tb_axis& ax, int npen,
 TB_HD int shifted(int k, int n) { int s = k + n / 2; return s >= n ? s - n : s; }
 TB_HD int negk(int k, int n) { return k == 0 ? 0 : n - k; }
 
-// disk_mask (filters_and_operators.py:176-195): centre floor(n/2) of the shifted grid = DC;
-// integer sum of squares compared strictly (< r^2) in float32, or in int64 for an int r.
-TB_HD float disk_value(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
-  const int64_t dh = shifted(kh, H) - H / 2, dw = shifted(kw, W) - W / 2, dd = shifted(kd, D) - D / 2;
-  const int64_t s = dh * dh + dw * dw + dd * dd;
-  bool in;
-  if (op.i[0]) in = s < op.l;               // int radius: exact integer compare
-  else in = (float)s < op.f[0];             // float radius: float32 compare (s < 2^24 exact)
-  if (op.i[1]) in = !in;                    // inside_off
-  return in ? 1.f : 0.f;
-}
-
-// GibbsNoise mask (filters_and_operators.py:686-698): float64 geometry, centre (n-1)/2,
-// dist <= r.  4*(s-c)^2 = (2s-(n-1))^2 is an exact integer; the host turns
-// fl64(sqrt(t/4)) <= r into the integer threshold t <= T4 (op.l).
-TB_HD bool gibbs_in(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
-  const int64_t eh = 2 * shifted(kh, H) - (H - 1), ew = 2 * shifted(kw, W) - (W - 1),
-                ed = 2 * shifted(kd, D) - (D - 1);
-  return eh * eh + ew * ew + ed * ed <= op.l;
-}
-
-// GibbsNoiseLayer mask (stylization_layers.py:99-109): float32 geometry, centre (n-1)/2,
-// norm_dist = dist / (alpha * max dist); mask = !(norm_dist > 1)  (NaN -> 1, inf -> 0)
 // correctly rounded IEEE float32 division / square root (bit-exact mask geometry)
 TB_HD float f32_div(float a, float b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -545,25 +523,45 @@ TB_HD float f32_sqrt(float a) {
   return __builtin_sqrtf(a);
 #endif
 }
-TB_HD bool layer_in(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
-  const float eh = (float)shifted(kh, H) - (float)(H - 1) * 0.5f;
-  const float ew = (float)shifted(kw, W) - (float)(W - 1) * 0.5f;
-  const float ed = (float)shifted(kd, D) - (float)(D - 1) * 0.5f;
-  const float d2 = (eh * eh + ew * ew) + ed * ed;   // exact: quarter-integers < 2^22
+
+// Per-axis geometry of a coefficient f (and its mirror -f), the only quantities the masks need:
+//   dsq = (s - n/2)^2               disk_mask: centre floor(n/2) (filters_and_operators.py:176-187)
+//   ef, en = (2s - (n-1))^2 at f, -f   GibbsNoise / GibbsNoiseLayer: 4*(s - (n-1)/2)^2, exact (:689-698)
+//   odd = s & 1                      WrapArtifact (:509-511); equal at f and -f
+// with s the fftshift-ed index.  Two of the three axes are constant along a pass-B column, so a
+// butterfly computes them once and each coefficient only adds its H part.
+struct AxisGeo {
+  int k, nk, dsq, ef, en, odd;
+};
+TB_HD AxisGeo axis_geo(int k, int n) {
+  AxisGeo g;
+  g.k = k;
+  g.nk = negk(k, n);
+  const int s = shifted(k, n), ns = shifted(g.nk, n);
+  const int d = s - n / 2, e = 2 * s - (n - 1), en = 2 * ns - (n - 1);
+  g.dsq = d * d;
+  g.ef = e * e;
+  g.en = en * en;
+  g.odd = s & 1;
+  return g;
+}
+struct FreqCol {  // W and D parts of a coefficient's geometry
+  int kw, kd, nkw, nkd, dsq, ef, en, odd;
+};
+TB_HD FreqCol freq_col(int kw, int kd, int W, int D) {
+  const AxisGeo w = axis_geo(kw, W), d = axis_geo(kd, D);
+  return FreqCol{kw, kd, w.nk, d.nk, w.dsq + d.dsq, w.ef + d.ef, w.en + d.en, w.odd + d.odd};
+}
+
+// GibbsNoiseLayer mask (stylization_layers.py:99-109): float32 geometry, centre (n-1)/2,
+// norm_dist = dist / (alpha * max dist); mask = !(norm_dist > 1)  (NaN -> 1, inf -> 0).
+// d2 = e2/4 is an exact quarter-integer, so its float32 sum order is immaterial.
+TB_HD bool layer_in(const tb_op& op, int e2) {
   // alpha * max_dist: from the launch arguments, or (op.l != 0) from the layer's device-resident
   // alpha buffer times max_dist in f[1] -- no host round trip for the alpha of Gibbs_GD updates
   const float an = op.l ? (*reinterpret_cast<const float*>(op.l)) * op.f[1] : op.f[0];
-  const float nd = f32_div(f32_sqrt(d2), an);
+  const float nd = f32_div(f32_sqrt((float)e2 * 0.25f), an);
   return !(nd > 1.f);
-}
-
-// wrap (filters_and_operators.py:509-511): alpha per axis whose shifted index is odd
-TB_HD float wrap_value(const tb_op& op, int kh, int kw, int kd, int H, int W, int D) {
-  float m = 1.f;
-  if (shifted(kh, H) & 1) m *= op.f[0];
-  if (shifted(kw, W) & 1) m *= op.f[0];
-  if (shifted(kd, D) & 1) m *= op.f[0];
-  return m;
 }
 
 // The target value of a spike: |k| := amp (= exp(intensity)), phase kept
@@ -588,8 +586,9 @@ TB_HD cf spike_target(const tb_op& op, cf kf) {
 // +conj(Delta)/2 at -f.  Consecutive SPIKE ops flagged `reserved = 1` belong to one
 // KSpaceSpikeNoise call: they are all measured against the spectrum BEFORE the group
 // (the reference writes every location into one log-amplitude array, :936-942).
-TB_HD cf apply_ops(const tb_sample_ops& so, int chan, cf v, int kh, int kw, int kd, int H, int W, int D) {
-  const int nkh = negk(kh, H), nkw = negk(kw, W), nkd = negk(kd, D);
+template <class SO>
+TB_HD cf apply_ops(const SO& so, int chan, cf v, const FreqCol& fc, int kh, int H) {
+  const AxisGeo h = axis_geo(kh, H);
   cf gbase = v;
   bool in_group = false;
   for (int o = 0; o < so.n; ++o) {   // op fields come straight from the kernarg segment (scalar loads)
@@ -602,28 +601,33 @@ TB_HD cf apply_ops(const tb_sample_ops& so, int chan, cf v, int kh, int kw, int 
     }
     if (op.chan >= 0 && op.chan != chan) continue;
     switch (op.kind) {
-      case TB_OP_DISK:
-        v = scl(v, disk_value(op, kh, kw, kd, H, W, D));
-        break;
+      case TB_OP_DISK: {
+        const int sq = h.dsq + fc.dsq;
+        bool in = op.i[0] ? ((int64_t)sq < op.l) : ((float)sq < op.f[0]);
+        if (op.i[1]) in = !in;                            // inside_off
+        v = in ? v : mk(0.f, 0.f);
+      } break;
       case TB_OP_GIBBS: {
-        const float m = 0.5f * ((gibbs_in(op, kh, kw, kd, H, W, D) ? 1.f : 0.f) +
-                                (gibbs_in(op, nkh, nkw, nkd, H, W, D) ? 1.f : 0.f));
+        const float m = 0.5f * (((int64_t)(h.ef + fc.ef) <= op.l ? 1.f : 0.f) +
+                                ((int64_t)(h.en + fc.en) <= op.l ? 1.f : 0.f));
         v = scl(v, m);
       } break;
       case TB_OP_LAYER: {
-        const float m = 0.5f * ((layer_in(op, kh, kw, kd, H, W, D) ? 1.f : 0.f) +
-                                (layer_in(op, nkh, nkw, nkd, H, W, D) ? 1.f : 0.f));
+        const float m = 0.5f * ((layer_in(op, h.ef + fc.ef) ? 1.f : 0.f) + (layer_in(op, h.en + fc.en) ? 1.f : 0.f));
         v = scl(v, m);
       } break;
-      case TB_OP_WRAP:
-        v = scl(v, wrap_value(op, kh, kw, kd, H, W, D));
-        break;
+      case TB_OP_WRAP: {
+        const int nodd = h.odd + fc.odd;
+        const float a = op.f[0];
+        const float m = nodd == 0 ? 1.f : (nodd == 1 ? a : (nodd == 2 ? a * a : a * a * a));
+        v = scl(v, m);
+      } break;
       case TB_OP_SPIKE: {
-        if (kh == op.i[0] && kw == op.i[1] && kd == op.i[2]) {        // this coefficient is f
+        if (kh == op.i[0] && fc.kw == op.i[1] && fc.kd == op.i[2]) {        // this coefficient is f
           const cf d = sub(spike_target(op, gbase), gbase);
           v = add(v, scl(d, 0.5f));
         }
-        if (nkh == op.i[0] && nkw == op.i[1] && nkd == op.i[2]) {     // this coefficient is -f
+        if (h.nk == op.i[0] && fc.nkw == op.i[1] && fc.nkd == op.i[2]) {    // this coefficient is -f
           const cf kf = conj(gbase);
           const cf d = sub(spike_target(op, kf), kf);
           v = add(v, scl(conj(d), 0.5f));
@@ -830,9 +834,26 @@ TB_HD void pass_a_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, const float* __
 // per (bc, tile of T spectrum columns): H stage 0 from HBM, H stages in LDS, the last forward
 // stage fused with the op program and the first inverse stage in registers, inverse stage 0
 // back to HBM.
-template <class Ctx, int RS>
+// the op program of one pass-B tile column: per-column geometry once, per-coefficient H part
+template <class SO>
+struct KOps {
+  const SO& so;
+  int chan, j0, Dh;
+  FastDiv fDh;
+  const int* irev;    // H slot -> frequency (LDS)
+  const int* irev_w;  // W slot -> frequency
+  int H, W, D;
+  TB_HD FreqCol col(int c) const {
+    const int j = j0 + c;
+    const int wp = fDh.div(j);
+    return freq_col(irev_w[wp], j - wp * Dh, W, D);
+  }
+  TB_HD cf operator()(const FreqCol& fc, int pos, cf v) const { return apply_ops(so, chan, v, fc, irev[pos], H); }
+};
+
+template <class Ctx, int RS, class SO>
 TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict__ S, int bc, int tile, int T,
-                       const tb_sample_ops& so, int chan) {
+                       const SO& so, int chan) {
   const int H = pl.H, W = pl.W, D = pl.D, Dh = D / 2 + 1;
   const int ncols_all = W * Dh;
   const int j0 = tile * T;
@@ -844,15 +865,10 @@ TB_HD void pass_b_body(Ctx& ctx, cf* lds, const tb_plan_dev& pl, cf* __restrict_
   ctx.sync();
   cf* Sb = S + (int64_t)bc * H * ncols_all + j0;
   const StridedAcc gacc{Sb, 1, ncols_all};
-  const FastDiv fDh = FastDiv::make(Dh);
-  auto ops = [&](int c, int pos, cf v) {
-    const int j = j0 + c;
-    const int wp = fDh.div(j), kd = j - wp * Dh;
-    return apply_ops(so, chan, v, irev[pos], pl.irev_w[wp], kd, H, W, D);
-  };
+  const KOps<SO> ops{so, chan, j0, Dh, FastDiv::make(Dh), irev, pl.irev_w, H, W, D};
   const tb_axis& ax = pl.ax[0];
   if (ax.nst == 0) {  // H == 1: the op program alone
-    for (int t = ctx.tid; t < nc; t += ctx.nthreads) Sb[t] = ops(t, 0, Sb[t]);
+    for (int t = ctx.tid; t < nc; t += ctx.nthreads) Sb[t] = ops(ops.col(t), 0, Sb[t]);
     return;
   }
   if (ax.nst == 1) {  // one radix: HBM -> DFT -> ops -> IDFT -> HBM, no LDS round trip

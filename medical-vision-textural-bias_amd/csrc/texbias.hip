@@ -313,7 +313,7 @@ __global__ __launch_bounds__(NT) void k_kspace_stats(StatsArgs) {
     const int hp = fnc.div(t), c = t - hp * nc;
     const int j = j0 + c;
     const int wp = fDh.div(j), kd = j - wp * Dh;
-    const cf v = apply_ops(so, chan, lds[hp * T + c], irev[hp], pl.irev_w[wp], kd, H, W, D);
+    const cf v = apply_ops(so, chan, lds[hp * T + c], freq_col(pl.irev_w[wp], kd, W, D), irev[hp], H);
     const float la = logf(f32_sqrt(v.x * v.x + v.y * v.y) + 1e-10f);
     acc += (kd == 0 || kd == Dtop) ? (double)la : 2.0 * (double)la;
   }
@@ -364,6 +364,7 @@ int pick_tile(int H, int lds_max) {
   }();
   int T = budget / (H * 8);
   if (T > 64) T = 64;
+  if (T >= 16) T &= ~7;   // whole 64-B segments per tile row
   if (T < 4) T = 4;
   while (tile_geo(H, T).total_cf * 8 > lds_max && T > 1) --T;
   return T;
