@@ -28,8 +28,10 @@
 
 #if defined(__HIPCC__)
 #define TB_HD __host__ __device__ __forceinline__
+#define TB_HD_NOINLINE __host__ __device__ __attribute__((noinline))
 #else
 #define TB_HD inline
+#define TB_HD_NOINLINE __attribute__((noinline))
 #endif
 
 #define TB_MAX_STAGES 8
@@ -412,6 +414,13 @@ TB_HD void stage_r(Ctx& ctx, Src src, Dst dst, const cf* tw, int Lb, int P, int 
   }
 }
 
+// the op program called out of line: the large odd-prime butterflies would otherwise inline R
+// copies of it (compile time and code size; those radices are rare on the H axis)
+template <class OpsF, class CC>
+TB_HD_NOINLINE cf ops_call(const OpsF& ops, const CC& cc, int pos, cf v) {
+  return ops(cc, pos, v);
+}
+
 // last forward stage + per-coefficient ops + first inverse stage, in registers.  The last DIF
 // stage has L = 1 and j = 0 (no twiddles): its butterfly groups are exactly the groups of the
 // first DIT stage, so forward DFT -> ops(position) -> inverse DFT never leaves the thread.
@@ -430,7 +439,10 @@ TB_HD void stage_mid_r(Ctx& ctx, Src src, Dst dst, int npen, int n, OpsF ops, bo
     Dft<R, true>::run(a);
     const auto cc = ops.col(p);   // geometry shared by the butterfly's R coefficients
 #pragma unroll
-    for (int q = 0; q < R; ++q) a[q] = ops(cc, base + q, a[q]);
+    for (int q = 0; q < R; ++q) {
+      if constexpr (IsStreamed<R>::value) a[q] = ops_call(ops, cc, base + q, a[q]);  // one out-of-line copy
+      else a[q] = ops(cc, base + q, a[q]);
+    }
     Dft<R, false>::run(a);
 #pragma unroll
     for (int q = 0; q < R; ++q) dp.st(base + q, a[q]);

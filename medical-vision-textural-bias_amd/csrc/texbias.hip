@@ -1,5 +1,7 @@
 // texbias.hip -- gfx950 kernels and the C ABI (include/texbias.h) of the texbias library.
 //
+// The pass kernels A/B/C (and the spectrum statistics) live in kern_*.hip, one translation unit
+// per kernel and radix set; this file holds the small kernels and the host side of the C ABI.
 // Pass plan of one k-space filter call (DESIGN.md "Kernels"):
 //   A  k_slab_fwd   per (bc, h) slab: real rows -> pair-packed R2C along D -> C2C along W,
 //                   in one 150 KB LDS slab; stores the half spectrum (digit-reversed W).
@@ -16,23 +18,13 @@
 #include <vector>
 
 #include "fft_core.h"
+#include "kernels.h"
 #include "plan_host.h"
 #include "sap_core.h"
 
 using namespace tb;
 
 namespace {
-
-struct DevCtx {
-  int tid, nthreads;
-  __device__ __forceinline__ void sync() { __syncthreads(); }
-};
-
-enum { RS_SMALL = 0, RS_ALL = 1 };
-
-struct BatchOps {
-  tb_sample_ops s[TB_MAX_BATCH];
-};
 
 thread_local int g_last_hip = 0;
 
@@ -75,110 +67,17 @@ struct Timer {  // records [begin, end) of one pass when timing is enabled
     std::lock_guard<std::mutex> lk(g_tmu);
     a = ev_get();
     b = ev_get();
-    if (a) hipEventRecord(a, st);
+    if (a) (void)hipEventRecord(a, st);
   }
   ~Timer() {
     if (!a || !b) return;
-    hipEventRecord(b, st);
+    (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> lk(g_tmu);
     g_recs.push_back({a, b, slot});
   }
 };
 
 // ---------------------------------------------------------------- kernels
-// Every kernel takes ONE argument struct and reads it through the kernarg segment pointer:
-// dynamically indexed by-value parameters (the plan's radix lists, a sample's op program)
-// are otherwise copied to per-lane scratch memory (2.4 KB per lane for the op programs).
-template <class A>
-__device__ __forceinline__ const A& kargs() {
-  return *(const A*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
-}
-
-struct SlabFwdArgs {
-  tb_plan_dev pl;
-  const float* x;
-  int64_t sbc, sh, sw;
-  cf* S;
-  int bc0;
-};
-template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_slab_fwd(SlabFwdArgs) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const SlabFwdArgs& a = kargs<SlabFwdArgs>();
-  DevCtx ctx{(int)threadIdx.x, NT};
-  pass_a_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.x, a.sbc, a.sh, a.sw, a.S,
-                          a.bc0 + (int)blockIdx.y, (int)blockIdx.x);
-}
-
-struct KspaceArgs {
-  tb_plan_dev pl;
-  cf* S;
-  int bc0, C, T, pad;
-  BatchOps ops;
-};
-template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_kspace(KspaceArgs) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const KspaceArgs& a = kargs<KspaceArgs>();
-  DevCtx ctx{(int)threadIdx.x, NT};
-  const int bcl = (int)blockIdx.y;
-  pass_b_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.S, a.bc0 + bcl, (int)blockIdx.x, a.T,
-                          a.ops.s[bcl / a.C], bcl % a.C);
-}
-
-__device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-// block min/max -> atomic keys (uses the first 2*NT/64 floats of smem after a barrier)
-template <int NT>
-__device__ __forceinline__ void block_minmax_atomic(float lo, float hi, float* red, uint32_t* mm) {
-  lo = wave_min(lo);
-  hi = wave_max(hi);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) {
-    red[wid] = lo;
-    red[NT / 64 + wid] = hi;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < NT / 64; ++w) {
-      lo = fminf(lo, red[w]);
-      hi = fmaxf(hi, red[NT / 64 + w]);
-    }
-    atomicMin(&mm[0], f2key(lo));
-    atomicMax(&mm[1], f2key(hi));
-  }
-}
-
-struct SlabInvArgs {
-  tb_plan_dev pl;
-  const cf* S;
-  float* y;
-  int64_t sbc, sh, sw;
-  int ypad, bc0, C;
-  float scale;
-  uint32_t* mm;
-};
-template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_slab_inv(SlabInvArgs) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const SlabInvArgs& a = kargs<SlabInvArgs>();
-  DevCtx ctx{(int)threadIdx.x, NT};
-  const int bc = a.bc0 + (int)blockIdx.y;
-  float lo, hi;
-  pass_c_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.S, a.y, a.sbc, a.sh, a.sw, a.ypad, bc,
-                          (int)blockIdx.x, a.scale, &lo, &hi);
-  if (a.mm) block_minmax_atomic<NT>(lo, hi, reinterpret_cast<float*>(smem), a.mm + 2 * (bc / a.C));
-}
 
 __global__ void k_minmax_init(uint32_t* mm, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -271,64 +170,6 @@ __global__ void k_disk_mask(float* __restrict__ m, int64_t outer, int n0, int n1
   }
 }
 
-// log-abs statistics of the op-processed spectrum (default spike intensity)
-struct StatsArgs {
-  tb_plan_dev pl;
-  const cf* S;
-  int bc0, C, T, pad;
-  double* out;
-  BatchOps ops;
-};
-template <int NT, int RS>
-__global__ __launch_bounds__(NT) void k_kspace_stats(StatsArgs) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const StatsArgs& a = kargs<StatsArgs>();
-  const tb_plan_dev& pl = a.pl;
-  cf* lds = reinterpret_cast<cf*>(smem);
-  DevCtx ctx{(int)threadIdx.x, NT};
-  const int bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
-  const int T = a.T;
-  const int H = pl.H, W = pl.W, D = pl.D, Dh = D / 2 + 1;
-  const int ncols_all = W * Dh;
-  const int j0 = (int)blockIdx.x * T;
-  const int nc = (ncols_all - j0) < T ? (ncols_all - j0) : T;
-  const TileGeo g = tile_geo(H, T);
-  cf* tw = lds + g.off_tw;
-  int* irev = reinterpret_cast<int*>(lds + g.off_irev);
-  for (int i = threadIdx.x; i < H; i += NT) { tw[i] = pl.tw[0][i]; irev[i] = pl.irev_h[i]; }
-  const cf* Sb = a.S + (int64_t)bc * H * ncols_all + j0;
-  const int nl = H * nc;
-  const FastDiv fnc = FastDiv::make(nc), fDh = FastDiv::make(Dh);
-  for (int t = threadIdx.x; t < nl; t += NT) {
-    const int hh = fnc.div(t), c = t - hh * nc;
-    lds[hh * T + c] = Sb[(int64_t)hh * ncols_all + c];
-  }
-  __syncthreads();
-  fft_dif<DevCtx, RS>(ctx, lds, tw, pl.ax[0], nc, TileAddr{T}, true);
-  double acc = 0.0;
-  const tb_sample_ops& so = a.ops.s[bcl / a.C];
-  const int chan = bcl % a.C;
-  const int Dtop = (D % 2 == 0) ? D / 2 : -1;
-  for (int t = threadIdx.x; t < nl; t += NT) {
-    const int hp = fnc.div(t), c = t - hp * nc;
-    const int j = j0 + c;
-    const int wp = fDh.div(j), kd = j - wp * Dh;
-    const cf v = apply_ops(so, chan, lds[hp * T + c], freq_col(pl.irev_w[wp], kd, W, D), irev[hp], H);
-    const float la = logf(f32_sqrt(v.x * v.x + v.y * v.y) + 1e-10f);
-    acc += (kd == 0 || kd == Dtop) ? (double)la : 2.0 * (double)la;
-  }
-  // block reduce in double
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  __syncthreads();
-  double* red = reinterpret_cast<double*>(smem);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < NT / 64; ++w) acc += red[w];
-    atomicAdd(&a.out[bc], acc);
-  }
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------- plan
@@ -343,8 +184,6 @@ struct tb_plan {
 
 namespace {
 
-constexpr int NT_SLAB = 512;
-constexpr int NT_TILE = 256;
 constexpr int NT_SAP = 256;
 
 bool needs_all(const tb_axis& ax) {
@@ -368,15 +207,6 @@ int pick_tile(int H, int lds_max) {
   if (T < 4) T = 4;
   while (tile_geo(H, T).total_cf * 8 > lds_max && T > 1) --T;
   return T;
-}
-
-template <class K>
-int set_lds(K kern, size_t bytes) {
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lk(mu);
-  TB_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)bytes));
-  return TB_OK;
 }
 
 }  // namespace
@@ -431,7 +261,7 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   }
   if (hipMalloc(&p->dmem, bytes) != hipSuccess) { delete p; return hip_fail(hipGetLastError()); }
   if (hipMemcpy(p->dmem, buf.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-    hipFree(p->dmem);
+    (void)hipFree(p->dmem);
     delete p;
     return hip_fail(hipGetLastError());
   }
@@ -452,7 +282,7 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
 
 int tb_plan_destroy(tb_plan* plan) {
   if (!plan) return TB_OK;
-  if (plan->dmem) hipFree(plan->dmem);
+  if (plan->dmem) (void)hipFree(plan->dmem);
   delete plan;
   return TB_OK;
 }
@@ -473,11 +303,8 @@ template <int RS>
 static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, cf* S, int bc0, int nbc,
                            hipStream_t st) {
   const size_t lds = (size_t)slab_geo(p->dev.W, p->dev.D).total_cf * sizeof(cf);
-  int rc = set_lds(k_slab_fwd<NT_SLAB, RS>, lds);
-  if (rc) return rc;
   SlabFwdArgs a{p->dev, x, xs[0], xs[1], xs[2], S, bc0};
-  hipLaunchKernelGGL((k_slab_fwd<NT_SLAB, RS>), dim3(p->dev.H, nbc), dim3(NT_SLAB), lds, st, a);
-  TB_HIP(hipGetLastError());
+  TB_HIP(tb::launch_slab_fwd<RS>(a, dim3(p->dev.H, nbc), lds, st));
   return TB_OK;
 }
 
@@ -501,10 +328,7 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
   const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
   const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
   const size_t lds_s = (size_t)slab_geo(W, D).total_cf * sizeof(cf);
-  int rc = set_lds(k_kspace<NT_TILE, RB>, lds_b);
-  if (rc) return rc;
-  rc = set_lds(k_slab_inv<NT_SLAB, RA>, lds_s);
-  if (rc) return rc;
+  int rc = TB_OK;
   // launch groups of <= TB_MAX_BATCH samples (the op programs travel in the kernel arguments)
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
@@ -519,14 +343,12 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     {
       Timer t(1, st);
       KspaceArgs ka{p->dev, S, b0 * C, C, T, 0, bo};
-      hipLaunchKernelGGL((k_kspace<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, ka);
-      TB_HIP(hipGetLastError());
+      TB_HIP(launch_kspace<RB>(ka, dim3(ntiles, nb * C), lds_b, st));
     }
     {
       Timer t(2, st);
       SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, b0 * C, C, scale, minmax};
-      hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RA>), dim3(H, nb * C), dim3(NT_SLAB), lds_s, st, ia);
-      TB_HIP(hipGetLastError());
+      TB_HIP(launch_slab_inv<RA>(ia, dim3(H, nb * C), lds_s, st));
     }
   }
   return TB_OK;
@@ -543,8 +365,7 @@ static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, voi
   const int T = pick_tile(H, p->lds_max);
   const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
   const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
-  int rc = set_lds(k_kspace_stats<NT_TILE, RB>, lds_b);
-  if (rc) return rc;
+  int rc = TB_OK;
   TB_HIP(hipMemsetAsync(out, 0, sizeof(double) * B * C, st));
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
@@ -554,8 +375,7 @@ static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, voi
     rc = launch_slab_fwd<RA>(p, x, xs, S, b0 * C, nb * C, st);
     if (rc) return rc;
     StatsArgs sa{p->dev, S, b0 * C, C, T, 0, out, bo};
-    hipLaunchKernelGGL((k_kspace_stats<NT_TILE, RB>), dim3(ntiles, nb * C), dim3(NT_TILE), lds_b, st, sa);
-    TB_HIP(hipGetLastError());
+    TB_HIP(launch_kspace_stats<RB>(sa, dim3(ntiles, nb * C), lds_b, st));
   }
   return TB_OK;
 }
