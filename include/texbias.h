@@ -144,6 +144,22 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
                         int Hi, int Wi, int stride, int pad, void* stream);
 
 /*
+ * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
+ * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution
+ * (MONAI Convolution, used by 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-199).
+ *   forward : y = prelu((x - mean) * rstd, a); stores mean[NC], rstd[NC] (biased var) for backward
+ *   backward: dx (and, if dw != NULL, dw[0] = dL/da) from x, dy and the saved mean/rstd
+ * prelu_w / dw are DEVICE pointers to one float.  ws: device scratch of
+ * tb_instnorm_prelu_workspace_bytes(NC) bytes (reused per call, stream-ordered).
+ */
+size_t tb_instnorm_prelu_workspace_bytes(int64_t NC);
+int tb_instnorm_prelu_fwd_f32(const float* x, float* y, float* mean, float* rstd, const float* prelu_w, int64_t NC,
+                              int64_t S, float eps, void* ws, size_t ws_bytes, void* stream);
+int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean, const float* rstd,
+                              const float* prelu_w, float* dx, float* dw, int64_t NC, int64_t S, void* ws,
+                              size_t ws_bytes, void* stream);
+
+/*
  * Per-pass device timing for measurement: while enabled, every launch function records HIP
  * events around each of its kernels on the caller's stream.  tb_get_pass_times_ms synchronises
  * on them and returns the summed milliseconds per pass -- [0] slab forward (A), [1] k-space

@@ -10,7 +10,8 @@ MONAI is not installed in this image).
 
 Blocks (MONAI 0.5 semantics):
 * ``Convolution`` = Conv3d / ConvTranspose3d -> InstanceNorm3d(affine=False) -> Dropout(0) -> PReLU
-  ("NDA" order), or the bare conv when ``conv_only``;
+  ("NDA" order; on HIP tensors one fused texbias kernel pair, ``texbias.norm``), or the bare conv
+  when ``conv_only``;
 * ``ResidualUnit`` = ``subunits`` Convolutions (first one strided) + residual path (strided 3^3
   conv, 1^3 conv when only the channel count changes, else identity), summed;
 * ``SkipConnection`` = cat([x, sub(x)], dim=1).
@@ -27,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from .conv import Conv3d, ConvTranspose3d
+from .norm import instnorm_prelu
 
 
 class ADN(nn.Sequential):
@@ -35,6 +37,12 @@ class ADN(nn.Sequential):
         self.add_module("N", nn.InstanceNorm3d(channels, eps=1e-5, affine=False, track_running_stats=False))
         self.add_module("D", nn.Dropout(p=dropout))
         self.add_module("A", nn.PReLU(num_parameters=1))
+
+    def forward(self, x):
+        # On the GPU the N -> D(0) -> A chain is one fused texbias op (two HBM sweeps per direction).
+        if x.is_cuda and x.dtype == torch.float32 and (self.D.p == 0.0 or not self.training):
+            return instnorm_prelu(x, self.A.weight, self.N.eps)
+        return super().forward(x)
 
 
 class Convolution(nn.Sequential):
