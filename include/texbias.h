@@ -160,6 +160,13 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
                               size_t ws_bytes, void* stream);
 
 /*
+ * Compiled plans: slab shapes with a compile-time FFT plan (W x D = 240 x 155, 128 x 128) run passes
+ * A and C on dedicated persistent kernels; enable = 0 forces the generic run-time-planned passes
+ * (same results to rounding).  Default on; TEXBIAS_COMPILED_PLANS=0 in the environment turns it off.
+ */
+int tb_set_compiled_plans(int enable);
+
+/*
  * Per-pass device timing for measurement: while enabled, every launch function records HIP
  * events around each of its kernels on the caller's stream.  tb_get_pass_times_ms synchronises
  * on them and returns the summed milliseconds per pass -- [0] slab forward (A), [1] k-space

@@ -1,21 +1,26 @@
 // conv_wgrad.hip -- 3-D convolution weight gradient (f32, MFMA 16x16x4) for the U-Net train step.
 //
 // The reference trains MONAI's 3-D U-Net (10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-204)
-// and its backward needs dW of every Conv3d / ConvTranspose3d.  MIOpen on gfx950 runs the
-// weight gradient of the full-resolution layers (K = N * 120*120*80 = 2.3 M reduction positions,
+// and its backward needs dW of every Conv3d / ConvTranspose3d.  MIOpen on gfx950 runs the weight
+// gradient of the full- and half-resolution layers (K = N * 120*120*80 = 2.3 M reduction positions,
 // only 16 x 16 x 27 outputs) with a naive kernel or a CK GEMM without split-K: ~350 ms each.
 // This kernel is a split-K implicit GEMM:
-//   dW[m][c][tz][ty][tx] = sum_n sum_{z,y,x} G[n][m][z][y][x] * X[n][c][s z + tz - p][s y + ty - p][s x + tx - p]
+//   dW[m][c][tz][ty][tx] = sum_n sum_{z,y,x} G[n][m][z][y][x] * X[n][c][s z + tz - 1][s y + ty - 1][s x + tx - 1]
 // which covers both layer kinds:
 //   Conv3d          : G = dY [N][Cout][out],  X = x  [N][Cin][in],   dW = [Cout][Cin][k^3]
 //   ConvTranspose3d : G = x  [N][Cin][in],    X = dY [N][Cout][out], dW = [Cin][Cout][k^3]
 // (PyTorch's transposed conv places x[q] at s q - p + t, the same index map).
 //
-// Work split: blockIdx.y = (16-row m tile, 16-col c tile); blockIdx.x strides over "chunks" =
-// (n, z, y, x-segment of XT outputs).  Per chunk the block stages G[16][XT] and the 3x3 (tz,ty)
-// input rows X[16][9][s(XT-1)+3] in LDS; each of the 4 waves owns 7 (or 6) of the 27 taps and
-// runs v_mfma_f32_16x16x4_f32 over the chunk's positions (K = 4 per instruction, exact f32 FMA
-// chains).  Partial sums leave the block once, by float atomics into dW (zeroed first).
+// v_mfma_f32_16x16x4_f32: rows = 16 output channels m, K = 4 consecutive x positions, columns =
+//   TX = 1: 16 input channels c; the 27 taps (tz,ty,tx) are accumulators split over the 4 waves;
+//   TX = 3: (c, tx) pairs of up to 5 channels -- the 3- and 4-channel layers fill 9-12 of the 16
+//           columns instead of 3-4 -- and the 9 (tz,ty) taps are the accumulators.
+// Work unit ("chunk") = (n, z, YB consecutive output rows, every x): the block stages G[16][YB][Wo]
+// and the input rows X[c][tz][S(YB-1)+3][x + halo] in LDS once and runs YB * Wo/4 k-steps of every
+// tap over them (each staged input row feeds up to 27 MFMA taps).  Rows are staged whole by one
+// wave each (scalar row bounds) as global->LDS DMA, every row of the chunk in flight at once.  At most ~78 KB of
+// LDS so two blocks share a CU and one block's staging hides under the other's MFMAs.  Partial sums
+// leave each block once, by float atomics into dW (zeroed first).
 #include <hip/hip_runtime.h>
 
 #include "texbias.h"
@@ -24,123 +29,216 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int S, int XT>
-struct WgGeo {
-  static constexpr int GP = XT + 1;                // padded G row (bank spread)
-  static constexpr int XS = S * (XT - 1) + 3;      // input row span per chunk
-  static constexpr int XP = XS | 1;                // odd pitch
-  static constexpr int ROWS = 9;                   // (tz, ty)
+constexpr int NT = 256;
+constexpr int LDS_FLOATS = 78 * 1024 / 4;
+
+struct WgArgs {
+  const float* G;
+  const float* X;
+  float* dW;
+  int M, Cc, Do, Ho, Wo, Di, Hi, Wi;
+  int YB, YR, Wo4, XP, PG, PC, ncc, ctiles, nyb, xcols;
+  int64_t nchunks;
 };
 
-template <int S, int XT>
-__global__ __launch_bounds__(256) void k_conv3d_wgrad(const float* __restrict__ G, const float* __restrict__ X,
-                                                      float* __restrict__ dW, int M, int Cc, int Do, int Ho, int Wo,
-                                                      int Di, int Hi, int Wi, int pad, int nxt, int64_t nchunks,
-                                                      int ctiles) {
-  using Gm = WgGeo<S, XT>;
-  __shared__ float gs[16 * Gm::GP];
-  __shared__ float xs[16 * Gm::ROWS * Gm::XP];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int mt = blockIdx.y / ctiles, ct = blockIdx.y - mt * ctiles;
-  const int m0 = mt * 16, c0 = ct * 16;
-  const int mv = min(16, M - m0), cv = min(16, Cc - c0);
-  const int64_t gstride_m = (int64_t)Do * Ho * Wo, xstride_c = (int64_t)Di * Hi * Wi;
-  f32x4 acc[7];
-#pragma unroll
-  for (int j = 0; j < 7; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
 
-  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    int64_t r = ch;
-    const int xt = (int)(r % nxt); r /= nxt;
-    const int y = (int)(r % Ho); r /= Ho;
-    const int z = (int)(r % Do);
-    const int n = (int)(r / Do);
-    const int x0 = xt * XT;
-    // stage G[m][x0 .. x0+XT)
-    const float* gb = G + ((int64_t)n * M + m0) * gstride_m + ((int64_t)z * Ho + y) * Wo;
-    for (int i = tid; i < 16 * XT; i += 256) {
-      const int m = i / XT, xx = i - m * XT;
-      float v = 0.f;
-      if (m < mv && x0 + xx < Wo) v = gb[(int64_t)m * gstride_m + x0 + xx];
-      gs[m * Gm::GP + xx] = v;
-    }
-    // stage X[c][(tz,ty)][S*x0 - pad + j], j < XS
-    const int xin0 = S * x0 - pad;
-    const float* xb = X + ((int64_t)n * Cc + c0) * xstride_c;
-    const int nx = cv * Gm::ROWS * Gm::XS;
-    for (int i = tid; i < 16 * Gm::ROWS * Gm::XS; i += 256) {
-      float v = 0.f;
-      const int c = i / (Gm::ROWS * Gm::XS);
-      const int rem = i - c * (Gm::ROWS * Gm::XS);
-      const int row = rem / Gm::XS, j = rem - row * Gm::XS;
-      if (i < nx) {
-        const int zi = S * z + row / 3 - pad, yi = S * y + row % 3 - pad, xi = xin0 + j;
-        if (zi >= 0 && zi < Di && yi >= 0 && yi < Hi && xi >= 0 && xi < Wi)
-          v = xb[(int64_t)c * xstride_c + ((int64_t)zi * Hi + yi) * Wi + xi];
-      }
-      xs[(c * Gm::ROWS + row) * Gm::XP + j] = v;
-    }
-    __syncthreads();
-    const int li = lane & 15, lk = lane >> 4;
-#pragma unroll 4
-    for (int kk = 0; kk < XT; kk += 4) {
-      const float a = gs[li * Gm::GP + kk + lk];
-      const int xoff = S * (kk + lk);
+// lanes copy src[x] -> dst[x], x < n, by 4-B global->LDS DMA pieces (dst wave-uniform)
+template <int SEG>
+__device__ __forceinline__ void copy_row(const float* src, float* dst, int n, int lane) {
 #pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        const int t = wave + 4 * j;
-        if (t < 27) {
-          const int row = t / 3, tx = t - 3 * row;   // t = (tz*3 + ty)*3 + tx
-          const float b = xs[(li * Gm::ROWS + row) * Gm::XP + xoff + tx];
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+  for (int s = 0; s < SEG; ++s) {
+    const int x = lane + 64 * s;
+    if (x < n) __builtin_amdgcn_global_load_lds((gptr_t)(src + x), (lptr_t)(dst + 64 * s), 4, 0, 0);
+  }
+}
+template <int SEG>
+__device__ __forceinline__ void zero_row(float* dst, int n, int lane) {
+#pragma unroll
+  for (int s = 0; s < SEG; ++s) {
+    const int x = lane + 64 * s;
+    if (x < n) dst[x] = 0.f;
+  }
+}
+
+template <int S, int TX, int SEG>
+__global__ __launch_bounds__(NT) void k_conv3d_wgrad(WgArgs a) {
+  constexpr int NTAP = TX == 1 ? 27 : 9;
+  constexpr int TPW = (NTAP + 3) / 4;  // taps per wave (the last wave may have one fewer)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* gs = smem;                 // [16][PG]          row m: YB rows of Wo4 (zero beyond Wo)
+  float* xs = smem + 16 * a.PG;     // [ncc][PC]         plane c: [3 tz][YR rows][XP], col 0 = left halo
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mt = (int)blockIdx.y / a.ctiles, ct = (int)blockIdx.y - mt * a.ctiles;
+  const int m0 = mt * 16, c0 = ct * a.ncc;
+  const int mv = min(16, a.M - m0), cv = min(a.ncc, a.Cc - c0);
+  const int nlds = 16 * a.PG + a.ncc * a.PC;
+  for (int i = tid; i < nlds; i += NT) smem[i] = 0.f;   // halos, x >= Wo, absent m / c stay zero
+  const int li = lane & 15, lk = lane >> 4;
+  int boff;
+  if (TX == 1) {
+    boff = li * a.PC;
+  } else {
+    const int c = li / 3, tx = li - 3 * c;
+    boff = c < cv ? c * a.PC + tx : 0;
+  }
+  int toff[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int t = wave + 4 * j;
+    toff[j] = TX == 1 ? ((t / 9) * a.YR + (t / 3) % 3) * a.XP + t % 3 : ((t / 3) * a.YR + t % 3) * a.XP;
+  }
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t gsm = (int64_t)a.Do * a.Ho * a.Wo, xsc = (int64_t)a.Di * a.Hi * a.Wi;
+  __syncthreads();
+
+  for (int64_t ch = blockIdx.x; ch < a.nchunks; ch += gridDim.x) {
+    int64_t r = ch;
+    const int yb = (int)(r % a.nyb);
+    r /= a.nyb;
+    const int z = (int)(r % a.Do);
+    const int n = (int)(r / a.Do);
+    const int y0 = yb * a.YB;
+    // Staging: one wave per row, rows dealt round-robin to the 4 waves; in-range rows go global ->
+    // LDS by DMA (global_load_lds, lane-linear 4-B pieces, no registers, all of a wave's rows in
+    // flight at once), out-of-range rows (z / y halo) are zero-filled.  The barrier below drains them.
+    const float* gb = a.G + ((int64_t)n * a.M + m0) * gsm + (int64_t)z * a.Ho * a.Wo;
+    int row = 0;
+    for (int m = 0; m < mv; ++m)
+      for (int yy = 0; yy < a.YB; ++yy, ++row) {
+        if ((row & 3) != wave) continue;
+        const int y = y0 + yy;
+        float* dst = gs + m * a.PG + yy * a.Wo4;
+        if (y < a.Ho) copy_row<SEG>(gb + m * gsm + (int64_t)y * a.Wo, dst, a.Wo, lane);
+        else zero_row<SEG>(dst, a.Wo, lane);
+      }
+    const float* xb0 = a.X + ((int64_t)n * a.Cc + c0) * xsc;
+    row = 0;
+    for (int c = 0; c < cv; ++c)
+      for (int tz = 0; tz < 3; ++tz) {
+        const int zi = S * z + tz - 1;
+        for (int yr = 0; yr < a.YR; ++yr, ++row) {
+          if ((row & 3) != wave) continue;
+          const int yi = S * y0 + yr - 1;
+          float* dst = xs + c * a.PC + (tz * a.YR + yr) * a.XP + 1;
+          if (zi >= 0 && zi < a.Di && yi >= 0 && yi < a.Hi)
+            copy_row<SEG>(xb0 + c * xsc + ((int64_t)zi * a.Hi + yi) * a.Wi, dst, a.xcols, lane);
+          else
+            zero_row<SEG>(dst, a.xcols, lane);
+        }
+      }
+    __syncthreads();
+    for (int yy = 0; yy < a.YB; ++yy) {
+      const float* ga = gs + li * a.PG + yy * a.Wo4 + lk;
+      const float* xq = xs + boff + (S * yy) * a.XP + S * lk;
+#pragma unroll 2
+      for (int x0 = 0; x0 < a.Wo4; x0 += 4) {
+        const float av = ga[x0];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          if (wave + 4 * j < NTAP)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xq[toff[j] + S * x0], acc[j], 0, 0, 0);
         }
       }
     }
     __syncthreads();
   }
-  // D[row = m][col = c]: lane holds rows (lane>>4)*4 + r, col lane & 15
-  const int c = lane & 15;
+  // D[row = m][col]: lane holds rows (lane>>4)*4 + rr, column lane & 15
 #pragma unroll
-  for (int j = 0; j < 7; ++j) {
+  for (int j = 0; j < TPW; ++j) {
     const int t = wave + 4 * j;
-    if (t >= 27 || c >= cv) continue;
+    if (t >= NTAP) continue;
+    int c, tap;
+    if (TX == 1) {
+      c = li;
+      tap = t;
+      if (c >= cv) continue;
+    } else {
+      c = li / 3;
+      tap = t * 3 + (li - 3 * c);
+      if (li >= 3 * cv) continue;
+    }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const int m = (lane >> 4) * 4 + rr;
-      if (m < mv) atomicAdd(&dW[((int64_t)(m0 + m) * Cc + (c0 + c)) * 27 + t], acc[j][rr]);
+      const int m = lk * 4 + rr;
+      if (m < mv) atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + tap], acc[j][rr]);
     }
   }
 }
 
-template <int S, int XT>
-int launch(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi,
-           int Wi, int pad, hipStream_t st) {
-  const int nxt = (Wo + XT - 1) / XT;
-  const int64_t nchunks = (int64_t)N * Do * Ho * nxt;
-  const int mtiles = (M + 15) / 16, ctiles = (Cc + 15) / 16;
-  // enough blocks to fill the chip ~4x over, never more than there are chunks
-  int64_t gx = (2048 + mtiles * ctiles - 1) / (mtiles * ctiles);
-  if (gx > nchunks) gx = nchunks;
+int pad_mod32(int v, int rem) {
+  while ((v & 31) != rem) ++v;
+  return v;
+}
+
+template <int S, int TX, int SEG>
+int launch(const WgArgs& a, int blocks_y, size_t lds, hipStream_t st) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_wgrad<S, TX, SEG>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  if (attr != hipSuccess) return TB_ERR_HIP;
+  // two blocks per CU over the whole chip, never more chunks than exist
+  int64_t gx = (512 + blocks_y - 1) / blocks_y;
+  if (gx > a.nchunks) gx = a.nchunks;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((k_conv3d_wgrad<S, XT>), dim3((unsigned)gx, mtiles * ctiles), dim3(256), 0, st, G, X, dW, M,
-                     Cc, Do, Ho, Wo, Di, Hi, Wi, pad, nxt, nchunks, ctiles);
+  hipLaunchKernelGGL((k_conv3d_wgrad<S, TX, SEG>), dim3((unsigned)gx, (unsigned)blocks_y), dim3(NT), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+template <int S, int TX>
+int launch_seg(const WgArgs& a, int seg, int by, size_t lds, hipStream_t st) {
+  switch (seg) {
+    case 1: return launch<S, TX, 1>(a, by, lds, st);
+    case 2: return launch<S, TX, 2>(a, by, lds, st);
+    case 3: return launch<S, TX, 3>(a, by, lds, st);
+    case 4: return launch<S, TX, 4>(a, by, lds, st);
+    default: return TB_ERR_UNSUPPORTED_SIZE;
+  }
 }
 
 }  // namespace
 
-// dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2 (see file header).
+// dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2, padding 1 (file header).
 int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
                         int Hi, int Wi, int stride, int pad, void* stream) {
   if (!G || !X || !dW || N < 1 || M < 1 || Cc < 1 || Do < 1 || Ho < 1 || Wo < 1 || Di < 1 || Hi < 1 || Wi < 1)
     return TB_ERR_INVALID_ARG;
-  if (stride != 1 && stride != 2) return TB_ERR_INVALID_ARG;
+  if ((stride != 1 && stride != 2) || pad != 1) return TB_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st) != hipSuccess) return TB_ERR_HIP;
-  const bool small = (Wo % 64 != 0) && ((Wo + 31) / 32 * 32 <= (Wo + 63) / 64 * 64 - 16);
-  if (stride == 1)
-    return small ? launch<1, 32>(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, pad, st)
-                 : launch<1, 64>(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, pad, st);
-  return small ? launch<2, 32>(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, pad, st)
-               : launch<2, 64>(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, pad, st);
+  WgArgs a{};
+  a.G = G; a.X = X; a.dW = dW;
+  a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
+  const int TX = Cc <= 5 ? 3 : 1;
+  a.ncc = TX == 3 ? 5 : 16;
+  a.Wo4 = (Wo + 3) / 4 * 4;
+  const int xw = stride * (a.Wo4 - 1) + 3;            // staged columns incl. the left halo
+  a.XP = xw | 1;
+  a.xcols = Wi < a.XP - 1 ? Wi : a.XP - 1;             // input columns that can be touched
+  const int seg = (((Wo > a.xcols ? Wo : a.xcols) + 63) / 64);
+  if (seg > 4) return TB_ERR_UNSUPPORTED_SIZE;
+  const int prem = TX == 3 ? 3 : 2;                     // plane pitch mod 32 (bank spread of B reads)
+  a.YB = 0;
+  for (int yb : {8, 4, 2, 1}) {
+    if (yb > 1 && yb > Ho) continue;
+    const int yr = stride * (yb - 1) + 3;
+    const int pg = pad_mod32(yb * a.Wo4, 2);
+    const int pc = pad_mod32(3 * yr * a.XP, prem);
+    if (16 * pg + a.ncc * pc <= LDS_FLOATS) {
+      a.YB = yb; a.YR = yr; a.PG = pg; a.PC = pc;
+      break;
+    }
+  }
+  if (!a.YB) return TB_ERR_UNSUPPORTED_SIZE;
+  a.nyb = (Ho + a.YB - 1) / a.YB;
+  a.nchunks = (int64_t)N * Do * a.nyb;
+  const int mtiles = (M + 15) / 16;
+  a.ctiles = (Cc + a.ncc - 1) / a.ncc;
+  const size_t lds = sizeof(float) * (size_t)(16 * a.PG + a.ncc * a.PC);
+  const int by = mtiles * a.ctiles;
+  if (stride == 1) return TX == 1 ? launch_seg<1, 1>(a, seg, by, lds, st) : launch_seg<1, 3>(a, seg, by, lds, st);
+  return TX == 1 ? launch_seg<2, 1>(a, seg, by, lds, st) : launch_seg<2, 3>(a, seg, by, lds, st);
 }

@@ -17,7 +17,7 @@ __global__ __launch_bounds__(NT) void k_kspace(KspaceArgs) {
 
 template <int RS>
 hipError_t launch_kspace(const KspaceArgs& a, dim3 grid, size_t lds, hipStream_t st) {
-  hipError_t e = allow_full_lds(k_kspace<NT_TILE, RS>);
+  hipError_t e = allow_lds(k_kspace<NT_TILE, RS>, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_kspace<NT_TILE, RS>), grid, dim3(NT_TILE), lds, st, a);
   return hipGetLastError();

@@ -1,0 +1,67 @@
+// Pass B for the H extents with a compile-time plan (kspace_ct.h: H = 240, 128): per (bc, tile of
+// 16 spectrum columns), one work item per thread per phase -- H stage 0 from HBM, the fused last
+// DIF stage / op program / first DIT stage in registers, the inverse stage 0 back to HBM.
+#include "kernels.h"
+#include "kspace_ct.h"
+
+namespace tb {
+namespace {
+using ct::v2;
+
+template <int H, int T, int NT>
+__global__ __launch_bounds__(NT) void k_kspace_ct(KspaceArgs) {
+  using P = ct::TilePlan<H, T>;
+  static_assert(P::N0 <= NT && P::NM <= NT, "one item per thread per phase");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const KspaceArgs& a = kargs<KspaceArgs>();
+  const int tid = (int)threadIdx.x;
+  const int bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int ncols = a.pl.W * (a.pl.D / 2 + 1);
+  const int j0 = (int)blockIdx.x * T;
+  const int nc = (ncols - j0) < T ? (ncols - j0) : T;
+  v2* Sc = reinterpret_cast<v2*>(a.S) + (int64_t)bc * H * ncols + j0;
+  const bool act = tid < P::N0 && (tid % T) < nc;
+  v2 r[P::Q0];
+#pragma unroll
+  for (int q = 0; q < P::Q0; ++q) r[q] = ct::V(0.f, 0.f);
+  if (act) ct::b_load<P>(r, Sc, ncols, tid);
+  for (int i = tid; i < H; i += NT) lds[P::OFF_TW + i] = ct::V(a.pl.tw[0][i].x, a.pl.tw[0][i].y);
+  __syncthreads();
+  if (tid < P::N0) ct::b_s0<P>(lds, r, tid);
+  __syncthreads();
+  if (tid < P::NM) {
+    const int c = tid % T;
+    const FreqCol fc = ct::tile_col(a.pl, j0 + (c < nc ? c : 0));
+    ct::b_mid<P>(lds, a.ops.s[bcl / a.C], bcl % a.C, fc, tid);
+  }
+  __syncthreads();
+  if (act) ct::b_s1<P>(lds, Sc, ncols, tid);
+}
+
+}  // namespace
+
+bool kspace_ct_supported(int H) {
+#define TB_X(h) if (H == h) return true;
+  TB_CT_TILE_H(TB_X)
+#undef TB_X
+  return false;
+}
+
+int kspace_ct_tile() { return ct::kCtTileT; }
+
+hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st) {
+#define TB_X(h)                                                                         \
+  if (a.pl.H == h) {                                                                    \
+    constexpr size_t lds = ct::TilePlan<h, ct::kCtTileT>::LDS_BYTES;                    \
+    hipError_t e = allow_lds(k_kspace_ct<h, ct::kCtTileT, NT_TILE>, lds);               \
+    if (e != hipSuccess) return e;                                                      \
+    hipLaunchKernelGGL((k_kspace_ct<h, ct::kCtTileT, NT_TILE>), grid, dim3(NT_TILE), lds, st, a); \
+    return hipGetLastError();                                                           \
+  }
+  TB_CT_TILE_H(TB_X)
+#undef TB_X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace tb

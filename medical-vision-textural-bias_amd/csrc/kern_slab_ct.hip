@@ -1,0 +1,205 @@
+// Passes A / C for the slab shapes with a compile-time plan (slab_ct.h: W x D = 240 x 155, 128 x 128).
+//
+// One 150 KB slab fills a CU's LDS, so a workgroup cannot overlap its HBM traffic with another
+// workgroup's FFT work on the same CU.  These kernels are therefore persistent (one workgroup per
+// CU walks the (bc, h) units u = blockIdx.x, +gridDim.x, ...) and software-pipelined: the
+// first-stage inputs of unit u + gridDim.x (pass A: 2*R0 floats per item, pass C: Q1 complex per
+// item) are loaded into registers during the last phases of unit u (after the register-heavy
+// prime-radix and unpack phases, so they do not raise the peak register count), and the last stage
+// of each unit writes HBM straight from registers.  Phases inside a unit are barrier-separated (slab_ct.h lists them).
+#include "kernels.h"
+#include "slab_ct.h"
+
+namespace tb {
+namespace {
+using ct::v2;
+
+template <int W, int D, int NT>
+__global__ __launch_bounds__(NT) void k_slab_fwd_ct(SlabFwdArgs) {
+  using P = ct::SlabPlan<W, D>;
+  constexpr int SF = ct::Slots<P::N_F0, NT>::value;
+  constexpr int SU = ct::Slots<P::N_U, NT>::value;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const SlabFwdArgs& a = kargs<SlabFwdArgs>();
+  const int tid = (int)threadIdx.x;
+  const int H = a.pl.H, units = H * a.nbc;
+  DevCtx ctx{tid, NT};
+  ct::load_tw<P>(ctx, lds, a.pl);
+  v2 rf[SF][P::R0];
+  int u = (int)blockIdx.x;
+  if (u < units) {
+    const int bcl = u / H, h = u - bcl * H;
+    const float* xb = a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh;
+#pragma unroll
+    for (int s = 0; s < SF; ++s)
+      if (tid + s * NT < P::N_F0) ct::a_load<P>(rf[s], xb, a.sw, tid + s * NT);
+  }
+  for (; u < units; u += (int)gridDim.x) {
+    __syncthreads();  // the previous unit's W1 reads are done (and the twiddles are visible)
+#pragma unroll
+    for (int s = 0; s < SF; ++s)
+      if (tid + s * NT < P::N_F0) ct::a_f0<P>(lds, rf[s], tid + s * NT);
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::a_d1<P>(lds, it);
+    __syncthreads();
+    {
+      v2 ru[SU][2];
+#pragma unroll
+      for (int s = 0; s < SU; ++s)
+        if (tid + s * NT < P::N_U) ct::a_u_read<P>(lds, ru[s], tid + s * NT);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SU; ++s)
+        if (tid + s * NT < P::N_U) ct::a_u_write<P>(lds, ru[s], tid + s * NT);
+    }
+    const int un = u + (int)gridDim.x;
+    {  // next unit's first-stage inputs, in flight during W0 / W1 below (unconditional -- a clamped
+       // unit on the last pass -- so the consumed registers are dead, not carried by a phi)
+      const int uc = un < units ? un : u;
+      const int bcl = uc / H, h = uc - bcl * H;
+      const float* xb = a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh;
+#pragma unroll
+      for (int s = 0; s < SF; ++s)
+        if (tid + s * NT < P::N_F0) ct::a_load<P>(rf[s], xb, a.sw, tid + s * NT);
+    }
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::a_w0<P>(lds, it);
+    __syncthreads();
+    const int bcl = u / H, h = u - bcl * H;
+    v2* Sb = reinterpret_cast<v2*>(a.S) + ((int64_t)(a.bc0 + bcl) * H + h) * (int64_t)(W * P::Dh);
+    _Pragma("unroll 1") for (int it = tid; it < P::N_W1; it += NT) ct::a_w1<P>(lds, Sb, it);
+  }
+}
+
+template <int W, int D, int NT>
+__global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
+  using P = ct::SlabPlan<W, D>;
+  constexpr int SG = ct::Slots<P::N_W1, NT>::value;
+  constexpr int SU = ct::Slots<P::N_U, NT>::value;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[2 * NT / 64];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const SlabInvArgs& a = kargs<SlabInvArgs>();
+  const int tid = (int)threadIdx.x;
+  const int H = a.pl.H, units = H * a.nbc;
+  const int64_t sstride = (int64_t)W * P::Dh;
+  DevCtx ctx{tid, NT};
+  ct::load_tw<P>(ctx, lds, a.pl);
+  v2 rg[SG][P::Q1];
+  float lo = 3.402823466e38f, hi = -3.402823466e38f;
+  int u = (int)blockIdx.x;
+  if (u < units) {
+    const v2* Sb = reinterpret_cast<const v2*>(a.S) + ((int64_t)a.bc0 * H + u) * sstride;
+#pragma unroll
+    for (int s = 0; s < SG; ++s)
+      if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
+  }
+  for (; u < units; u += (int)gridDim.x) {
+    __syncthreads();  // the previous unit's E0 reads are done
+#pragma unroll
+    for (int s = 0; s < SG; ++s)
+      if (tid + s * NT < P::N_W1) ct::c_g0<P>(lds, rg[s], tid + s * NT);
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::c_g1<P>(lds, it);
+    __syncthreads();
+    {
+      v2 ru[SU][2];
+#pragma unroll
+      for (int s = 0; s < SU; ++s)
+        if (tid + s * NT < P::N_U) ct::c_r_read<P>(lds, ru[s], tid + s * NT);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SU; ++s)
+        if (tid + s * NT < P::N_U) ct::c_r_write<P>(lds, ru[s], tid + s * NT);
+    }
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::c_e1<P>(lds, it);
+    const int un = u + (int)gridDim.x;
+    {  // next unit's first-stage inputs, in flight during E0 below (unconditional, as in pass A)
+      const v2* Sb = reinterpret_cast<const v2*>(a.S) + ((int64_t)a.bc0 * H + (un < units ? un : u)) * sstride;
+#pragma unroll
+      for (int s = 0; s < SG; ++s)
+        if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
+    }
+    __syncthreads();
+    const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
+    float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
+    _Pragma("unroll 1") for (int it = tid; it < P::N_F0; it += NT) ct::c_e0<P>(lds, yb, a.sw, a.scale, it, lo, hi);
+    if (a.ypad > 0) {
+      const FastDiv fp = FastDiv::make(a.ypad);
+      for (int t = tid; t < W * a.ypad; t += NT) {
+        const int w = fp.div(t);
+        yb[(int64_t)w * a.sw + D + (t - w * a.ypad)] = 0.f;
+      }
+    }
+    // flush the running min/max when the next unit belongs to another sample (or there is none)
+    const int b = bc / a.C;
+    if (a.mm && (un >= units || (a.bc0 + un / H) / a.C != b)) {
+      block_minmax_atomic<NT>(lo, hi, red, a.mm + 2 * b);
+      lo = 3.402823466e38f;
+      hi = -3.402823466e38f;
+    }
+  }
+}
+
+int slab_grid(int units, size_t lds, int ncu) {
+  int per_cu = (int)(163840 / (lds ? lds : 1));
+  per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
+  const int g = ncu * per_cu;
+  return units < g ? units : g;
+}
+
+template <class K, class A>
+hipError_t launch_ct(K kern, int nt, size_t lds, int units, int ncu, const A& a, hipStream_t st) {
+  hipError_t e = allow_lds(kern, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(slab_grid(units, lds, ncu)), dim3(nt), lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// threads per workgroup: 768 (3 waves per SIMD) by default; TEXBIAS_CT_NT=512 selects 512 (tuning)
+static int ct_nt() {
+  static const int nt = [] {
+    const char* e = std::getenv("TEXBIAS_CT_NT");
+    return (e && std::atoi(e) == 512) ? 512 : 768;
+  }();
+  return nt;
+}
+
+bool slab_ct_supported(int W, int D) {
+#define TB_X(w, d) if (W == w && D == d) return true;
+  TB_CT_SLAB_SHAPES(TB_X)
+#undef TB_X
+  return false;
+}
+
+hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st) {
+  const int units = a.pl.H * a.nbc;
+#define TB_X(w, d)                                                                                  \
+  if (a.pl.W == w && a.pl.D == d) {                                                                 \
+    constexpr size_t lds = ct::SlabPlan<w, d>::LDS_BYTES;                                           \
+    if (ct_nt() == 512) return launch_ct(k_slab_fwd_ct<w, d, 512>, 512, lds, units, ncu, a, st);    \
+    return launch_ct(k_slab_fwd_ct<w, d, 768>, 768, lds, units, ncu, a, st);                        \
+  }
+  TB_CT_SLAB_SHAPES(TB_X)
+#undef TB_X
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st) {
+  const int units = a.pl.H * a.nbc;
+#define TB_X(w, d)                                                                                  \
+  if (a.pl.W == w && a.pl.D == d) {                                                                 \
+    constexpr size_t lds = ct::SlabPlan<w, d>::LDS_BYTES;                                           \
+    if (ct_nt() == 512) return launch_ct(k_slab_inv_ct<w, d, 512>, 512, lds, units, ncu, a, st);    \
+    return launch_ct(k_slab_inv_ct<w, d, 768>, 768, lds, units, ncu, a, st);                        \
+  }
+  TB_CT_SLAB_SHAPES(TB_X)
+#undef TB_X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace tb

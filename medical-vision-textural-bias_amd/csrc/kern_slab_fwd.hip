@@ -16,7 +16,7 @@ __global__ __launch_bounds__(NT) void k_slab_fwd(SlabFwdArgs) {
 
 template <int RS>
 hipError_t launch_slab_fwd(const SlabFwdArgs& a, dim3 grid, size_t lds, hipStream_t st) {
-  hipError_t e = allow_full_lds(k_slab_fwd<NT_SLAB, RS>);
+  hipError_t e = allow_lds(k_slab_fwd<NT_SLAB, RS>, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_slab_fwd<NT_SLAB, RS>), grid, dim3(NT_SLAB), lds, st, a);
   return hipGetLastError();

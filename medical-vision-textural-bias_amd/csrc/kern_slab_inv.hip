@@ -20,7 +20,7 @@ __global__ __launch_bounds__(NT) void k_slab_inv(SlabInvArgs) {
 
 template <int RS>
 hipError_t launch_slab_inv(const SlabInvArgs& a, dim3 grid, size_t lds, hipStream_t st) {
-  hipError_t e = allow_full_lds(k_slab_inv<NT_SLAB, RS>);
+  hipError_t e = allow_lds(k_slab_inv<NT_SLAB, RS>, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_slab_inv<NT_SLAB, RS>), grid, dim3(NT_SLAB), lds, st, a);
   return hipGetLastError();

@@ -7,6 +7,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+
 #include "fft_core.h"
 #include "sap_core.h"
 
@@ -24,6 +28,7 @@ struct SlabFwdArgs {
   int64_t sbc, sh, sw;
   cf* S;
   int bc0;
+  int nbc;  // volume-channels of the launch (persistent compiled-plan kernels walk H * nbc units)
 };
 
 struct KspaceArgs {
@@ -41,6 +46,7 @@ struct SlabInvArgs {
   int ypad, bc0, C;
   float scale;
   uint32_t* mm;
+  int nbc;
 };
 
 struct StatsArgs {
@@ -59,6 +65,15 @@ template <int RS> hipError_t launch_slab_fwd(const SlabFwdArgs& a, dim3 grid, si
 template <int RS> hipError_t launch_kspace(const KspaceArgs& a, dim3 grid, size_t lds, hipStream_t st);
 template <int RS> hipError_t launch_slab_inv(const SlabInvArgs& a, dim3 grid, size_t lds, hipStream_t st);
 template <int RS> hipError_t launch_kspace_stats(const StatsArgs& a, dim3 grid, size_t lds, hipStream_t st);
+
+// Compile-time slab plans (slab_ct.h, kern_slab_ct.hip): persistent passes A / C, grid from ncu.
+bool slab_ct_supported(int W, int D);
+hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st);
+hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st);
+// Compile-time pass-B plans (kspace_ct.h, kern_kspace_ct.hip): tile width kspace_ct_tile() columns.
+bool kspace_ct_supported(int H);
+int kspace_ct_tile();
+hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st);
 
 #if defined(__HIPCC__)
 struct DevCtx {
@@ -107,12 +122,24 @@ __device__ __forceinline__ void block_minmax_atomic(float lo, float hi, float* r
   }
 }
 
-// Raise a kernel's dynamic-LDS limit to the CU's full 160 KiB once per process.
+// Raise a kernel's dynamic-LDS limit to `bytes` (the launch's dynamic LDS) once per kernel: the
+// kernels share one function type, so the cache is keyed by the kernel's address.  The request is
+// the launch's own size -- 160 KiB plus a kernel's static LDS would be refused.
+template <class K>
+hipError_t allow_lds(K kern, size_t bytes) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> done;
+  const void* f = reinterpret_cast<const void*>(kern);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = done.find(f);
+  if (it != done.end() && it->second >= bytes) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) done[f] = bytes;
+  return e;
+}
 template <class K>
 hipError_t allow_full_lds(K kern) {
-  static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  return e;
+  return allow_lds(kern, 163840);
 }
 #endif
 

@@ -1,0 +1,166 @@
+// kspace_ct.h -- compile-time-planned pass B (H-axis pencils + the k-space op program).
+//
+// Pass B of the generic path (fft_core.h pass_b_body) with H fixed at compile time (two DIF
+// stages, H = Q0*Q1, e.g. 240 = 16*15), one work item per thread per phase:
+//   S0  (c, j):   H stage 0 (radix Q0, L = H/Q0) from HBM into the LDS tile [H][T]
+//   MID (c, blk): last DIF stage (radix Q1) -> op program on its Q1 coefficients -> first inverse
+//                 stage, all in registers; the op program runs ops-outermost over the butterfly's
+//                 coefficients (one decode of each op per butterfly, geometry per coefficient)
+//   S1  (c, j):   inverse H stage 0 (radix Q0) from the tile back to HBM (in place)
+// Semantics of the op program are those of apply_ops (fft_core.h), which cites the reference.
+#pragma once
+
+#include "slab_ct.h"
+
+namespace tb {
+namespace ct {
+
+template <int H_, int T_> struct TilePlan {
+  static constexpr int H = H_, T = T_;
+  static constexpr int Q0 = first_radix(H), Q1 = H / Q0, L = Q1;
+  static_assert(two_stage(H), "H must factor as two supported radices");
+  static constexpr int N0 = T * L;   // (c, j)    first DIF / last DIT stage items
+  static constexpr int NM = T * Q0;  // (c, blk)  fused middle items
+  static constexpr int OFF_TW = H * T;
+  static constexpr int TOTAL = OFF_TW + H;
+  static constexpr size_t LDS_BYTES = (size_t)TOTAL * 8;
+};
+
+// op program over the R coefficients of one butterfly; coefficient q has H frequency kh0 + kst*q
+template <int R, int H, class SO>
+TB_HD void ops_bfly(const SO& so, int chan, v2* v, const FreqCol& fc, int kh0, int kst) {
+  v2 gb[R];
+  bool in_group = false;
+  for (int o = 0; o < so.n; ++o) {
+    const tb_op& op = so.op[o];
+    const bool spike = op.kind == TB_OP_SPIKE;
+    if (spike && (!in_group || op.reserved != 1)) {
+      TB_UNROLL
+      for (int q = 0; q < R; ++q) gb[q] = v[q];
+    }
+    in_group = spike;
+    if (op.chan >= 0 && op.chan != chan) continue;
+    switch (op.kind) {
+      case TB_OP_DISK: {
+        const bool ir = op.i[0] != 0, off = op.i[1] != 0;
+        TB_UNROLL
+        for (int q = 0; q < R; ++q) {
+          const AxisGeo h = axis_geo(kh0 + kst * q, H);
+          const int sq = h.dsq + fc.dsq;
+          bool in = ir ? ((int64_t)sq < op.l) : ((float)sq < op.f[0]);
+          if (off) in = !in;
+          v[q] = in ? v[q] : V(0.f, 0.f);
+        }
+      } break;
+      case TB_OP_GIBBS: {
+        TB_UNROLL
+        for (int q = 0; q < R; ++q) {
+          const AxisGeo h = axis_geo(kh0 + kst * q, H);
+          const float m = 0.5f * (((int64_t)(h.ef + fc.ef) <= op.l ? 1.f : 0.f) +
+                                  ((int64_t)(h.en + fc.en) <= op.l ? 1.f : 0.f));
+          v[q] = m * v[q];
+        }
+      } break;
+      case TB_OP_LAYER: {
+        TB_UNROLL
+        for (int q = 0; q < R; ++q) {
+          const AxisGeo h = axis_geo(kh0 + kst * q, H);
+          const float m = 0.5f * ((layer_in(op, h.ef + fc.ef) ? 1.f : 0.f) + (layer_in(op, h.en + fc.en) ? 1.f : 0.f));
+          v[q] = m * v[q];
+        }
+      } break;
+      case TB_OP_WRAP: {
+        const float a = op.f[0];
+        TB_UNROLL
+        for (int q = 0; q < R; ++q) {
+          const int nodd = axis_geo(kh0 + kst * q, H).odd + fc.odd;
+          const float m = nodd == 0 ? 1.f : (nodd == 1 ? a : (nodd == 2 ? a * a : a * a * a));
+          v[q] = m * v[q];
+        }
+      } break;
+      case TB_OP_SPIKE: {
+        if (fc.kw == op.i[1] && fc.kd == op.i[2]) {  // this column holds f (at most one coefficient)
+          TB_UNROLL
+          for (int q = 0; q < R; ++q) {
+            if (kh0 + kst * q == op.i[0]) {
+              const cf g = mk(gb[q].x, gb[q].y);
+              const cf d = sub(spike_target(op, g), g);
+              v[q] += 0.5f * V(d.x, d.y);
+            }
+          }
+        }
+        if (fc.nkw == op.i[1] && fc.nkd == op.i[2]) {  // ... or -f
+          TB_UNROLL
+          for (int q = 0; q < R; ++q) {
+            if (negk(kh0 + kst * q, H) == op.i[0]) {
+              const cf kf = mk(gb[q].x, -gb[q].y);
+              const cf d = sub(spike_target(op, kf), kf);
+              v[q] += 0.5f * V(d.x, -d.y);
+            }
+          }
+        }
+      } break;
+      default: break;
+    }
+  }
+}
+
+// S0 item (c, j): loads (global, column c of the tile) then DFT + twiddles into the LDS tile
+template <class P>
+TB_HD void b_load(v2* r, const v2* __restrict__ Sc, int64_t ncols, int it) {
+  const int j = it / P::T, c = it - j * P::T;
+  const v2* s = Sc + (int64_t)j * ncols + c;
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) r[q] = s[(int64_t)(q * P::L) * ncols];
+}
+template <class P>
+TB_HD void b_s0(v2* lds, v2* a, int it) {
+  const int j = it / P::T, c = it - j * P::T;
+  const v2* tw = lds + P::OFF_TW;
+  Dv<P::Q0, true>::run(a);
+  v2* t = lds + j * P::T + c;
+  t[0] = a[0];
+  TB_UNROLL
+  for (int q = 1; q < P::Q0; ++q) t[q * P::L * P::T] = j ? cmul(a[q], tw[j * q]) : a[q];
+}
+template <class P, class SO>
+TB_HD void b_mid(v2* lds, const SO& so, int chan, const FreqCol& fc, int it) {
+  const int blk = it / P::T, c = it - blk * P::T;
+  v2* t = lds + (blk * P::L) * P::T + c;
+  v2 a[P::Q1];
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) a[q] = t[q * P::T];
+  Dv<P::Q1, true>::run(a);
+  ops_bfly<P::Q1, P::H>(so, chan, a, fc, blk, P::Q0);  // slot blk*L + q holds kh = blk + Q0*q
+  Dv<P::Q1, false>::run(a);
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) t[q * P::T] = a[q];
+}
+template <class P>
+TB_HD void b_s1(const v2* lds, v2* __restrict__ Sc, int64_t ncols, int it) {
+  const int j = it / P::T, c = it - j * P::T;
+  const v2* tw = lds + P::OFF_TW;
+  const v2* t = lds + j * P::T + c;
+  v2 a[P::Q0];
+  a[0] = t[0];
+  TB_UNROLL
+  for (int q = 1; q < P::Q0; ++q) a[q] = j ? cmulc(t[q * P::L * P::T], tw[j * q]) : t[q * P::L * P::T];
+  Dv<P::Q0, false>::run(a);
+  v2* s = Sc + (int64_t)j * ncols + c;
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) s[(int64_t)(q * P::L) * ncols] = a[q];
+}
+
+// column geometry of tile column c (spectrum column j0 + c = w' * Dh + kd)
+TB_HD FreqCol tile_col(const tb_plan_dev& pl, int col) {
+  const int Dh = pl.D / 2 + 1;
+  const int wp = col / Dh;
+  return freq_col(pl.irev_w[wp], col - wp * Dh, pl.W, pl.D);
+}
+
+// H extents with a compile-time pass-B plan in the device library (tile width T = 16 columns)
+#define TB_CT_TILE_H(X) X(240) X(128)
+constexpr int kCtTileT = 16;
+
+}  // namespace ct
+}  // namespace tb

@@ -27,6 +27,12 @@ using namespace tb;
 namespace {
 
 thread_local int g_last_hip = 0;
+// compiled (compile-time) plans enabled: TEXBIAS_COMPILED_PLANS=0 or tb_set_compiled_plans(0) turns
+// them off, e.g. to compare against the generic passes
+bool g_compiled_plans = [] {
+  const char* e = std::getenv("TEXBIAS_COMPILED_PLANS");
+  return !(e && e[0] == '0');
+}();
 
 inline int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -180,6 +186,9 @@ struct tb_plan {
   int rset_h = RS_ALL;   // radix set of the H axis (pass B)
   int rset_wd = RS_ALL;  // radix set of the W and D axes (passes A, C)
   int lds_max = 65536;
+  int ncu = 256;         // compute units (grid of the persistent compiled-plan slab kernels)
+  bool ct_slab = false;  // (W, D) has a compile-time slab plan (slab_ct.h)
+  bool ct_tile = false;  // H has a compile-time pass-B plan (kspace_ct.h)
 };
 
 namespace {
@@ -238,6 +247,12 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   int lds = 0;
   if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess && lds > 0)
     p->lds_max = lds;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+    p->ncu = ncu;
+  // compile-time slab plan: same shape and therefore the same radix order as the runtime plan
+  p->ct_slab = tb::slab_ct_supported(W, D);
+  p->ct_tile = tb::kspace_ct_supported(H);
   const SlabGeo sg = slab_geo(W, D);
   if ((size_t)sg.total_cf * 8 > (size_t)p->lds_max) { delete p; return TB_ERR_UNSUPPORTED_SIZE; }
   // device tables: tw[H], tw[W], tw[D] (cf) + rev_d[D], irev_h[H], irev_w[W] (int)
@@ -299,11 +314,17 @@ int tb_plan_radices(const tb_plan* plan, int axis, int* radices) {
   return a.nst;
 }
 
+static bool use_ct_slab(const tb_plan* p) { return g_compiled_plans && p->ct_slab; }
+
 template <int RS>
 static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, cf* S, int bc0, int nbc,
                            hipStream_t st) {
+  SlabFwdArgs a{p->dev, x, xs[0], xs[1], xs[2], S, bc0, nbc};
+  if (use_ct_slab(p)) {
+    TB_HIP(tb::launch_slab_fwd_ct(a, p->ncu, st));
+    return TB_OK;
+  }
   const size_t lds = (size_t)slab_geo(p->dev.W, p->dev.D).total_cf * sizeof(cf);
-  SlabFwdArgs a{p->dev, x, xs[0], xs[1], xs[2], S, bc0};
   TB_HIP(tb::launch_slab_fwd<RS>(a, dim3(p->dev.H, nbc), lds, st));
   return TB_OK;
 }
@@ -342,13 +363,22 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     }
     {
       Timer t(1, st);
-      KspaceArgs ka{p->dev, S, b0 * C, C, T, 0, bo};
-      TB_HIP(launch_kspace<RB>(ka, dim3(ntiles, nb * C), lds_b, st));
+      if (g_compiled_plans && p->ct_tile) {
+        const int Tc = tb::kspace_ct_tile();
+        KspaceArgs ka{p->dev, S, b0 * C, C, Tc, 0, bo};
+        TB_HIP(tb::launch_kspace_ct(ka, dim3((W * (D / 2 + 1) + Tc - 1) / Tc, nb * C), st));
+      } else {
+        KspaceArgs ka{p->dev, S, b0 * C, C, T, 0, bo};
+        TB_HIP(launch_kspace<RB>(ka, dim3(ntiles, nb * C), lds_b, st));
+      }
     }
     {
       Timer t(2, st);
-      SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, b0 * C, C, scale, minmax};
-      TB_HIP(launch_slab_inv<RA>(ia, dim3(H, nb * C), lds_s, st));
+      SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, b0 * C, C, scale, minmax, nb * C};
+      if (use_ct_slab(p))
+        TB_HIP(tb::launch_slab_inv_ct(ia, p->ncu, st));
+      else
+        TB_HIP(launch_slab_inv<RA>(ia, dim3(H, nb * C), lds_s, st));
     }
   }
   return TB_OK;
@@ -450,6 +480,11 @@ int tb_disk_mask_f32(float* mask, int64_t outer, int n0, int n1, int n2, int int
   hipLaunchKernelGGL(k_disk_mask, dim3((unsigned)blocks), dim3(256), 0, st, mask, outer, n0, n1, n2, int_r, r2i, r2f,
                      inside_off);
   TB_HIP(hipGetLastError());
+  return TB_OK;
+}
+
+int tb_set_compiled_plans(int enable) {
+  g_compiled_plans = enable != 0;
   return TB_OK;
 }
 

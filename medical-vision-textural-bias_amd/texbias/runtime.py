@@ -304,6 +304,12 @@ def logabs_sums(x: torch.Tensor, n_dims: int, programs: Sequence[Sequence], chan
     return out
 
 
+def set_compiled_plans(enable: bool) -> None:
+    """Passes A/C on the compile-time slab plans (240x155, 128x128) when True (default), else the
+    generic run-time-planned kernels (tb_set_compiled_plans)."""
+    check(lib().tb_set_compiled_plans(1 if enable else 0))
+
+
 def set_pass_timing(enable: bool) -> None:
     check(lib().tb_set_pass_timing(1 if enable else 0))
 

@@ -171,3 +171,51 @@ def test_tile_width_independent():
     y1, _ = _emu.kspace_filter(x[None], 3, [prog], T=7)
     y2, _ = _emu.kspace_filter(x[None], 3, [prog], T=64)
     np.testing.assert_array_equal(y1, y2)
+
+
+@pytest.mark.parametrize("shape", [(3, 5, 24, 35), (2, 4, 20, 28), (1, 3, 240, 155), (1, 2, 128, 128)])
+def test_compiled_slab_plan(shape):
+    """Passes A/C through the compile-time slab plan (slab_ct.h) == oracle, and == the generic path to
+    rounding; pads zeroed, min/max epilogue exact."""
+    rng = np.random.default_rng(sum(shape))
+    x = rng.standard_normal(shape).astype(np.float32)
+    geo = K.geometry(x.shape[1:])
+    idx = (1, min(3, shape[2] - 1), min(7, shape[3] // 2))
+    prog = [K.disk_op(0.3 * min(shape[1:]), False), K.spike_op(idx, geo, 6.0, phase=0.7), K.wrap_op(0.5)]
+    yc, mmc = _emu.kspace_filter(x[None], 3, [prog], pad=3, ct=True)
+    yg, _ = _emu.kspace_filter(x[None], 3, [prog], pad=3, ct=False)
+    ref = O.wrap_artifact(O.plane_waves(O.fourier_disk(x, 0.3 * min(shape[1:])), idx, 6.0, phase=[0.7] * shape[0]), 0.5)
+    assert relerr(yc[0, ..., :shape[-1]], ref) < TOL
+    assert relerr(yc, yg) < 2e-6
+    assert np.all(yc[0, ..., shape[-1]:] == 0)
+    y0 = yc[0, ..., :shape[-1]]
+    np.testing.assert_array_equal(mmc[0], [y0.min(), y0.max()])
+
+
+def test_compiled_slab_identity():
+    x = np.random.default_rng(3).standard_normal((2, 2, 6, 240, 155)).astype(np.float32)
+    y, mm = _emu.kspace_filter(x, 3, [[], []], ct=True)
+    assert relerr(y, x) < 2e-6
+
+
+@pytest.mark.parametrize("shape", [(2, 20, 24, 35), (2, 36, 20, 28), (1, 128, 20, 28), (1, 240, 24, 35)])
+def test_compiled_tile_plan(shape):
+    """Pass B through the compile-time tile plan (kspace_ct.h, H in {20, 36, 128, 240}) together with
+    the compiled slab passes: == oracle for disk/spike/wrap/Gibbs and a grouped pair of spikes."""
+    rng = np.random.default_rng(sum(shape) + 1)
+    x = rng.standard_normal(shape).astype(np.float32)
+    sp = x.shape[1:]
+    geo = K.geometry(sp)
+    idx = (min(5, sp[0] - 1), min(3, sp[1] - 1), min(7, sp[2] // 2))
+    prog = [K.disk_op(0.3 * min(sp), False), K.spike_op(idx, geo, 6.0, phase=0.7), K.wrap_op(0.5)]
+    yc, _ = _emu.kspace_filter(x[None], 3, [prog], ct=True)
+    ref = O.wrap_artifact(O.plane_waves(O.fourier_disk(x, 0.3 * min(sp)), idx, 6.0, phase=[0.7] * shape[0]), 0.5)
+    assert relerr(yc[0], ref) < TOL
+    yg, _ = _emu.kspace_filter(x[None], 3, [[K.gibbs_op(0.4, sp)]], ct=True)
+    assert relerr(yg[0], O.gibbs_noise(x, 0.4)) < TOL
+    # two spikes of one KSpaceSpikeNoise call (grouped), per channel
+    prog2 = [K.spike_op(idx, geo, 5.0, phase=0.1, chan=0), K.spike_op((1, 1, 1), geo, 7.0, phase=-0.3, chan=0)]
+    prog2[1].reserved = 1
+    y2c, _ = _emu.kspace_filter(x[None], 3, [prog2], ct=True)
+    y2g, _ = _emu.kspace_filter(x[None], 3, [prog2], ct=False)
+    assert relerr(y2c, y2g) < 2e-6

@@ -182,3 +182,34 @@ def test_default_intensity_stats(rt):
     n = np.prod(a["x"].shape[1:])
     dflt = s / n * 2.5
     np.testing.assert_allclose(dflt, O.kspace_default_intensity(a["x"]), rtol=2e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 240, 240, 155), (1, 4, 128, 128, 128)])
+def test_compiled_slab_plan_matches_generic(rt, shape):
+    """Passes A/C on the compile-time slab plans == the generic passes (to rounding) and == the
+    oracle on one channel; D padding zeroed; per-sample min/max keys identical in value."""
+    torch.manual_seed(5)
+    x = torch.randn(shape, device="cuda")
+    geo = K.geometry(shape[2:])
+    idx = (9, 17, 23)
+    prog = [K.disk_op(12.5, False), K.spike_op(idx, geo, 12.0, phase=0.4), K.wrap_op(0.5)]
+    B = shape[0]
+    mm_c = torch.empty((B, 2), dtype=torch.int32, device="cuda")
+    mm_g = torch.empty((B, 2), dtype=torch.int32, device="cuda")
+    try:
+        rt.set_compiled_plans(True)
+        yc = rt.kspace_filter(x, 3, [prog] * B, shape[1], pad=5, minmax=mm_c)
+        rt.set_compiled_plans(False)
+        yg = rt.kspace_filter(x, 3, [prog] * B, shape[1], pad=5, minmax=mm_g)
+    finally:
+        rt.set_compiled_plans(True)
+    torch.cuda.synchronize()
+    assert torch.all(yc[..., shape[-1]:] == 0)
+    assert (yc - yg).abs().max().item() / yg.abs().max().item() < 2e-6
+    x0 = x[B - 1, 1].cpu().numpy()
+    ref = O.wrap_artifact(O.plane_waves(O.fourier_disk(x0[None], 12.5), idx, 12.0, phase=[0.4]), 0.5)[0]
+    assert relerr(yc[B - 1, 1, ..., :shape[-1]].cpu().numpy(), ref) < TOL
+    yv = yc[..., :shape[-1]].reshape(B, -1)
+    mmf = rt.keys_to_float(mm_c)
+    np.testing.assert_array_equal(mmf[:, 0], yv.min(1).values.cpu().numpy())
+    np.testing.assert_array_equal(mmf[:, 1], yv.max(1).values.cpu().numpy())
