@@ -144,6 +144,25 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
                         int Hi, int Wi, int stride, int pad, void* stream);
 
 /*
+ * Dice statistics of DiceLoss(sigmoid, squared_pred) (MONAI 0.5 formula, used by the reference's
+ * train step stylized_gibbs12p5.py:201): for NC instances of S contiguous voxels of logits x and
+ * target t, sums[nc] = {sum t p, sum t^2 (t), sum p^2 (p)} in float64 (DEVICE double[NC][3],
+ * overwritten), p = sigmoid(x) if sigmoid else x.  The backward writes dx from the sums' gradients
+ * g (DEVICE float[NC][3]).
+ */
+int tb_dice_sums_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, int sigmoid, int squared,
+                     void* stream);
+int tb_dice_sums_bwd_f32(const float* x, const float* t, const float* g, float* dx, int64_t NC, int64_t S, int sigmoid,
+                         int squared, void* stream);
+
+/*
+ * out[c] = sum over n < N, s < S of x[n][c][s] (x contiguous [N][C][S], device; out DEVICE float[C],
+ * overwritten): the bias gradient of a Conv3d / ConvTranspose3d, grad_out summed over (N, D, H, W)
+ * -- replaces ATen's generic reduction in the U-Net backward (stylized_gibbs12p5.py:232-243).
+ */
+int tb_channel_sum_f32(const float* x, float* out, int64_t N, int64_t C, int64_t S, void* stream);
+
+/*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
  * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution
  * (MONAI Convolution, used by 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-199).

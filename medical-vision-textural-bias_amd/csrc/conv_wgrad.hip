@@ -23,6 +23,8 @@
 // leave each block once, by float atomics into dW (zeroed first).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "texbias.h"
 
 namespace {
@@ -180,8 +182,13 @@ int launch(const WgArgs& a, int blocks_y, size_t lds, hipStream_t st) {
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_wgrad<S, TX, SEG>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return TB_ERR_HIP;
-  // two blocks per CU over the whole chip, never more chunks than exist
-  int64_t gx = (512 + blocks_y - 1) / blocks_y;
+  // two blocks per CU over the whole chip (TEXBIAS_WGRAD_BLOCKS overrides, tuning), never more
+  // chunks than exist
+  static const int target = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_BLOCKS");
+    return e ? std::atoi(e) : 512;
+  }();
+  int64_t gx = (target + blocks_y - 1) / blocks_y;
   if (gx > a.nchunks) gx = a.nchunks;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL((k_conv3d_wgrad<S, TX, SEG>), dim3((unsigned)gx, (unsigned)blocks_y), dim3(NT), lds, st, a);
@@ -222,8 +229,12 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
   if (seg > 4) return TB_ERR_UNSUPPORTED_SIZE;
   const int prem = TX == 3 ? 3 : 2;                     // plane pitch mod 32 (bank spread of B reads)
   a.YB = 0;
+  static const int yb_max = [] {  // TEXBIAS_WGRAD_YB caps the rows per chunk (tuning)
+    const char* e = std::getenv("TEXBIAS_WGRAD_YB");
+    return e ? std::atoi(e) : 8;
+  }();
   for (int yb : {8, 4, 2, 1}) {
-    if (yb > 1 && yb > Ho) continue;
+    if ((yb > 1 && yb > Ho) || yb > yb_max) continue;
     const int yr = stride * (yb - 1) + 3;
     const int pg = pad_mod32(yb * a.Wo4, 2);
     const int pc = pad_mod32(3 * yr * a.XP, prem);

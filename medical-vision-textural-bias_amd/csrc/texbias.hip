@@ -134,11 +134,18 @@ __global__ __launch_bounds__(NT) void k_salt_pepper(const float* __restrict__ x,
     for (int q = 0; q < 4; ++q) {
       const int64_t i = 4 * g + q;
       if (i >= n) break;
-      const int64_t row = i / len;
-      const int64_t off = b * sb + row * ld + (i - row * len);
+      // element offset of voxel i; 32-bit division while the sample fits (the 64-bit one is ~4x the
+      // VALU work), and in the sparse Philox path only for the ~p of voxels that are written
+      auto offset_of = [&]() -> int64_t {
+        const int64_t row = n < 0x7fffffff ? (int64_t)((uint32_t)i / (uint32_t)len) : i / len;
+        return b * sb + row * ld + (i - row * len);
+      };
       float u;
-      if (uin) u = uin[off];
-      else {
+      int64_t off = -1;
+      if (uin) {
+        off = offset_of();
+        u = uin[off];
+      } else {
         // counter of logical voxel L = lin0 + i: the group index and lane of L itself, so the
         // stream is independent of how samples are batched when n % 4 == 0 (the usual case)
         if ((lin0 & 3) == 0) u = u01(r.v[q]);
@@ -148,11 +155,14 @@ __global__ __launch_bounds__(NT) void k_salt_pepper(const float* __restrict__ x,
         }
       }
       const int c = sap_class(u, lo, hi);
-      if (cls) cls[off] = (int8_t)c;
-      if (sparse) {
-        if (c) y[off] = c == 1 ? vmin : vmax;
-      } else {
-        y[off] = c == 0 ? x[off] : (c == 1 ? vmin : vmax);
+      if (cls || !sparse || c) {
+        if (off < 0) off = offset_of();
+        if (cls) cls[off] = (int8_t)c;
+        if (sparse) {
+          if (c) y[off] = c == 1 ? vmin : vmax;
+        } else {
+          y[off] = c == 0 ? x[off] : (c == 1 ? vmin : vmax);
+        }
       }
     }
   }

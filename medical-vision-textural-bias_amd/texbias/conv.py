@@ -1,10 +1,12 @@
 """Conv3d / ConvTranspose3d whose weight gradient runs on the texbias MFMA split-K kernel.
 
 Forward and input-gradient stay on MIOpen/CK (``aten.convolution_backward`` with the weight
-output masked off); the weight gradient of 3x3x3 layers with a long reduction (the U-Net's
-full- and half-resolution levels, where MIOpen falls back to naive or non-split-K kernels at
-~350 ms per layer on gfx950) goes to ``tb_conv3d_wgrad_f32``.  Parameter names and shapes are
-those of ``nn.Conv3d`` / ``nn.ConvTranspose3d``, so state dicts are interchangeable.
+and bias outputs masked off); the weight gradient of 3x3x3 layers with a long reduction (the
+U-Net's full- and half-resolution levels, where MIOpen falls back to naive or non-split-K kernels
+at ~350 ms per layer on gfx950) goes to ``tb_conv3d_wgrad_f32``, and every bias gradient (grad_out
+summed over N, D, H, W -- ATen's generic reduction ran at 0.1-0.3 TB/s, ~7 ms of a 46 ms step) to
+``tb_channel_sum_f32``.  Parameter names and shapes are those of ``nn.Conv3d`` /
+``nn.ConvTranspose3d``, so state dicts are interchangeable.
 """
 from __future__ import annotations
 
@@ -42,10 +44,27 @@ def wgrad(G: torch.Tensor, X: torch.Tensor, w_shape, stride: int, pad: int) -> t
     return dW.view(w_shape)
 
 
+def channel_sum(g: torch.Tensor) -> torch.Tensor:
+    """g [N, C, *spatial] -> [C]: sum over N and the spatial axes (tb_channel_sum_f32)."""
+    g = g.contiguous()
+    N, Cc = g.shape[:2]
+    out = torch.empty(Cc, dtype=torch.float32, device=g.device)
+    with torch.cuda.device(g.device):
+        check(lib().tb_channel_sum_f32(g.data_ptr(), out.data_ptr(), N, Cc, g[0, 0].numel(), _stream(g)),
+              "tb_channel_sum_f32")
+    return out
+
+
+def custom_backward_applies(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """float32 HIP tensors: the layer's backward goes through _ConvFn (texbias bias/weight grads)."""
+    return ENABLED and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32
+
+
 def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, padding, transposed: bool) -> bool:
-    if not ENABLED or not (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32):
+    if not custom_backward_applies(x, w):
         return False
-    if tuple(w.shape[2:]) != (3, 3, 3) or len(set(stride)) != 1 or stride[0] not in (1, 2) or len(set(padding)) != 1:
+    if tuple(w.shape[2:]) != (3, 3, 3) or len(set(stride)) != 1 or stride[0] not in (1, 2) or padding[0] != 1 or \
+            len(set(padding)) != 1:
         return False
     pos = x.shape[0] * math.prod(out_spatial if not transposed else x.shape[2:])
     return pos >= MIN_K_PER_OUTPUT * w.shape[0] * w.shape[1] * 27 // 16
@@ -53,47 +72,53 @@ def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, pa
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, output_padding, transposed):
+    def forward(ctx, x, w, b, stride, padding, output_padding, transposed, fast_w):
         if transposed:
             y = F.conv_transpose3d(x, w, b, stride, padding, output_padding)
         else:
             y = F.conv3d(x, w, b, stride, padding)
         ctx.save_for_backward(x, w)
-        ctx.cfg = (stride, padding, output_padding, transposed, b is not None)
+        ctx.cfg = (stride, padding, output_padding, transposed, b is not None, fast_w)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        stride, padding, output_padding, transposed, has_b = ctx.cfg
+        stride, padding, output_padding, transposed, has_b, fast_w = ctx.cfg
         gy = gy.contiguous()
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         gx = gb = gw = None
-        if need_x or (need_b and has_b):
-            cout = w.shape[1] if transposed else w.shape[0]
-            gx, _, gb = torch.ops.aten.convolution_backward(
-                gy, x, w, [cout] if has_b else None, list(stride), list(padding), [1, 1, 1], transposed,
-                list(output_padding), 1, [need_x, False, need_b and has_b])
-        if need_w:
+        lib_w = need_w and not fast_w
+        if need_x or lib_w:
+            gx, gw, _ = torch.ops.aten.convolution_backward(
+                gy, x, w, None, list(stride), list(padding), [1, 1, 1], transposed, list(output_padding), 1,
+                [need_x, lib_w, False])
+        if need_w and fast_w:
             if transposed:   # dW[ci][co] = corr(x, gy)
                 gw = wgrad(x, gy, w.shape, stride[0], padding[0])
             else:            # dW[co][ci] = corr(gy, x)
                 gw = wgrad(gy, x, w.shape, stride[0], padding[0])
-        return gx, gw, gb, None, None, None, None
+        if need_b and has_b:
+            gb = channel_sum(gy)
+        return gx, gw, gb, None, None, None, None, None
 
 
 class Conv3d(nn.Conv3d):
     def forward(self, x):
-        out_sp = [(n + 2 * p - 3) // s + 1 for n, p, s in zip(x.shape[2:], self.padding, self.stride)]
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
-                fast_wgrad_applies(x, self.weight, out_sp, self.stride, self.padding, False):
-            return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, (0, 0, 0), False)
+                custom_backward_applies(x, self.weight):
+            k = self.weight.shape[2:]
+            out_sp = [(n + 2 * p - kk) // s + 1 for n, p, s, kk in zip(x.shape[2:], self.padding, self.stride, k)]
+            fast = fast_wgrad_applies(x, self.weight, out_sp, self.stride, self.padding, False)
+            return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, (0, 0, 0), False, fast)
         return super().forward(x)
 
 
 class ConvTranspose3d(nn.ConvTranspose3d):
     def forward(self, x, output_size=None):
         if output_size is None and self.groups == 1 and self.dilation == (1, 1, 1) and \
-                fast_wgrad_applies(x, self.weight, None, self.stride, self.padding, True):
-            return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, self.output_padding, True)
+                custom_backward_applies(x, self.weight):
+            fast = fast_wgrad_applies(x, self.weight, None, self.stride, self.padding, True)
+            return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, self.output_padding, True,
+                                 fast)
         return super().forward(x, output_size)
