@@ -63,6 +63,20 @@ def algorithmic_bytes(bc, H, W, D, pad):
     return {"slab_fwd": real + spec, "kspace": 2 * spec, "slab_inv": spec + outp}
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1b", "traffic.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of a filter pass from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), or None when not measured for this build."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rec = json.load(f)["kernels"].get(kernel)
+        return int(rec["traffic_bytes"]) if rec else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(x0: np.ndarray, args) -> dict:
     """The reference's CPU filter path restated op for op (oracle/, numpy complex64, 1 thread)."""
     from oracle import filters_oracle as O
@@ -196,7 +210,9 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": (pmc_traffic(dom) if (H, W, D, B) == (240, 240, 155, 2) else None),
+                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r1b/traffic.json)",
                          "algorithmic_bytes_per_launch": nbytes[dom]},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),

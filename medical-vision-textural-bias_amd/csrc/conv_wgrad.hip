@@ -33,6 +33,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;
 constexpr int LDS_FLOATS = 78 * 1024 / 4;
+constexpr int kSlack = 16;  // floats after the carve: the pipelined operand read one k-step past a row
 
 struct WgArgs {
   const float* G;
@@ -69,19 +70,21 @@ __global__ __launch_bounds__(NT) void k_conv3d_wgrad(WgArgs a) {
   constexpr int NTAP = TX == 1 ? 27 : 9;
   constexpr int TPW = (NTAP + 3) / 4;  // taps per wave (the last wave may have one fewer)
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* gs = smem;                 // [16][PG]          row m: YB rows of Wo4 (zero beyond Wo)
-  float* xs = smem + 16 * a.PG;     // [ncc][PC]         plane c: [3 tz][YR rows][XP], col 0 = left halo
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int mt = (int)blockIdx.y / a.ctiles, ct = (int)blockIdx.y - mt * a.ctiles;
   const int m0 = mt * 16, c0 = ct * a.ncc;
   const int mv = min(16, a.M - m0), cv = min(a.ncc, a.Cc - c0);
-  const int nlds = 16 * a.PG + a.ncc * a.PC;
+  // the carve holds only this block's mv rows and cv channel planes; lanes of absent rows / columns
+  // read row 0 / plane 0 (their MFMA results are never stored)
+  float* gs = smem;               // [mv][PG]   row m: YB rows of Wo4 (zero beyond Wo)
+  float* xs = smem + mv * a.PG;   // [cv][PC]   plane c: [3 tz][YR rows][XP], col 0 = left halo
+  const int nlds = mv * a.PG + cv * a.PC + kSlack;
   for (int i = tid; i < nlds; i += NT) smem[i] = 0.f;   // halos, x >= Wo, absent m / c stay zero
   const int li = lane & 15, lk = lane >> 4;
   int boff;
   if (TX == 1) {
-    boff = li * a.PC;
+    boff = (li < cv ? li : 0) * a.PC;
   } else {
     const int c = li / 3, tx = li - 3 * c;
     boff = c < cv ? c * a.PC + tx : 0;
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(NT) void k_conv3d_wgrad(WgArgs a) {
   int toff[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
-    const int t = wave + 4 * j;
+    const int t = wave + 4 * j < NTAP ? wave + 4 * j : 0;
     toff[j] = TX == 1 ? ((t / 9) * a.YR + (t / 3) % 3) * a.XP + t % 3 : ((t / 3) * a.YR + t % 3) * a.XP;
   }
   f32x4 acc[TPW];
@@ -134,17 +137,26 @@ __global__ __launch_bounds__(NT) void k_conv3d_wgrad(WgArgs a) {
         }
       }
     __syncthreads();
+    // k-steps of 4 x positions: every wave runs TPW taps with no per-tap branch (a wave's taps past
+    // NTAP read a valid address and are never stored); the operands of step x0 + 4 are read while
+    // the MFMAs of step x0 run (the read past the row end stays inside the carve's slack)
     for (int yy = 0; yy < a.YB; ++yy) {
-      const float* ga = gs + li * a.PG + yy * a.Wo4 + lk;
+      const float* ga = gs + (li < mv ? li : 0) * a.PG + yy * a.Wo4 + lk;
       const float* xq = xs + boff + (S * yy) * a.XP + S * lk;
-#pragma unroll 2
-      for (int x0 = 0; x0 < a.Wo4; x0 += 4) {
-        const float av = ga[x0];
+      float av = ga[0];
+      float bv[TPW];
 #pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-          if (wave + 4 * j < NTAP)
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xq[toff[j] + S * x0], acc[j], 0, 0, 0);
-        }
+      for (int j = 0; j < TPW; ++j) bv[j] = xq[toff[j]];
+      for (int x0 = 0; x0 < a.Wo4; x0 += 4) {
+        const float an = ga[x0 + 4];
+        float bn[TPW];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) bn[j] = xq[toff[j] + S * (x0 + 4)];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
+        av = an;
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) bv[j] = bn[j];
       }
     }
     __syncthreads();
@@ -238,7 +250,7 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
     const int yr = stride * (yb - 1) + 3;
     const int pg = pad_mod32(yb * a.Wo4, 2);
     const int pc = pad_mod32(3 * yr * a.XP, prem);
-    if (16 * pg + a.ncc * pc <= LDS_FLOATS) {
+    if ((M < 16 ? M : 16) * pg + (Cc < a.ncc ? Cc : a.ncc) * pc + kSlack <= LDS_FLOATS) {
       a.YB = yb; a.YR = yr; a.PG = pg; a.PC = pc;
       break;
     }
@@ -248,7 +260,7 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
   a.nchunks = (int64_t)N * Do * a.nyb;
   const int mtiles = (M + 15) / 16;
   a.ctiles = (Cc + a.ncc - 1) / a.ncc;
-  const size_t lds = sizeof(float) * (size_t)(16 * a.PG + a.ncc * a.PC);
+  const size_t lds = sizeof(float) * (size_t)((M < 16 ? M : 16) * a.PG + (Cc < a.ncc ? Cc : a.ncc) * a.PC + kSlack);
   const int by = mtiles * a.ctiles;
   if (stride == 1) return TX == 1 ? launch_seg<1, 1>(a, seg, by, lds, st) : launch_seg<1, 3>(a, seg, by, lds, st);
   return TX == 1 ? launch_seg<2, 1>(a, seg, by, lds, st) : launch_seg<2, 3>(a, seg, by, lds, st);
