@@ -163,6 +163,17 @@ int tb_dice_sums_bwd_f32(const float* x, const float* t, const float* g, float* 
 int tb_channel_sum_f32(const float* x, float* out, int64_t N, int64_t C, int64_t S, void* stream);
 
 /*
+ * Direct 3x3x3 convolution, stride 1, padding 1, for Cin, Cout <= 4 (the U-Net's full-resolution
+ * 3 -> 3 ResidualUnit conv, where the implicit-GEMM library kernels run at ~1 TFLOP/s):
+ *   y[n][co][z][h][w] = b[co] + sum w[co][ci][tz][ty][tx] x[n][ci][z+tz-1][h+ty-1][w+tx-1]
+ * x [N][Cin][D][H][W], w [Cout][Cin][3][3][3], b [Cout] or NULL, y [N][Cout][D][H][W] (device,
+ * contiguous); W <= 168.  The input gradient is the same call on grad_y with the flipped,
+ * channel-transposed weights.
+ */
+int tb_conv3d_small_f32(const float* x, const float* w, const float* b, float* y, int N, int Cin, int Cout, int D,
+                        int H, int W, void* stream);
+
+/*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
  * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution
  * (MONAI Convolution, used by 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-199).

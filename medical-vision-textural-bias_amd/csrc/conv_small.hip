@@ -1,0 +1,116 @@
+// conv_small.hip -- direct 3x3x3 convolution (stride 1, padding 1) for few channels (Cin, Cout <= 4).
+//
+// The U-Net the reference trains (MONAI UNet, 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-199)
+// ends in a full-resolution ResidualUnit(3, 3): a 3 -> 3 Conv3d over 2 x 240 x 240 x 160 voxels.
+// With 3 channels the implicit-GEMM library kernels (CK via MIOpen) run at ~1 TFLOP/s (3.5 ms
+// forward, 4.8 ms input gradient per step).  The layer is a stencil: each output needs 27 * Cin
+// inputs and Cout * 27 * Cin FMAs, so a direct kernel is bound by one HBM sweep of x and y.
+//
+//   y[n][co][z][h][w] = b[co] + sum_{ci, tz, ty, tx} wt[co][ci][tz][ty][tx] x[n][ci][z+tz-1][h+ty-1][w+tx-1]
+//
+// The input gradient of the same layer is this convolution of dY with the flipped, transposed
+// weights (wt'[ci][co][t] = wt[co][ci][26 - t]), prepared by the caller.
+// Block = (n, z, 6 rows of h, all of w): the input tile x[ci][3 tz][8 rows][W + 2] is staged in LDS
+// once; each thread owns 4 consecutive w outputs of one row for every co (12 accumulators for
+// 3 -> 3), reads 6 inputs per (ci, tz, ty) row and applies 3 tx taps; weights are wave-uniform
+// (scalar loads).
+#include <hip/hip_runtime.h>
+
+#include "texbias.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int ROWS = 6;   // output rows (h) per block
+constexpr int WPT = 4;    // consecutive w outputs per thread
+
+template <int CI, int CO>
+__global__ __launch_bounds__(NT) void k_conv3d_small(const float* __restrict__ x, const float* __restrict__ wt,
+                                                     const float* __restrict__ bias, float* __restrict__ y, int D,
+                                                     int H, int W, int XP, int nhb) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [CI][3][ROWS + 2][XP], col 0 = w = -1
+  const int tid = (int)threadIdx.x;
+  const int hb = (int)blockIdx.x % nhb, z = (int)blockIdx.x / nhb, n = (int)blockIdx.y;
+  const int h0 = hb * ROWS;
+  const int64_t plane = (int64_t)H * W, vol = (int64_t)D * plane;
+  // stage: rows (ci, tz, r) of W floats at column 1; halo columns and out-of-range rows are zero
+  constexpr int NR = CI * 3 * (ROWS + 2);
+  for (int i = tid; i < NR * XP; i += NT) {
+    const int row = i / XP, col = i - row * XP;
+    const int ci = row / (3 * (ROWS + 2)), rem = row - ci * (3 * (ROWS + 2));
+    const int tz = rem / (ROWS + 2), r = rem - tz * (ROWS + 2);
+    const int zi = z + tz - 1, hi = h0 + r - 1, wi = col - 1;
+    float v = 0.f;
+    if (zi >= 0 && zi < D && hi >= 0 && hi < H && wi >= 0 && wi < W)
+      v = x[((int64_t)n * CI + ci) * vol + (int64_t)zi * plane + (int64_t)hi * W + wi];
+    xs[i] = v;
+  }
+  __syncthreads();
+  const int tpr = (W + WPT - 1) / WPT;  // threads per output row
+  const int r = tid / tpr, w0 = (tid - r * tpr) * WPT;
+  if (r >= ROWS || h0 + r >= H) return;
+  float acc[CO][WPT];
+#pragma unroll
+  for (int co = 0; co < CO; ++co) {
+    const float b = bias ? bias[co] : 0.f;
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) acc[co][k] = b;
+  }
+#pragma unroll
+  for (int ci = 0; ci < CI; ++ci) {
+#pragma unroll
+    for (int tz = 0; tz < 3; ++tz) {
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty) {
+        const float* src = xs + ((ci * 3 + tz) * (ROWS + 2) + r + ty) * XP + w0;  // column w0 = w0 - 1 + halo
+        float v[WPT + 2];
+#pragma unroll
+        for (int k = 0; k < WPT + 2; ++k) v[k] = src[k];
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const float wv = wt[(((co * CI + ci) * 3 + tz) * 3 + ty) * 3 + tx];
+#pragma unroll
+            for (int k = 0; k < WPT; ++k) acc[co][k] = fmaf(wv, v[k + tx], acc[co][k]);
+          }
+        }
+      }
+    }
+  }
+  const int h = h0 + r;
+#pragma unroll
+  for (int co = 0; co < CO; ++co) {
+    float* dst = y + ((int64_t)n * CO + co) * vol + (int64_t)z * plane + (int64_t)h * W + w0;
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (w0 + k < W) dst[k] = acc[co][k];
+  }
+}
+
+template <int CI, int CO>
+int launch(const float* x, const float* w, const float* b, float* y, int N, int D, int H, int W, hipStream_t st) {
+  const int XP = W + 2 + WPT;  // halo on both sides, slack for the last thread's 6-wide read
+  const size_t lds = sizeof(float) * (size_t)CI * 3 * (ROWS + 2) * XP;
+  if ((W + WPT - 1) / WPT * ROWS > NT || lds > 65536) return TB_ERR_UNSUPPORTED_SIZE;
+  const int nhb = (H + ROWS - 1) / ROWS;
+  hipLaunchKernelGGL((k_conv3d_small<CI, CO>), dim3((unsigned)(nhb * D), (unsigned)N), dim3(NT), lds, st, x, w, b, y,
+                     D, H, W, XP, nhb);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+}  // namespace
+
+int tb_conv3d_small_f32(const float* x, const float* w, const float* b, float* y, int N, int Cin, int Cout, int D,
+                        int H, int W, void* stream) {
+  if (!x || !w || !y || N < 1 || D < 1 || H < 1 || W < 1 || N > 65535) return TB_ERR_INVALID_ARG;
+  if (Cin < 1 || Cin > 4 || Cout < 1 || Cout > 4) return TB_ERR_UNSUPPORTED_SIZE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define TB_CASE(ci, co) \
+  if (Cin == ci && Cout == co) return launch<ci, co>(x, w, b, y, N, D, H, W, st);
+#define TB_ROW(ci) TB_CASE(ci, 1) TB_CASE(ci, 2) TB_CASE(ci, 3) TB_CASE(ci, 4)
+  TB_ROW(1) TB_ROW(2) TB_ROW(3) TB_ROW(4)
+#undef TB_ROW
+#undef TB_CASE
+  return TB_ERR_UNSUPPORTED_SIZE;
+}

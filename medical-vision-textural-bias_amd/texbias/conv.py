@@ -103,8 +103,55 @@ class _ConvFn(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None, None
 
 
+def small_conv(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+    """Direct 3x3x3, stride 1, padding 1 convolution for <= 4 channels (tb_conv3d_small_f32)."""
+    x = x.contiguous()
+    w = w.contiguous()
+    N, Cin, D, H, W = x.shape
+    Cout = w.shape[0]
+    y = torch.empty((N, Cout, D, H, W), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device):
+        check(lib().tb_conv3d_small_f32(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+                                        y.data_ptr(), N, Cin, Cout, D, H, W, _stream(x)), "tb_conv3d_small_f32")
+    return y
+
+
+def small_conv_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
+    return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and \
+        tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and w.shape[0] <= 4 and w.shape[1] <= 4 and \
+        x.shape[-1] <= 168
+
+
+class _SmallConvFn(torch.autograd.Function):
+    """Few-channel stride-1 3x3x3 Conv3d: forward and input gradient on the direct kernel, weight
+    gradient on the split-K MFMA kernel, bias gradient on the channel-sum kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = small_conv(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+        if ctx.needs_input_grad[1]:
+            gw = wgrad(gy, x, w.shape, 1, 1)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = channel_sum(gy)
+        return gx, gw, gb
+
+
 class Conv3d(nn.Conv3d):
     def forward(self, x):
+        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
+                small_conv_applies(x, self.weight, self.stride, self.padding):
+            return _SmallConvFn.apply(x, self.weight, self.bias)
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
                 custom_backward_applies(x, self.weight):
             k = self.weight.shape[2:]

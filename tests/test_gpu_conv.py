@@ -71,3 +71,23 @@ def test_unet_uses_fast_path_and_trains(conv):
     for _ in range(5):
         l1 = step(x, lab).item()
     assert l1 < l0
+
+
+@pytest.mark.parametrize("cin,cout,shape", [(3, 3, (2, 12, 10, 40)), (4, 2, (1, 7, 9, 160)), (1, 4, (2, 5, 13, 17))])
+def test_small_conv_direct(conv, cin, cout, shape):
+    """Direct few-channel conv (tb_conv3d_small_f32): forward, input, weight and bias gradients vs
+    PyTorch's Conv3d (float32)."""
+    torch.manual_seed(0)
+    ref = nn.Conv3d(cin, cout, 3, padding=1).cuda()
+    ours = conv.Conv3d(cin, cout, 3, padding=1).cuda()
+    ours.load_state_dict(ref.state_dict())
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
+    assert conv.small_conv_applies(x, ours.weight, ours.stride, ours.padding)
+    torch.manual_seed(1)
+    yr, gxr, gwr, gbr = _grads(ref, x)
+    torch.manual_seed(1)
+    yo, gxo, gwo, gbo = _grads(ours, x)
+    torch.testing.assert_close(yo, yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gxo, gxr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gbo, gbr, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gwo, gwr, rtol=1e-4, atol=1e-3 * gwr.abs().max().item())
