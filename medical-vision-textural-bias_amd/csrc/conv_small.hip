@@ -12,8 +12,8 @@
 // weights (wt'[ci][co][t] = wt[co][ci][26 - t]), prepared by the caller.
 // Block = (n, z, 6 rows of h, all of w): the input tile x[ci][3 tz][8 rows][W + 2] is staged in LDS
 // once; each thread owns 4 consecutive w outputs of one row for every co (12 accumulators for
-// 3 -> 3), reads 6 inputs per (ci, tz, ty) row and applies 3 tx taps; weights are wave-uniform
-// (scalar loads).
+// 3 -> 3), reads 6 inputs per (ci, tz, ty) row and applies 3 tx taps; the weights sit in LDS
+// (every lane reads the same address: broadcast).
 #include <hip/hip_runtime.h>
 
 #include "texbias.h"
@@ -23,27 +23,42 @@ namespace {
 constexpr int NT = 256;
 constexpr int ROWS = 6;   // output rows (h) per block
 constexpr int WPT = 4;    // consecutive w outputs per thread
+constexpr int kSeg = 3;   // 64-lane segments per staged row: XP <= 192
 
 template <int CI, int CO>
 __global__ __launch_bounds__(NT) void k_conv3d_small(const float* __restrict__ x, const float* __restrict__ wt,
                                                      const float* __restrict__ bias, float* __restrict__ y, int D,
                                                      int H, int W, int XP, int nhb) {
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [CI][3][ROWS + 2][XP], col 0 = w = -1
+  static_assert(WPT == 4, "the input reads are one float4 + one float2");
+  // weights after the input tile (broadcast LDS reads; 243 of them would spill SGPRs).  No static
+  // LDS in this kernel: the dynamic base stays 16-B aligned for the float4 reads.
+  float* ws = xs + CI * 3 * (ROWS + 2) * XP;
   const int tid = (int)threadIdx.x;
+  for (int i = tid; i < CO * CI * 27; i += NT) ws[i] = wt[i];
   const int hb = (int)blockIdx.x % nhb, z = (int)blockIdx.x / nhb, n = (int)blockIdx.y;
   const int h0 = hb * ROWS;
   const int64_t plane = (int64_t)H * W, vol = (int64_t)D * plane;
-  // stage: rows (ci, tz, r) of W floats at column 1; halo columns and out-of-range rows are zero
+  // stage: rows (ci, tz, r) of W floats at column 1, one wave per row (row bounds are scalar);
+  // halo columns and out-of-range rows are zero
   constexpr int NR = CI * 3 * (ROWS + 2);
-  for (int i = tid; i < NR * XP; i += NT) {
-    const int row = i / XP, col = i - row * XP;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  static_assert(NR % (NT / 64) == 0, "rows deal evenly to the waves");
+#pragma unroll
+  for (int row = wave; row < NR; row += NT / 64) {  // fully unrolled: every row's loads in flight
     const int ci = row / (3 * (ROWS + 2)), rem = row - ci * (3 * (ROWS + 2));
     const int tz = rem / (ROWS + 2), r = rem - tz * (ROWS + 2);
-    const int zi = z + tz - 1, hi = h0 + r - 1, wi = col - 1;
-    float v = 0.f;
-    if (zi >= 0 && zi < D && hi >= 0 && hi < H && wi >= 0 && wi < W)
-      v = x[((int64_t)n * CI + ci) * vol + (int64_t)zi * plane + (int64_t)hi * W + wi];
-    xs[i] = v;
+    const int zi = z + tz - 1, hi = h0 + r - 1;
+    const bool ok = zi >= 0 && zi < D && hi >= 0 && hi < H;
+    const float* src = x + ((int64_t)n * CI + ci) * vol + (ok ? (int64_t)zi * plane + (int64_t)hi * W : 0) - 1;
+    float* dst = xs + row * XP;
+#pragma unroll
+    for (int sg = 0; sg < kSeg; ++sg) {
+      const int col = lane + 64 * sg;
+      const bool in = ok && col >= 1 && col <= W;
+      const float v = src[in ? col : 1];
+      if (col < XP) dst[col] = in ? v : 0.f;
+    }
   }
   __syncthreads();
   const int tpr = (W + WPT - 1) / WPT;  // threads per output row
@@ -56,21 +71,23 @@ __global__ __launch_bounds__(NT) void k_conv3d_small(const float* __restrict__ x
 #pragma unroll
     for (int k = 0; k < WPT; ++k) acc[co][k] = b;
   }
-#pragma unroll
-  for (int ci = 0; ci < CI; ++ci) {
-#pragma unroll
-    for (int tz = 0; tz < 3; ++tz) {
+  // (ci, tz) not unrolled: only that slice's 9 * CO weights and 6 inputs per row are live
+#pragma unroll 1
+  for (int ct = 0; ct < CI * 3; ++ct) {
+    const int ci = ct / 3, tz = ct - 3 * ci;
+    {
 #pragma unroll
       for (int ty = 0; ty < 3; ++ty) {
-        const float* src = xs + ((ci * 3 + tz) * (ROWS + 2) + r + ty) * XP + w0;  // column w0 = w0 - 1 + halo
-        float v[WPT + 2];
-#pragma unroll
-        for (int k = 0; k < WPT + 2; ++k) v[k] = src[k];
+        const float* src = xs + (ct * (ROWS + 2) + r + ty) * XP + w0;  // column w0 = w0 - 1 + halo
+        // 16-B aligned (XP % 4 == 0, w0 % 4 == 0): one ds_read_b128 + one ds_read_b64, no conflicts
+        const float4 v4 = *reinterpret_cast<const float4*>(src);
+        const float2 v2 = *reinterpret_cast<const float2*>(src + 4);
+        const float v[WPT + 2] = {v4.x, v4.y, v4.z, v4.w, v2.x, v2.y};
 #pragma unroll
         for (int co = 0; co < CO; ++co) {
 #pragma unroll
           for (int tx = 0; tx < 3; ++tx) {
-            const float wv = wt[(((co * CI + ci) * 3 + tz) * 3 + ty) * 3 + tx];
+            const float wv = ws[(((co * CI + ci) * 3 + tz) * 3 + ty) * 3 + tx];
 #pragma unroll
             for (int k = 0; k < WPT; ++k) acc[co][k] = fmaf(wv, v[k + tx], acc[co][k]);
           }
@@ -90,9 +107,9 @@ __global__ __launch_bounds__(NT) void k_conv3d_small(const float* __restrict__ x
 
 template <int CI, int CO>
 int launch(const float* x, const float* w, const float* b, float* y, int N, int D, int H, int W, hipStream_t st) {
-  const int XP = W + 2 + WPT;  // halo on both sides, slack for the last thread's 6-wide read
-  const size_t lds = sizeof(float) * (size_t)CI * 3 * (ROWS + 2) * XP;
-  if ((W + WPT - 1) / WPT * ROWS > NT || lds > 65536) return TB_ERR_UNSUPPORTED_SIZE;
+  const int XP = (W + 2 + WPT + 3) / 4 * 4;  // halo, slack for the last thread's 6-wide read, 16-B rows
+  const size_t lds = sizeof(float) * ((size_t)CI * 3 * (ROWS + 2) * XP + CO * CI * 27);
+  if ((W + WPT - 1) / WPT * ROWS > NT || lds > 65536 || XP > 64 * kSeg) return TB_ERR_UNSUPPORTED_SIZE;
   const int nhb = (H + ROWS - 1) / ROWS;
   hipLaunchKernelGGL((k_conv3d_small<CI, CO>), dim3((unsigned)(nhb * D), (unsigned)N), dim3(NT), lds, st, x, w, b, y,
                      D, H, W, XP, nhb);
