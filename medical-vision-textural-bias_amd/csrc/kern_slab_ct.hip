@@ -14,7 +14,7 @@ namespace tb {
 namespace {
 using ct::v2;
 
-template <int W, int D, int NT>
+template <int W, int D, int NT, bool FUSE>
 __global__ __launch_bounds__(NT) void k_slab_fwd_ct(SlabFwdArgs) {
   using P = ct::SlabPlan<W, D>;
   constexpr int SF = ct::Slots<P::N_F0, NT>::value;
@@ -41,9 +41,19 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct(SlabFwdArgs) {
     for (int s = 0; s < SF; ++s)
       if (tid + s * NT < P::N_F0) ct::a_f0<P>(lds, rf[s], tid + s * NT);
     __syncthreads();
-    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::a_d1<P>(lds, it);
-    __syncthreads();
-    {
+    if constexpr (FUSE && P::FUSED_DU) {  // D stage 1 + unpack in one phase (slab_ct.h a_du_*)
+      constexpr int SD = ct::Slots<P::N_DU, NT>::value;
+      v2 rd[SD][2 * P::R1];
+#pragma unroll
+      for (int s = 0; s < SD; ++s)
+        if (tid + s * NT < P::N_DU) ct::a_du_load<P>(lds, rd[s], tid + s * NT);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SD; ++s)
+        if (tid + s * NT < P::N_DU) ct::a_du_compute<P>(lds, rd[s], tid + s * NT);
+    } else {
+      _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::a_d1<P>(lds, it);
+      __syncthreads();
       v2 ru[SU][2];
 #pragma unroll
       for (int s = 0; s < SU; ++s)
@@ -72,7 +82,7 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct(SlabFwdArgs) {
   }
 }
 
-template <int W, int D, int NT>
+template <int W, int D, int NT, bool FUSE>
 __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
   using P = ct::SlabPlan<W, D>;
   constexpr int SG = ct::Slots<P::N_W1, NT>::value;
@@ -103,7 +113,17 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
     __syncthreads();
     _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::c_g1<P>(lds, it);
     __syncthreads();
-    {
+    if constexpr (FUSE && P::FUSED_DU) {  // repack + inverse D stage 1 in one phase (slab_ct.h c_re_*)
+      constexpr int SD = ct::Slots<P::N_DU, NT>::value;
+      v2 rd[SD][2 * P::R1];
+#pragma unroll
+      for (int s = 0; s < SD; ++s)
+        if (tid + s * NT < P::N_DU) ct::c_re_load<P>(lds, rd[s], tid + s * NT);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SD; ++s)
+        if (tid + s * NT < P::N_DU) ct::c_re_compute<P>(lds, rd[s], tid + s * NT);
+    } else {
       v2 ru[SU][2];
 #pragma unroll
       for (int s = 0; s < SU; ++s)
@@ -112,9 +132,9 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
 #pragma unroll
       for (int s = 0; s < SU; ++s)
         if (tid + s * NT < P::N_U) ct::c_r_write<P>(lds, ru[s], tid + s * NT);
+      __syncthreads();
+      _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::c_e1<P>(lds, it);
     }
-    __syncthreads();
-    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::c_e1<P>(lds, it);
     const int un = u + (int)gridDim.x;
     {  // next unit's first-stage inputs, in flight during E0 below (unconditional, as in pass A)
       const v2* Sb = reinterpret_cast<const v2*>(a.S) + ((int64_t)a.bc0 * H + (un < units ? un : u)) * sstride;
@@ -160,13 +180,23 @@ hipError_t launch_ct(K kern, int nt, size_t lds, int units, int ncu, const A& a,
 
 }  // namespace
 
-// threads per workgroup: 768 (3 waves per SIMD) by default; TEXBIAS_CT_NT=512 selects 512 (tuning)
+// threads per workgroup: 768 (3 waves per SIMD) by default; TEXBIAS_CT_NT=512 selects 512 (tuning).
+// TEXBIAS_CT_FUSE (bit 1: forward, bit 2: inverse; default 2) selects the fused DU / RE phase
+// variant (slab_ct.h) at 512 threads for plans with odd R0 and D: it holds two butterflies'
+// inputs across a barrier, which fits the register file only at 2 waves per SIMD.
 static int ct_nt() {
   static const int nt = [] {
     const char* e = std::getenv("TEXBIAS_CT_NT");
     return (e && std::atoi(e) == 512) ? 512 : 768;
   }();
   return nt;
+}
+static int ct_fuse() {
+  static const int f = [] {
+    const char* e = std::getenv("TEXBIAS_CT_FUSE");
+    return e ? std::atoi(e) : 2;
+  }();
+  return f;
 }
 
 bool slab_ct_supported(int W, int D) {
@@ -181,8 +211,10 @@ hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st) {
 #define TB_X(w, d)                                                                                  \
   if (a.pl.W == w && a.pl.D == d) {                                                                 \
     constexpr size_t lds = ct::SlabPlan<w, d>::LDS_BYTES;                                           \
-    if (ct_nt() == 512) return launch_ct(k_slab_fwd_ct<w, d, 512>, 512, lds, units, ncu, a, st);    \
-    return launch_ct(k_slab_fwd_ct<w, d, 768>, 768, lds, units, ncu, a, st);                        \
+    if (ct::SlabPlan<w, d>::FUSED_DU && (ct_fuse() & 1))                                         \
+      return launch_ct(k_slab_fwd_ct<w, d, 512, true>, 512, lds, units, ncu, a, st);                \
+    if (ct_nt() == 512) return launch_ct(k_slab_fwd_ct<w, d, 512, false>, 512, lds, units, ncu, a, st); \
+    return launch_ct(k_slab_fwd_ct<w, d, 768, false>, 768, lds, units, ncu, a, st);                 \
   }
   TB_CT_SLAB_SHAPES(TB_X)
 #undef TB_X
@@ -194,8 +226,10 @@ hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st) {
 #define TB_X(w, d)                                                                                  \
   if (a.pl.W == w && a.pl.D == d) {                                                                 \
     constexpr size_t lds = ct::SlabPlan<w, d>::LDS_BYTES;                                           \
-    if (ct_nt() == 512) return launch_ct(k_slab_inv_ct<w, d, 512>, 512, lds, units, ncu, a, st);    \
-    return launch_ct(k_slab_inv_ct<w, d, 768>, 768, lds, units, ncu, a, st);                        \
+    if (ct::SlabPlan<w, d>::FUSED_DU && (ct_fuse() & 2))                                         \
+      return launch_ct(k_slab_inv_ct<w, d, 512, true>, 512, lds, units, ncu, a, st);                \
+    if (ct_nt() == 512) return launch_ct(k_slab_inv_ct<w, d, 512, false>, 512, lds, units, ncu, a, st); \
+    return launch_ct(k_slab_inv_ct<w, d, 768, false>, 768, lds, units, ncu, a, st);                 \
   }
   TB_CT_SLAB_SHAPES(TB_X)
 #undef TB_X

@@ -220,6 +220,13 @@ template <int W_, int D_> struct SlabPlan {
   static constexpr int N_W0 = Dh * LW;   // (kd, j)   W stage 0  (pass C: G1)
   static constexpr int N_W1 = Dh * Q0;   // (kd, blk) W stage 1  (pass C: G0)
   TB_HD static int rev(int k) { return (k % R0) * L0 + k / R0; }  // D frequency -> DIF slot
+  // Fused D stage 1 + pair (un)pack (odd R0 and D): the stage-1 butterflies blk and R0 - blk hold
+  // mirror frequencies (k = blk + R0 q and D - k = (R0 - blk) + R0 (R1 - 1 - q)), so one work item
+  // per (p, group g) -- g = 0: butterfly 0 alone, g > 0: butterflies g and R0 - g -- owns every
+  // (k, D - k) pair it needs and no unpack phase is required.
+  static constexpr bool FUSED_DU = (R0 % 2 == 1) && (D % 2 == 1);
+  static constexpr int G = R0 / 2 + 1;
+  static constexpr int N_DU = NP * G;    // (g, p)   fused D stage 1 + unpack (pass C: repack + E1)
 };
 
 template <int N, int NT> struct Slots { static constexpr int value = (N + NT - 1) / NT; };
@@ -276,6 +283,49 @@ TB_HD void a_u_write(v2* lds, const v2* r, int it) {
   v2* x = lds + k * P::PX + 2 * p;
   x[0] = r[0];
   x[1] = r[1];
+}
+
+// DU (fused D stage 1 + unpack), item (g, p) with p fastest: load the stage-1 inputs of butterflies
+// g and R0 - g of pair row p into registers (r[0, R1) and r[R1, 2 R1)); after a barrier (X overlaps
+// Z) a_du_compute transforms them and writes the two rows' spectra X[k][2p], X[k][2p + 1], k < Dh.
+template <class P>
+TB_HD void a_du_load(const v2* lds, v2* r, int it) {
+  const int g = it / P::NP, p = it - g * P::NP;
+  const v2* z = lds + p * P::PR;
+  const int b2 = g ? P::R0 - g : 0;
+  TB_UNROLL
+  for (int q = 0; q < P::R1; ++q) r[q] = z[g * P::L0 + q];
+  TB_UNROLL
+  for (int q = 0; q < P::R1; ++q) r[P::R1 + q] = z[b2 * P::L0 + q];
+}
+// X[k][2p], X[k][2p+1] from Z(k) and Z(D - k): (zk + conj zm) / 2, (zk - conj zm) / (2i)
+template <class P>
+TB_HD void a_x_write(v2* lds, int k, int p, v2 zk, v2 zmk) {
+  const v2 zm = conjv(zmk);
+  v2* x = lds + k * P::PX + 2 * p;
+  x[0] = 0.5f * (zk + zm);
+  const v2 dd = 0.5f * (zk - zm);
+  x[1] = V(dd.y, -dd.x);
+}
+template <class P>
+TB_HD void a_du_compute(v2* lds, v2* r, int it) {
+  static_assert(P::FUSED_DU, "fused DU needs odd R0 and D");
+  const int g = it / P::NP, p = it - g * P::NP;
+  v2 o1[P::R1];
+  dft_store<P::R1, true>(r, [&](int q, v2 v) { o1[q] = v; });
+  if (g == 0) {  // k = R0 q, mirror D - k = R0 (R1 - q)
+    TB_UNROLL
+    for (int q = 0; q < P::R1; ++q)
+      if (P::R0 * q < P::Dh) a_x_write<P>(lds, P::R0 * q, p, o1[q], o1[(P::R1 - q) % P::R1]);
+  } else {       // butterfly R0 - g streams its outputs; each pairs with o1[R1 - 1 - q]
+    const int b2 = P::R0 - g;
+    dft_store<P::R1, true>(r + P::R1, [&](int q, v2 v) {
+      const int q1 = P::R1 - 1 - q;
+      const int k2 = b2 + P::R0 * q, k1 = g + P::R0 * q1;  // k1 + k2 = D: exactly one is < Dh
+      if (k2 < P::Dh) a_x_write<P>(lds, k2, p, v, o1[q1]);
+      else a_x_write<P>(lds, k1, p, o1[q1], v);
+    });
+  }
 }
 
 template <class P>
@@ -356,6 +406,54 @@ TB_HD void c_r_write(v2* lds, const v2* r, int it) {
   } else {
     z[P::rev(k)] = V(xa.x - xb.y, xa.y + xb.x);         // xa + i xb
     z[P::rev(P::D - k)] = V(xa.x + xb.y, xb.x - xa.y);  // conj(xa) + i conj(xb)
+  }
+}
+
+// RE (fused repack + inverse D stage 1), item (g, p): gather the (k, D - k) pairs of butterflies
+// g and R0 - g into their stage-1 inputs (registers); after a barrier (Z overlaps X) c_re_compute
+// runs the inverse butterflies in place of pair row p.
+template <class P>
+TB_HD void c_re_load(const v2* lds, v2* r, int it) {
+  const int g = it / P::NP, p = it - g * P::NP;
+  if (g == 0) {
+    TB_UNROLL
+    for (int q = 0; q < P::R1; ++q) {
+      if (P::R0 * q >= P::Dh) continue;
+      const int k = P::R0 * q;
+      const v2* x = lds + k * P::PX + 2 * p;
+      const v2 xa = x[0], xb = x[1];
+      if (k == 0) {
+        r[0] = V(xa.x, xb.x);  // c2r keeps Re of DC
+      } else {
+        r[q] = V(xa.x - xb.y, xa.y + xb.x);                   // Z(k) = xa + i xb
+        r[P::R1 - q] = V(xa.x + xb.y, xb.x - xa.y);           // Z(D - k) = conj(xa) + i conj(xb)
+      }
+    }
+  } else {
+    const int b2 = P::R0 - g;
+    TB_UNROLL
+    for (int q = 0; q < P::R1; ++q) {  // pair (k2 = b2 + R0 q, k1 = g + R0 (R1 - 1 - q))
+      const int q1 = P::R1 - 1 - q;
+      const int k2 = b2 + P::R0 * q, k1 = g + P::R0 * q1;
+      const bool two = k2 < P::Dh;     // the stored (< Dh) member of the pair
+      const v2* x = lds + (two ? k2 : k1) * P::PX + 2 * p;
+      const v2 xa = x[0], xb = x[1];
+      const v2 zs = V(xa.x - xb.y, xa.y + xb.x), zm = V(xa.x + xb.y, xb.x - xa.y);
+      r[P::R1 + q] = two ? zs : zm;    // butterfly b2, output q  = Z(k2)
+      r[q1] = two ? zm : zs;           // butterfly g,  output q1 = Z(k1)
+    }
+  }
+}
+template <class P>
+TB_HD void c_re_compute(v2* lds, v2* r, int it) {
+  static_assert(P::FUSED_DU, "fused RE needs odd R0 and D");
+  const int g = it / P::NP, p = it - g * P::NP;
+  v2* z = lds + p * P::PR;
+  v2* z1 = z + g * P::L0;
+  dft_store<P::R1, false>(r, [&](int q, v2 v) { z1[q] = v; });
+  if (g != 0) {
+    v2* z2 = z + (P::R0 - g) * P::L0;
+    dft_store<P::R1, false>(r + P::R1, [&](int q, v2 v) { z2[q] = v; });
   }
 }
 

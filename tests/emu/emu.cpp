@@ -47,10 +47,16 @@ void ct_slab_fwd(const tb_plan_dev& pl, v2* lds, const float* xb, int64_t sw, v2
   ct::load_tw<P>(ctx, lds, pl);
   v2 r[P::R0];
   for (int it = 0; it < P::N_F0; ++it) { ct::a_load<P>(r, xb, sw, it); ct::a_f0<P>(lds, r, it); }
-  for (int it = 0; it < P::N_D1; ++it) ct::a_d1<P>(lds, it);
-  std::vector<v2> ru(2 * (size_t)P::N_U);
-  for (int it = 0; it < P::N_U; ++it) ct::a_u_read<P>(lds, &ru[2 * it], it);
-  for (int it = 0; it < P::N_U; ++it) ct::a_u_write<P>(lds, &ru[2 * it], it);
+  if constexpr (P::FUSED_DU) {
+    std::vector<v2> rd(2 * (size_t)P::R1 * P::N_DU);
+    for (int it = 0; it < P::N_DU; ++it) ct::a_du_load<P>(lds, &rd[2 * P::R1 * it], it);
+    for (int it = 0; it < P::N_DU; ++it) ct::a_du_compute<P>(lds, &rd[2 * P::R1 * it], it);
+  } else {
+    for (int it = 0; it < P::N_D1; ++it) ct::a_d1<P>(lds, it);
+    std::vector<v2> ru(2 * (size_t)P::N_U);
+    for (int it = 0; it < P::N_U; ++it) ct::a_u_read<P>(lds, &ru[2 * it], it);
+    for (int it = 0; it < P::N_U; ++it) ct::a_u_write<P>(lds, &ru[2 * it], it);
+  }
   for (int it = 0; it < P::N_W0; ++it) ct::a_w0<P>(lds, it);
   for (int it = 0; it < P::N_W1; ++it) ct::a_w1<P>(lds, Sb, it);
 }
@@ -64,10 +70,16 @@ void ct_slab_inv(const tb_plan_dev& pl, v2* lds, const v2* Sb, float* yb, int64_
   v2 r[P::Q1];
   for (int it = 0; it < P::N_W1; ++it) { ct::c_load<P>(r, Sb, it); ct::c_g0<P>(lds, r, it); }
   for (int it = 0; it < P::N_W0; ++it) ct::c_g1<P>(lds, it);
-  std::vector<v2> ru(2 * (size_t)P::N_U);
-  for (int it = 0; it < P::N_U; ++it) ct::c_r_read<P>(lds, &ru[2 * it], it);
-  for (int it = 0; it < P::N_U; ++it) ct::c_r_write<P>(lds, &ru[2 * it], it);
-  for (int it = 0; it < P::N_D1; ++it) ct::c_e1<P>(lds, it);
+  if constexpr (P::FUSED_DU) {
+    std::vector<v2> rd(2 * (size_t)P::R1 * P::N_DU);
+    for (int it = 0; it < P::N_DU; ++it) ct::c_re_load<P>(lds, &rd[2 * P::R1 * it], it);
+    for (int it = 0; it < P::N_DU; ++it) ct::c_re_compute<P>(lds, &rd[2 * P::R1 * it], it);
+  } else {
+    std::vector<v2> ru(2 * (size_t)P::N_U);
+    for (int it = 0; it < P::N_U; ++it) ct::c_r_read<P>(lds, &ru[2 * it], it);
+    for (int it = 0; it < P::N_U; ++it) ct::c_r_write<P>(lds, &ru[2 * it], it);
+    for (int it = 0; it < P::N_D1; ++it) ct::c_e1<P>(lds, it);
+  }
   for (int it = 0; it < P::N_F0; ++it) ct::c_e0<P>(lds, yb, sw, scale, it, lo, hi);
   for (int w = 0; w < W; ++w)
     for (int d = D; d < D + ypad; ++d) yb[w * sw + d] = 0.f;
