@@ -66,13 +66,16 @@ def algorithmic_bytes(bc, H, W, D, pad):
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1b", "traffic.json")
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, launch_bytes: int):
     """HBM bytes per launch of a filter pass from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
-    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), or None when not measured for this build."""
+    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), or None when not measured for launches of
+    this size (the record carries the algorithmic bytes of the launches it measured)."""
     try:
         with open(TRAFFIC_FILE) as f:
             rec = json.load(f)["kernels"].get(kernel)
-        return int(rec["traffic_bytes"]) if rec else None
+        if not rec or int(rec.get("algorithmic_bytes_per_launch", -1)) != int(launch_bytes):
+            return None
+        return int(rec["traffic_bytes"])
     except (OSError, ValueError, KeyError):
         return None
 
@@ -181,10 +184,14 @@ def main():
                 avg = ms[i] / cnt[i]
                 passes[nm] = {"avg_ms": round(avg, 4), "launches": cnt[i]}
                 if nm in nbytes:
-                    passes[nm]["algorithmic_MB"] = round(nbytes[nm] / 1e6, 2)
-                    passes[nm]["GB_s"] = round(nbytes[nm] / (avg * 1e-3) / 1e9, 1)
+                    # the chain may run per chunk of channel-volumes (several launches per step)
+                    per_launch = nbytes[nm] * args.steps / cnt[i]
+                    passes[nm]["algorithmic_bytes"] = int(round(per_launch))
+                    passes[nm]["algorithmic_MB"] = round(per_launch / 1e6, 2)
+                    passes[nm]["GB_s"] = round(per_launch / (avg * 1e-3) / 1e9, 1)
         dom = max((n for n in nbytes if n in passes), key=lambda n: passes[n]["avg_ms"])
         ach = passes[dom]["GB_s"]
+        dom_bytes = passes[dom]["algorithmic_bytes"]
         line = {
             "metric": METRIC,
             "value": round(vols / elapsed, 4),
@@ -211,9 +218,9 @@ def main():
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4),
-                         "traffic": (pmc_traffic(dom) if (H, W, D, B) == (240, 240, 155, 2) else None),
+                         "traffic": pmc_traffic(dom, dom_bytes),
                          "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r1b/traffic.json)",
-                         "algorithmic_bytes_per_launch": nbytes[dom]},
+                         "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),
         }

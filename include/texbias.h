@@ -197,6 +197,15 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
 int tb_set_compiled_plans(int enable);
 
 /*
+ * Channel-volumes per pass A -> B -> C chain inside tb_kspace_filter_f32.  n > 0 runs the three
+ * passes per chunk of n channel-volumes (the chunk's half spectrum is re-read by B and C from the
+ * 256 MiB Infinity Cache rather than HBM), n = 0 runs each pass once over the whole batch group,
+ * n < 0 restores the default (TEXBIAS_CHUNK_BC, else 0; chunking measured slower at C3).  Results
+ * do not depend on n (bit-identical).
+ */
+int tb_set_chain_chunk(int n);
+
+/*
  * Per-pass device timing for measurement: while enabled, every launch function records HIP
  * events around each of its kernels on the caller's stream.  tb_get_pass_times_ms synchronises
  * on them and returns the summed milliseconds per pass -- [0] slab forward (A), [1] k-space

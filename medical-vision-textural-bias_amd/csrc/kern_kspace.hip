@@ -11,7 +11,7 @@ __global__ __launch_bounds__(NT) void k_kspace(KspaceArgs) {
   DevCtx ctx{(int)threadIdx.x, NT};
   const int bcl = (int)blockIdx.y;
   pass_b_body<DevCtx, RS>(ctx, reinterpret_cast<cf*>(smem), a.pl, a.S, a.bc0 + bcl, (int)blockIdx.x, a.T,
-                          a.ops.s[bcl / a.C], bcl % a.C);
+                          a.ops.s[(a.cofs + bcl) / a.C], (a.cofs + bcl) % a.C);
 }
 }  // namespace
 

@@ -33,10 +33,39 @@ __global__ __launch_bounds__(NT) void k_kspace_ct(KspaceArgs) {
   if (tid < P::NM) {
     const int c = tid % T;
     const FreqCol fc = ct::tile_col(a.pl, j0 + (c < nc ? c : 0));
-    ct::b_mid<P>(lds, a.ops.s[bcl / a.C], bcl % a.C, fc, tid);
+    ct::b_mid<P>(lds, a.ops.s[(a.cofs + bcl) / a.C], (a.cofs + bcl) % a.C, fc, tid);
   }
   __syncthreads();
   if (act) ct::b_s1<P>(lds, Sc, ncols, tid);
+}
+
+// Paired variant (ncols even, ncols % T == 0): stage-0 items cover two adjacent columns, so the
+// HBM loads / stores are 16 B per lane; the middle phase runs NM / NT items per thread.
+template <int H, int T, int NT>
+__global__ __launch_bounds__(NT) void k_kspace_ct2(KspaceArgs) {
+  using P = ct::TilePlan<H, T>;
+  static_assert(P::N0 / 2 <= NT && P::NM % NT == 0, "paired items: one per thread per stage-0 phase");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const KspaceArgs& a = kargs<KspaceArgs>();
+  const int tid = (int)threadIdx.x;
+  const int bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int ncols = a.pl.W * (a.pl.D / 2 + 1);
+  const int j0 = (int)blockIdx.x * T;
+  v2* Sc = reinterpret_cast<v2*>(a.S) + (int64_t)bc * H * ncols + j0;
+  for (int i = tid; i < H; i += NT) lds[P::OFF_TW + i] = ct::V(a.pl.tw[0][i].x, a.pl.tw[0][i].y);
+  __syncthreads();
+  if (tid < P::N0 / 2) ct::b_s0_pair<P>(lds, Sc, ncols, tid);
+  __syncthreads();
+  const int sl = a.cofs + bcl;
+#pragma unroll
+  for (int s = 0; s < P::NM / NT; ++s) {
+    const int it = tid + s * NT;
+    const FreqCol fc = ct::tile_col(a.pl, j0 + it % T);
+    ct::b_mid<P>(lds, a.ops.s[sl / a.C], sl % a.C, fc, it);
+  }
+  __syncthreads();
+  if (tid < P::N0 / 2) ct::b_s1_pair<P>(lds, Sc, ncols, tid);
 }
 
 }  // namespace
@@ -48,10 +77,27 @@ bool kspace_ct_supported(int H) {
   return false;
 }
 
-int kspace_ct_tile() { return ct::kCtTileT; }
+// the paired kernel when every tile is full and rows stay 16-B aligned
+static bool use_pair(int ncols) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_KSPACE_PAIR");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && ncols % ct::kCtTileT2 == 0;
+}
+
+int kspace_ct_tile(int ncols) { return use_pair(ncols) ? ct::kCtTileT2 : ct::kCtTileT; }
 
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st) {
+  const bool pair = use_pair(a.pl.W * (a.pl.D / 2 + 1));
 #define TB_X(h)                                                                         \
+  if (a.pl.H == h && pair) {                                                            \
+    constexpr size_t lds = ct::TilePlan<h, ct::kCtTileT2>::LDS_BYTES;                   \
+    hipError_t e = allow_lds(k_kspace_ct2<h, ct::kCtTileT2, NT_TILE>, lds);             \
+    if (e != hipSuccess) return e;                                                      \
+    hipLaunchKernelGGL((k_kspace_ct2<h, ct::kCtTileT2, NT_TILE>), grid, dim3(NT_TILE), lds, st, a); \
+    return hipGetLastError();                                                           \
+  }                                                                                     \
   if (a.pl.H == h) {                                                                    \
     constexpr size_t lds = ct::TilePlan<h, ct::kCtTileT>::LDS_BYTES;                    \
     hipError_t e = allow_lds(k_kspace_ct<h, ct::kCtTileT, NT_TILE>, lds);               \

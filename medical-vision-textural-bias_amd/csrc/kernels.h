@@ -34,7 +34,8 @@ struct SlabFwdArgs {
 struct KspaceArgs {
   tb_plan_dev pl;
   cf* S;
-  int bc0, C, T, pad;
+  int bc0, C, T;
+  int cofs;  // channel-volume index of blockIdx.y = 0 within ops (bc0 - first sample's bc)
   BatchOps ops;
 };
 
@@ -72,7 +73,7 @@ hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st);
 hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st);
 // Compile-time pass-B plans (kspace_ct.h, kern_kspace_ct.hip): tile width kspace_ct_tile() columns.
 bool kspace_ct_supported(int H);
-int kspace_ct_tile();
+int kspace_ct_tile(int ncols);
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st);
 
 #if defined(__HIPCC__)

@@ -151,6 +151,63 @@ TB_HD void b_s1(const v2* lds, v2* __restrict__ Sc, int64_t ncols, int it) {
   for (int q = 0; q < P::Q0; ++q) s[(int64_t)(q * P::L) * ncols] = a[q];
 }
 
+// Paired items (16-B lanes, ncols even): item it covers tile columns c = 2*cp and c+1 of row j,
+// so every HBM access is one f4 (MI355X_MICROARCH.md: 8-B accesses run at 0.54-0.70x the
+// 16-B rate) and a wave covers 64*16/T/8 rows of T*8 contiguous bytes.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <class P>
+TB_HD void b_s0_pair(v2* lds, const v2* __restrict__ Sc, int64_t ncols, int it) {
+  const int j = it / (P::T / 2), c = 2 * (it - j * (P::T / 2));
+  const f4* s = reinterpret_cast<const f4*>(Sc + (int64_t)j * ncols + c);
+  const int64_t st = (int64_t)P::L * (ncols / 2);
+  v2 a[P::Q0], b[P::Q0];
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) {
+    const f4 u = s[q * st];
+    a[q] = V(u.x, u.y);
+    b[q] = V(u.z, u.w);
+  }
+  const v2* tw = lds + P::OFF_TW;
+  Dv<P::Q0, true>::run(a);
+  Dv<P::Q0, true>::run(b);
+  f4* t = reinterpret_cast<f4*>(lds + j * P::T + c);
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) {
+    v2 x = a[q], y = b[q];
+    if (q && j) {
+      const v2 w = tw[j * q];
+      x = cmul(x, w);
+      y = cmul(y, w);
+    }
+    t[q * P::L * P::T / 2] = f4{x.x, x.y, y.x, y.y};
+  }
+}
+template <class P>
+TB_HD void b_s1_pair(const v2* lds, v2* __restrict__ Sc, int64_t ncols, int it) {
+  const int j = it / (P::T / 2), c = 2 * (it - j * (P::T / 2));
+  const v2* tw = lds + P::OFF_TW;
+  const f4* t = reinterpret_cast<const f4*>(lds + j * P::T + c);
+  v2 a[P::Q0], b[P::Q0];
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) {
+    const f4 u = t[q * P::L * P::T / 2];
+    a[q] = V(u.x, u.y);
+    b[q] = V(u.z, u.w);
+    if (q && j) {
+      const v2 w = tw[j * q];
+      a[q] = cmulc(a[q], w);
+      b[q] = cmulc(b[q], w);
+    }
+  }
+  Dv<P::Q0, false>::run(a);
+  Dv<P::Q0, false>::run(b);
+  f4* s = reinterpret_cast<f4*>(Sc + (int64_t)j * ncols + c);
+  const int64_t st = (int64_t)P::L * (ncols / 2);
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) s[q * st] = f4{a[q].x, a[q].y, b[q].x, b[q].y};
+}
+
 // column geometry of tile column c (spectrum column j0 + c = w' * Dh + kd)
 TB_HD FreqCol tile_col(const tb_plan_dev& pl, int col) {
   const int Dh = pl.D / 2 + 1;
@@ -161,6 +218,8 @@ TB_HD FreqCol tile_col(const tb_plan_dev& pl, int col) {
 // H extents with a compile-time pass-B plan in the device library (tile width T = 16 columns)
 #define TB_CT_TILE_H(X) X(240) X(128)
 constexpr int kCtTileT = 16;
+// paired (16-B lane) variant, used when the spectrum row length is even and divisible by it
+constexpr int kCtTileT2 = 32;
 
 }  // namespace ct
 }  // namespace tb

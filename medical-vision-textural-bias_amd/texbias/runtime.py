@@ -310,6 +310,12 @@ def set_compiled_plans(enable: bool) -> None:
     check(lib().tb_set_compiled_plans(1 if enable else 0))
 
 
+def set_chain_chunk(n: int) -> None:
+    """Channel-volumes per pass A -> B -> C chain (tb_set_chain_chunk): n > 0 chunks, 0 = whole
+    batch group per pass, n < 0 = default (Infinity-Cache-sized chunks)."""
+    check(lib().tb_set_chain_chunk(int(n)))
+
+
 def set_pass_timing(enable: bool) -> None:
     check(lib().tb_set_pass_timing(1 if enable else 0))
 

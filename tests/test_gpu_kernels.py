@@ -213,3 +213,29 @@ def test_compiled_slab_plan_matches_generic(rt, shape):
     mmf = rt.keys_to_float(mm_c)
     np.testing.assert_array_equal(mmf[:, 0], yv.min(1).values.cpu().numpy())
     np.testing.assert_array_equal(mmf[:, 1], yv.max(1).values.cpu().numpy())
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 240, 240, 155), (2, 3, 32, 30, 16)])
+def test_chain_chunking_is_bit_identical(rt, shape):
+    """Running passes A -> B -> C per chunk of channel-volumes (Infinity-Cache-sized, chunk edges
+    inside a sample) gives the same bits and the same per-sample min/max as one chain over the
+    batch; the 16-B paired pass-B kernel (full C3 shape) is part of both runs."""
+    torch.manual_seed(11)
+    x = torch.randn(shape, device="cuda")
+    geo = K.geometry(shape[2:])
+    B, C = shape[0], shape[1]
+    progs = [[K.disk_op(12.5, False), K.spike_op((3, 5, 7), geo, 12.0, phase=0.3 + b), K.wrap_op(0.5)]
+             for b in range(B)]
+    outs = []
+    try:
+        for n in (0, 1, 3):
+            rt.set_chain_chunk(n)
+            mm = torch.empty((B, 2), dtype=torch.int32, device="cuda")
+            y = rt.kspace_filter(x, 3, progs, C, pad=5, minmax=mm)
+            outs.append((y, mm))
+    finally:
+        rt.set_chain_chunk(-1)
+    torch.cuda.synchronize()
+    for y, mm in outs[1:]:
+        assert torch.equal(y, outs[0][0])
+        assert torch.equal(mm, outs[0][1])
