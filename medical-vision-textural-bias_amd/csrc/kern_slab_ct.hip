@@ -82,6 +82,87 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct(SlabFwdArgs) {
   }
 }
 
+// Pass A with 16-B loads (contiguous slabs: sw == D, 16-B aligned): the next unit's whole raw
+// slab is prefetched as float4 lanes during W0 / W1 (instead of 4-B lanes in F0 item order, which
+// cost ~110 of the ~280 us per C3 launch), written to LDS at the start of the unit (raw rows 2p,
+// 2p+1 are the bytes of pair row p of Z), then F0 reads its inputs from there.
+template <int W, int D, int NT, bool EARLY>
+__global__ __launch_bounds__(NT) void k_slab_fwd_ct16(SlabFwdArgs) {
+  using P = ct::SlabPlan<W, D>;
+  static_assert((W * D) % 4 == 0, "whole float4 slabs");
+  constexpr int NV = W * D / 4;
+  constexpr int SV = ct::Slots<NV, NT>::value;
+  constexpr int SF = ct::Slots<P::N_F0, NT>::value;
+  constexpr int SU = ct::Slots<P::N_U, NT>::value;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const SlabFwdArgs& a = kargs<SlabFwdArgs>();
+  const int tid = (int)threadIdx.x;
+  const int H = a.pl.H, units = H * a.nbc;
+  DevCtx ctx{tid, NT};
+  ct::load_tw<P>(ctx, lds, a.pl);
+  f4 rv[SV];
+  int u = (int)blockIdx.x;
+  if (u < units) {
+    const int bcl = u / H, h = u - bcl * H;
+    const f4* xb = reinterpret_cast<const f4*>(a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh);
+#pragma unroll
+    for (int s = 0; s < SV; ++s)
+      if (tid + s * NT < NV) rv[s] = xb[tid + s * NT];
+  }
+  for (; u < units; u += (int)gridDim.x) {
+    __syncthreads();  // the previous unit's W1 reads are done (and the twiddles are visible)
+    {
+      f4* raw4 = reinterpret_cast<f4*>(smem);
+#pragma unroll
+      for (int s = 0; s < SV; ++s)
+        if (tid + s * NT < NV) raw4[tid + s * NT] = rv[s];
+    }
+    __syncthreads();
+    v2 rf[SF][P::R0];
+#pragma unroll
+    for (int s = 0; s < SF; ++s)
+      if (tid + s * NT < P::N_F0) ct::a_load_raw<P>(reinterpret_cast<const float*>(smem), rf[s], tid + s * NT);
+    __syncthreads();  // every raw read is done before Z (the same bytes) is written
+#pragma unroll
+    for (int s = 0; s < SF; ++s)
+      if (tid + s * NT < P::N_F0) ct::a_f0<P>(lds, rf[s], tid + s * NT);
+    // next unit's raw slab (clamped on the last pass, as in k_slab_fwd_ct): EARLY issues it here,
+    // in flight during D1 / U / W0 / W1, else after U (in flight during W0 / W1 only)
+    auto prefetch = [&]() {
+      const int un = u + (int)gridDim.x;
+      const int uc = un < units ? un : u;
+      const int bcl = uc / H, h = uc - bcl * H;
+      const f4* xb = reinterpret_cast<const f4*>(a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh);
+#pragma unroll
+      for (int s = 0; s < SV; ++s)
+        if (tid + s * NT < NV) rv[s] = xb[tid + s * NT];
+    };
+    if constexpr (EARLY) prefetch();
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::a_d1<P>(lds, it);
+    __syncthreads();
+    {
+      v2 ru[SU][2];
+#pragma unroll
+      for (int s = 0; s < SU; ++s)
+        if (tid + s * NT < P::N_U) ct::a_u_read<P>(lds, ru[s], tid + s * NT);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < SU; ++s)
+        if (tid + s * NT < P::N_U) ct::a_u_write<P>(lds, ru[s], tid + s * NT);
+    }
+    if constexpr (!EARLY) prefetch();
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::a_w0<P>(lds, it);
+    __syncthreads();
+    const int bcl = u / H, h = u - bcl * H;
+    v2* Sb = reinterpret_cast<v2*>(a.S) + ((int64_t)(a.bc0 + bcl) * H + h) * (int64_t)(W * P::Dh);
+    _Pragma("unroll 1") for (int it = tid; it < P::N_W1; it += NT) ct::a_w1<P>(lds, Sb, it);
+  }
+}
+
 template <int W, int D, int NT, bool FUSE>
 __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
   using P = ct::SlabPlan<W, D>;
@@ -206,11 +287,32 @@ bool slab_ct_supported(int W, int D) {
   return false;
 }
 
+// 16-B staged loads when the slabs are contiguous and 16-B aligned (TEXBIAS_SLAB_RAW16=0: off)
+static bool raw16_ok(const SlabFwdArgs& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_SLAB_RAW16");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on && a.sw == a.pl.D && a.sh % 4 == 0 && a.sbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
+         (a.pl.W * a.pl.D) % 4 == 0;
+}
+
+static bool raw16_early() {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_SLAB_EARLY");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st) {
   const int units = a.pl.H * a.nbc;
+  const bool r16 = raw16_ok(a);
 #define TB_X(w, d)                                                                                  \
   if (a.pl.W == w && a.pl.D == d) {                                                                 \
     constexpr size_t lds = ct::SlabPlan<w, d>::LDS_BYTES;                                           \
+    if (r16 && raw16_early()) return launch_ct(k_slab_fwd_ct16<w, d, 768, true>, 768, lds, units, ncu, a, st); \
+    if (r16) return launch_ct(k_slab_fwd_ct16<w, d, 768, false>, 768, lds, units, ncu, a, st);     \
     if (ct::SlabPlan<w, d>::FUSED_DU && (ct_fuse() & 1))                                         \
       return launch_ct(k_slab_fwd_ct<w, d, 512, true>, 512, lds, units, ncu, a, st);                \
     if (ct_nt() == 512) return launch_ct(k_slab_fwd_ct<w, d, 512, false>, 512, lds, units, ncu, a, st); \

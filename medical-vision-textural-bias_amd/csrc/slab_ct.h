@@ -242,6 +242,16 @@ TB_HD void a_load(v2* r, const float* __restrict__ xb, int64_t sw, int it) {
   for (int q = 0; q < P::R0; ++q) r[q] = V(r0[q * P::L0], r1[q * P::L0]);
 }
 
+// F0 inputs from the raw slab image staged in LDS (floats [w][d], pitch D: the same bytes as Z)
+template <class P>
+TB_HD void a_load_raw(const float* raw, v2* r, int it) {
+  const int p = it / P::L0, j = it - p * P::L0;
+  const float* r0 = raw + (2 * p) * P::D + j;
+  const float* r1 = r0 + P::D;
+  TB_UNROLL
+  for (int q = 0; q < P::R0; ++q) r[q] = V(r0[q * P::L0], r1[q * P::L0]);
+}
+
 template <class P>
 TB_HD void a_f0(v2* lds, const v2* r, int it) {
   const int p = it / P::L0, j = it - p * P::L0;
