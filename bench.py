@@ -63,7 +63,7 @@ def algorithmic_bytes(bc, H, W, D, pad):
     return {"slab_fwd": real + spec, "kspace": 2 * spec, "slab_inv": spec + outp}
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1b", "traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1d", "traffic.json")
 
 
 def pmc_traffic(kernel: str, launch_bytes: int):
@@ -219,7 +219,7 @@ def main():
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(dom, dom_bytes),
-                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r1b/traffic.json)",
+                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r1d/traffic.json)",
                          "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),
