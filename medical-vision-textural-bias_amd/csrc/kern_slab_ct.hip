@@ -163,14 +163,8 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct16(SlabFwdArgs) {
   }
 }
 
-// R16: the slab's half spectrum (contiguous [w'][kd], W * Dh complex) is prefetched as 16-B lanes
-// and staged through LDS at the unit start; G0 reads its inputs from there (as k_slab_fwd_ct16).
-template <int W, int D, int NT, bool FUSE, bool R16 = false>
+template <int W, int D, int NT, bool FUSE>
 __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  static_assert(!R16 || (W * (D / 2 + 1)) % 2 == 0, "whole float4 slabs");
-  constexpr int NV = W * (D / 2 + 1) / 2;
-  constexpr int SV = ct::Slots<NV, NT>::value;
   using P = ct::SlabPlan<W, D>;
   constexpr int SG = ct::Slots<P::N_W1, NT>::value;
   constexpr int SU = ct::Slots<P::N_U, NT>::value;
@@ -183,42 +177,20 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
   const int64_t sstride = (int64_t)W * P::Dh;
   DevCtx ctx{tid, NT};
   ct::load_tw<P>(ctx, lds, a.pl);
-  v2 rg[R16 ? 1 : SG][P::Q1];
-  f4 rv[R16 ? SV : 1];
+  v2 rg[SG][P::Q1];
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
   int u = (int)blockIdx.x;
   if (u < units) {
     const v2* Sb = reinterpret_cast<const v2*>(a.S) + ((int64_t)a.bc0 * H + u) * sstride;
-    if constexpr (R16) {
 #pragma unroll
-      for (int s = 0; s < SV; ++s)
-        if (tid + s * NT < NV) rv[s] = reinterpret_cast<const f4*>(Sb)[tid + s * NT];
-    } else {
-#pragma unroll
-      for (int s = 0; s < SG; ++s)
-        if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
-    }
+    for (int s = 0; s < SG; ++s)
+      if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
   }
   for (; u < units; u += (int)gridDim.x) {
     __syncthreads();  // the previous unit's E0 reads are done
-    if constexpr (R16) {
 #pragma unroll
-      for (int s = 0; s < SV; ++s)
-        if (tid + s * NT < NV) reinterpret_cast<f4*>(smem)[tid + s * NT] = rv[s];
-      __syncthreads();
-      v2 rs[SG][P::Q1];
-#pragma unroll
-      for (int s = 0; s < SG; ++s)
-        if (tid + s * NT < P::N_W1) ct::c_load<P>(rs[s], lds, tid + s * NT);
-      __syncthreads();  // every staged read is done before X (the same bytes) is written
-#pragma unroll
-      for (int s = 0; s < SG; ++s)
-        if (tid + s * NT < P::N_W1) ct::c_g0<P>(lds, rs[s], tid + s * NT);
-    } else {
-#pragma unroll
-      for (int s = 0; s < SG; ++s)
-        if (tid + s * NT < P::N_W1) ct::c_g0<P>(lds, rg[s], tid + s * NT);
-    }
+    for (int s = 0; s < SG; ++s)
+      if (tid + s * NT < P::N_W1) ct::c_g0<P>(lds, rg[s], tid + s * NT);
     __syncthreads();
     _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::c_g1<P>(lds, it);
     __syncthreads();
@@ -247,15 +219,9 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
     const int un = u + (int)gridDim.x;
     {  // next unit's first-stage inputs, in flight during E0 below (unconditional, as in pass A)
       const v2* Sb = reinterpret_cast<const v2*>(a.S) + ((int64_t)a.bc0 * H + (un < units ? un : u)) * sstride;
-      if constexpr (R16) {
 #pragma unroll
-        for (int s = 0; s < SV; ++s)
-          if (tid + s * NT < NV) rv[s] = reinterpret_cast<const f4*>(Sb)[tid + s * NT];
-      } else {
-#pragma unroll
-        for (int s = 0; s < SG; ++s)
-          if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
-      }
+      for (int s = 0; s < SG; ++s)
+        if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
     }
     __syncthreads();
     const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
@@ -357,22 +323,11 @@ hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-// staged 16-B spectrum loads in pass C (TEXBIAS_INV_R16=1 selects them; measured in DESIGN.md)
-static bool inv_r16() {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_INV_R16");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
 hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st) {
   const int units = a.pl.H * a.nbc;
 #define TB_X(w, d)                                                                                  \
   if (a.pl.W == w && a.pl.D == d) {                                                                 \
     constexpr size_t lds = ct::SlabPlan<w, d>::LDS_BYTES;                                           \
-    if (ct::SlabPlan<w, d>::FUSED_DU && (ct_fuse() & 2) && inv_r16())                            \
-      return launch_ct(k_slab_inv_ct<w, d, 512, true, true>, 512, lds, units, ncu, a, st);          \
     if (ct::SlabPlan<w, d>::FUSED_DU && (ct_fuse() & 2))                                         \
       return launch_ct(k_slab_inv_ct<w, d, 512, true>, 512, lds, units, ncu, a, st);                \
     if (ct_nt() == 512) return launch_ct(k_slab_inv_ct<w, d, 512, false>, 512, lds, units, ncu, a, st); \
