@@ -53,17 +53,18 @@ __global__ __launch_bounds__(NT) void k_kspace_ct2(KspaceArgs) {
   const int ncols = a.pl.W * (a.pl.D / 2 + 1);
   const int j0 = (int)blockIdx.x * T;
   v2* Sc = reinterpret_cast<v2*>(a.S) + (int64_t)bc * H * ncols + j0;
+  // the middle phase's column geometry (its w' -> kw table read is a dependent global load):
+  // formed before the stage-0 loads so its latency hides under theirs; NT % T == 0, so every
+  // middle item of this thread has tile column tid % T
+  static_assert(NT % T == 0, "one tile column per thread in the middle phase");
+  const FreqCol fc = ct::tile_col(a.pl, j0 + tid % T);
   for (int i = tid; i < H; i += NT) lds[P::OFF_TW + i] = ct::V(a.pl.tw[0][i].x, a.pl.tw[0][i].y);
   __syncthreads();
   if (tid < P::N0 / 2) ct::b_s0_pair<P>(lds, Sc, ncols, tid);
   __syncthreads();
   const int sl = a.cofs + bcl;
 #pragma unroll
-  for (int s = 0; s < P::NM / NT; ++s) {
-    const int it = tid + s * NT;
-    const FreqCol fc = ct::tile_col(a.pl, j0 + it % T);
-    ct::b_mid<P>(lds, a.ops.s[sl / a.C], sl % a.C, fc, it);
-  }
+  for (int s = 0; s < P::NM / NT; ++s) ct::b_mid<P>(lds, a.ops.s[sl / a.C], sl % a.C, fc, tid + s * NT);
   __syncthreads();
   if (tid < P::N0 / 2) ct::b_s1_pair<P>(lds, Sc, ncols, tid);
 }
@@ -77,7 +78,9 @@ bool kspace_ct_supported(int H) {
   return false;
 }
 
-// the paired kernel when every tile is full and rows stay 16-B aligned
+// the paired kernel when every tile is full and rows stay 16-B aligned.  Tile width (TEXBIAS_KSPACE_T2):
+// 16 columns on 128-thread workgroups by default (4 per CU by LDS: 196 us per C3 launch), 32 on
+// 256 threads (2 per CU: 206 us), or 8 on 64 threads
 static bool use_pair(int ncols) {
   static const bool on = [] {
     const char* e = std::getenv("TEXBIAS_KSPACE_PAIR");
@@ -85,12 +88,34 @@ static bool use_pair(int ncols) {
   }();
   return on && ncols % ct::kCtTileT2 == 0;
 }
+static int pair_tile() {
+  static const int t = [] {
+    const char* e = std::getenv("TEXBIAS_KSPACE_T2");
+    const int v = e ? std::atoi(e) : 16;
+    return (v == 8 || v == 32) ? v : 16;
+  }();
+  return t;
+}
 
-int kspace_ct_tile(int ncols) { return use_pair(ncols) ? ct::kCtTileT2 : ct::kCtTileT; }
+int kspace_ct_tile(int ncols) { return use_pair(ncols) ? pair_tile() : ct::kCtTileT; }
 
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st) {
   const bool pair = use_pair(a.pl.W * (a.pl.D / 2 + 1));
 #define TB_X(h)                                                                         \
+  if (a.pl.H == h && pair && pair_tile() == 8) {                                        \
+    constexpr size_t lds = ct::TilePlan<h, 8>::LDS_BYTES;                               \
+    hipError_t e = allow_lds(k_kspace_ct2<h, 8, 64>, lds);                              \
+    if (e != hipSuccess) return e;                                                      \
+    hipLaunchKernelGGL((k_kspace_ct2<h, 8, 64>), grid, dim3(64), lds, st, a);           \
+    return hipGetLastError();                                                           \
+  }                                                                                     \
+  if (a.pl.H == h && pair && pair_tile() == 16) {                                       \
+    constexpr size_t lds = ct::TilePlan<h, 16>::LDS_BYTES;                              \
+    hipError_t e = allow_lds(k_kspace_ct2<h, 16, 128>, lds);                            \
+    if (e != hipSuccess) return e;                                                      \
+    hipLaunchKernelGGL((k_kspace_ct2<h, 16, 128>), grid, dim3(128), lds, st, a);        \
+    return hipGetLastError();                                                           \
+  }                                                                                     \
   if (a.pl.H == h && pair) {                                                            \
     constexpr size_t lds = ct::TilePlan<h, ct::kCtTileT2>::LDS_BYTES;                   \
     hipError_t e = allow_lds(k_kspace_ct2<h, ct::kCtTileT2, NT_TILE>, lds);             \
