@@ -56,28 +56,38 @@ def parse():
     return ap.parse_args()
 
 
-def algorithmic_bytes(bc, H, W, D, pad):
-    """Per-launch algorithmic bytes of the three k-space passes (DESIGN.md 'Kernels')."""
-    dh = D // 2 + 1
-    real, spec, outp = bc * H * W * D * 4, bc * H * W * dh * 8, bc * H * W * (D + pad) * 4
-    return {"slab_fwd": real + spec, "kspace": 2 * spec, "slab_inv": spec + outp}
-
-
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1d", "traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2", "traffic.json")
 
 
 def pmc_traffic(kernel: str, launch_bytes: int):
-    """HBM bytes per launch of a filter pass from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
+    """HBM bytes per launch of a filter kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
     WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), or None when not measured for launches of
-    this size (the record carries the algorithmic bytes of the launches it measured)."""
+    this size (the record carries the kernel name and the algorithmic bytes of the launches it measured)."""
     try:
         with open(TRAFFIC_FILE) as f:
             rec = json.load(f)["kernels"].get(kernel)
-        if not rec or int(rec.get("algorithmic_bytes_per_launch", -1)) != int(launch_bytes):
+        if not rec or abs(int(rec.get("algorithmic_bytes_per_launch", -1)) - int(launch_bytes)) > 0.001 * launch_bytes:
             return None
         return int(rec["traffic_bytes"])
     except (OSError, ValueError, KeyError):
         return None
+
+
+def maybe_launch_ranks(args) -> None:
+    """``bench.py --gpus N`` without a torchrun environment: start N ranks (one process per GPU)
+    under torch.distributed.run as a CHILD process -- nothing here has touched the GPU -- and exit
+    with its status.  Under torchrun (WORLD_SIZE set) this returns and the rank runs."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    sys.exit(subprocess.call(cmd))
 
 
 def cpu_baseline(x0: np.ndarray, args) -> dict:
@@ -100,6 +110,7 @@ def cpu_baseline(x0: np.ndarray, args) -> dict:
 
 def main():
     args = parse()
+    maybe_launch_ranks(args)
     from texbias import runtime as rt
     from texbias.pipeline import FusedChain
     from texbias.synth import brats_labels, brats_like
@@ -107,6 +118,11 @@ def main():
     import filters_and_operators as F
 
     rank, world, local = init_distributed()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} ranks")
+    if rank == 0:
+        print(f"[bench] world size {world} (backend {dist.get_backend() if world > 1 else 'none'})",
+              file=sys.stderr, flush=True)
     dev = torch.device("cuda", local)
     H, W, D = (int(v) for v in args.shape.split(","))
     B, C = args.batch, 4
@@ -167,7 +183,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ms, cnt = rt.pass_times_ms()
+    ms, cnt, nbytes, kernels = rt.pass_stats()
     rt.set_pass_timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -176,20 +192,19 @@ def main():
 
     if rank == 0:
         vols = B * world * args.steps
-        nbytes = algorithmic_bytes(B * C, H, W, D, pad)
-        names = ["slab_fwd", "kspace", "slab_inv", "salt_pepper"]
+        names = ["forward", "kspace", "inverse", "salt_pepper"]
         passes = {}
         for i, nm in enumerate(names):
             if cnt[i]:
                 avg = ms[i] / cnt[i]
-                passes[nm] = {"avg_ms": round(avg, 4), "launches": cnt[i]}
-                if nm in nbytes:
-                    # the chain may run per chunk of channel-volumes (several launches per step)
-                    per_launch = nbytes[nm] * args.steps / cnt[i]
+                passes[nm] = {"kernel": kernels[i], "avg_ms": round(avg, 4), "launches": cnt[i]}
+                if nbytes[i] > 0:
+                    per_launch = nbytes[i] / cnt[i]
                     passes[nm]["algorithmic_bytes"] = int(round(per_launch))
                     passes[nm]["algorithmic_MB"] = round(per_launch / 1e6, 2)
                     passes[nm]["GB_s"] = round(per_launch / (avg * 1e-3) / 1e9, 1)
-        dom = max((n for n in nbytes if n in passes), key=lambda n: passes[n]["avg_ms"])
+        # the dominant (longest) k-space pass, its bytes and time both measured live on its stream
+        dom = max((n for n in names[:3] if n in passes and "GB_s" in passes[n]), key=lambda n: passes[n]["avg_ms"])
         ach = passes[dom]["GB_s"]
         dom_bytes = passes[dom]["algorithmic_bytes"]
         line = {
@@ -216,10 +231,10 @@ def main():
                 "global_batch": B * world,
                 "parallelism": f"dp{world}",
             },
-            "roofline": {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(dom, dom_bytes),
-                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r1d/traffic.json)",
+            "roofline": {"kernel": passes[dom]["kernel"], "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic(passes[dom]["kernel"], dom_bytes),
+                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r2/traffic.json)",
                          "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),

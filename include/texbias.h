@@ -19,7 +19,7 @@
  *   tb_salt_pepper_f32     SaltAndPepper.salt_and_pepper             filters_and_operators.py:465-482
  *   tb_minmax_f32          the x.max()/2, x.min()/2 of SaltAndPepper                   :476
  *   tb_disk_mask_f32       disk_mask.binary_mask_2d / binary_mask_3d                   :136-197
- *   tb_kspace_logabs_mean_f32  the default spike log-intensity 2.5*mean(log(|k|+1e-10)) :927-933, 1125-1131
+ *   tb_kspace_logabs_sum_f32   the default spike log-intensity 2.5*mean(log(|k|+1e-10)) :927-933, 1125-1131
  */
 #ifndef TEXBIAS_H
 #define TEXBIAS_H
@@ -214,6 +214,21 @@ int tb_set_chain_chunk(int n);
  */
 int tb_set_pass_timing(int enable);
 int tb_get_pass_times_ms(float* ms_sum4, int* count4);
+/* Same record plus the summed ALGORITHMIC bytes per pass (each global input/output element of a
+ * launch counted once; sparse salt-and-pepper counts 0), then clears it.  bytes4 may be NULL. */
+int tb_get_pass_stats(float* ms_sum4, int* count4, double* bytes4);
+/* Name of the kernel last timed in pass slot 0..3 ("" if none). */
+const char* tb_pass_kernel(int slot);
+
+/*
+ * Band-limited plans: a program containing an all-channel low-pass (disk with inside_off = 0,
+ * Gibbs, or a layer mask with host alpha) whose kept box is small runs the pruned passes A'/B'/C'
+ * (one image read, one image write, the box spectrum in between) instead of the full-spectrum
+ * passes; spikes outside the box are synthesised in the same store.  Same results to rounding.
+ * Default on; TEXBIAS_BAND=0 in the environment turns it off.  Samples whose program is empty are
+ * copied through unchanged (bit-identical, as the reference returns them untouched).
+ */
+int tb_set_band_plans(int enable);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,141 @@
+// band.h -- band-limited ("pruned") k-space filter passes.
+//
+// The reference's drivers start their chains with a small low-pass: RandFourierDiskMaskd(r=12.5)
+// keeps 8,217 of the 8.9 M coefficients of a 240x240x155 volume
+// (10_scripts/127_.../..._3modalities.py:171-174, source_code/filters_and_operators.py:236-252).
+// Everything after it in k-space is diagonal (wrap, further masks, filters_and_operators.py:503-515)
+// or a point update (plane-wave / k-space spikes, :383-390, :936-942).  So the whole program's
+// output spectrum lives in a small box around DC plus a handful of spike points, and the full
+// mixed-radix FFT round trip (passes A/B/C, 32 B/voxel of HBM traffic) is replaced by:
+//
+//   A' k_band_fwd   per (bc, h) slab, 64-row chunks staged in LDS: pruned real DFT along D
+//                   (kd in [0, NDk), d-symmetric, twiddles from scalar loads), then pruned DFT
+//                   along W (kw in [-KW, KW]) accumulated in registers over the chunks;
+//                   writes P[bc][h][NW][NDk].  Reads the image once.
+//   B' k_band_mid   per (bc, kh, 64 columns): pruned DFT along H (kh and -kh at once), the
+//                   sample's op program (apply_ops, the same code as pass B) on every box
+//                   coefficient, stored as the kh/-kh sum and difference AB[bc][kh][col]; the
+//                   out-of-box spike points' coefficients = the program applied to 0.
+//   C' k_band_inv   per (bc, h) slab: inverse H and W on the box (VALU), then the C2R along D as
+//                   an f32 MFMA product [rows x 2(NDk+points)] . [2(NDk+points) x D+pad] whose
+//                   second factor is the cos/sin table with zero pad columns -- so the U-Net's
+//                   D-padding comes out of the MFMA as zeros -- stored straight from the
+//                   accumulators; per-sample min/max epilogue.  Writes the image once.
+//
+// Exactness: the box contains every coefficient the low-pass keeps (host-checked with the
+// mask's own arithmetic), a spike outside the box lands on a coefficient that is zero after the
+// low-pass, so its final value is the program applied to 0 (SURVEY G4/G5 and DESIGN.md).
+#pragma once
+
+#include "kernels.h"
+
+namespace tb {
+
+constexpr int BAND_NT = 256;
+constexpr int BAND_MAX_PTS = 8;    // out-of-box half-spectrum spike points per sample
+constexpr int BAND_ROWS_A = 64;    // image rows per pass-A' chunk (one per lane)
+constexpr int BAND_ROWS_C = 128;   // image rows per pass-C' chunk (4 waves x one 32-row MFMA tile)
+constexpr int BAND_MAX_NDK = 32;
+
+struct BandPt {
+  int16_t kh, kw, kd, pad;  // unsigned frequency of the stored (kd <= D/2) coefficient
+};
+struct BandSamplePts {
+  int n;
+  BandPt p[BAND_MAX_PTS];
+};
+
+struct BandGeo {
+  int KH, KW, NDk;  // box: signed kh in [-KH, KH], signed kw in [-KW, KW], kd in [0, NDk)
+  int NW, ncol;     // 2 KW + 1, NW * NDk  (a "column" = one (kw, kd) pair of the box)
+  int KS;           // k-steps of the inverse D MFMA: NDk band columns + the launch's max points
+  int NCOL;         // output columns of the MFMA n-tiles: 32 * ceil((D + pad) / 32)
+};
+
+struct BandFwdArgs {
+  tb_plan_dev pl;
+  const float* x;
+  int64_t sbc, sh, sw;
+  cf* P;            // [bc][H][ncol]  (bc absolute)
+  const float2* tdf;  // [d][NKP] = (cos, sin)(2 pi kd d / D), d in [0, D/2]
+  int NKP;
+  int bc0, nbc;
+  BandGeo g;
+};
+
+struct BandMidArgs {
+  tb_plan_dev pl;
+  const cf* P;
+  float4* AB;       // [bc][KH + 1][ncol]: (Q'(kh) + Q'(-kh), Q'(kh) - Q'(-kh))
+  cf* pts;          // [bc][BAND_MAX_PTS]
+  int bc0, C, cofs, nbc;
+  BandGeo g;
+  BandSamplePts sp[TB_MAX_BATCH];
+  BatchOps ops;
+};
+
+struct BandInvArgs {
+  tb_plan_dev pl;
+  const float4* AB;
+  const cf* pts;
+  float* y;
+  int64_t sbc, sh, sw;
+  int ypad, bc0, C, cofs, nbc;
+  float scale;      // 1 / (H W D)
+  uint32_t* mm;
+  BandGeo g;
+  BandSamplePts sp[TB_MAX_BATCH];
+};
+
+// workspace carve (bytes from the workspace base) for `bcn` volume-channels
+struct BandWs {
+  size_t off_P, off_AB, off_pts, total;
+};
+TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
+  BandWs w;
+  w.off_P = 0;
+  w.off_AB = (size_t)bcn * H * g.ncol * 8;
+  w.off_AB = (w.off_AB + 255) & ~(size_t)255;
+  w.off_pts = w.off_AB + (size_t)bcn * (g.KH + 1) * g.ncol * 16;
+  w.total = w.off_pts + (size_t)bcn * BAND_MAX_PTS * 8;
+  return w;
+}
+
+// LDS bytes of the two slab kernels
+TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
+  const int P = (D & 1) ? D : D + 1;
+  return (size_t)BAND_ROWS_A * P * 4 + (size_t)g.NDk * (BAND_ROWS_A + 1) * 8 + (size_t)W * 8;
+}
+struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
+  int bimg, va, zb, awbw, tww, total;
+};
+TB_HD int band_al16(int b) { return (b + 15) & ~15; }
+TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W) {
+  const int KC2 = 2 * g.KS;
+  BandInvCarve c;
+  c.bimg = 0;
+  c.va = band_al16(c.bimg + KC2 * g.NCOL * 4);
+  c.zb = band_al16(c.va + BAND_ROWS_C * (KC2 + 1) * 4);
+  c.awbw = band_al16(c.zb + g.ncol * 8);
+  c.tww = band_al16(c.awbw + (g.KW + 1) * g.NDk * 16);
+  c.total = band_al16(c.tww + W * 8);
+  return c;
+}
+
+// Launchers (kern_band.hip).  ncu = compute units (persistent slab grids).
+hipError_t launch_band_fwd(const BandFwdArgs& a, int ncu, hipStream_t st);
+hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st);
+hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);
+
+// identity samples (empty program): strided copy + zero D-padding + min/max
+struct CopyArgs {
+  const float* x;
+  int64_t xsbc, xsh, xsw;
+  float* y;
+  int64_t ysbc, ysh, ysw;
+  int H, W, D, ypad, bc0, C, nbc;
+  uint32_t* mm;
+};
+hipError_t launch_copy_pad(const CopyArgs& a, hipStream_t st);
+
+}  // namespace tb

@@ -12,11 +12,13 @@
 //   D  k_salt_pepper  Philox u, class, sparse in-place MIN/MAX scatter.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
 
+#include "band.h"
 #include "fft_core.h"
 #include "kernels.h"
 #include "plan_host.h"
@@ -48,11 +50,13 @@ inline int hip_fail(hipError_t e) {
 struct TimingRec {
   hipEvent_t a, b;
   int slot;
+  double bytes;
 };
 std::mutex g_tmu;
 bool g_timing = false;
 std::vector<TimingRec> g_recs;
 std::vector<hipEvent_t> g_pool;
+const char* g_slot_kernel[4] = {"", "", "", ""};
 
 hipEvent_t ev_get() {
   if (!g_pool.empty()) {
@@ -67,10 +71,14 @@ hipEvent_t ev_get() {
 struct Timer {  // records [begin, end) of one pass when timing is enabled
   hipEvent_t a = nullptr, b = nullptr;
   int slot;
+  double bytes;
   hipStream_t st;
-  Timer(int s, hipStream_t stream) : slot(s), st(stream) {
+  // bytes: the launch's algorithmic HBM bytes (each global input/output element counted once)
+  Timer(int s, hipStream_t stream, double nbytes = 0.0, const char* kernel = nullptr)
+      : slot(s), bytes(nbytes), st(stream) {
     if (!g_timing) return;
     std::lock_guard<std::mutex> lk(g_tmu);
+    if (kernel) g_slot_kernel[s] = kernel;
     a = ev_get();
     b = ev_get();
     if (a) (void)hipEventRecord(a, st);
@@ -79,7 +87,7 @@ struct Timer {  // records [begin, end) of one pass when timing is enabled
     if (!a || !b) return;
     (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> lk(g_tmu);
-    g_recs.push_back({a, b, slot});
+    g_recs.push_back({a, b, slot, bytes});
   }
 };
 
@@ -199,6 +207,8 @@ struct tb_plan {
   int ncu = 256;         // compute units (grid of the persistent compiled-plan slab kernels)
   bool ct_slab = false;  // (W, D) has a compile-time slab plan (slab_ct.h)
   bool ct_tile = false;  // H has a compile-time pass-B plan (kspace_ct.h)
+  float2* tdf = nullptr; // band pass A': [D/2 + 1][NKP] (cos, sin)(2 pi kd d / D)
+  int NKP = 0;
 };
 
 namespace {
@@ -299,6 +309,25 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   p->dev.rev_d = reinterpret_cast<const int*>(d + off_i[0]);
   p->dev.irev_h = reinterpret_cast<const int*>(d + off_i[1]);
   p->dev.irev_w = reinterpret_cast<const int*>(d + off_i[2]);
+  {  // pruned-DFT twiddles of the band-limited pass A' (kd padded past any wave's kd group)
+    const int Ld = D / 2 + 1;
+    int nkp = Ld > 32 ? Ld : 32;
+    nkp = (nkp + 7) & ~7;
+    std::vector<float2> t((size_t)Ld * nkp);
+    for (int d = 0; d < Ld; ++d)
+      for (int k = 0; k < nkp; ++k) {
+        const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)k * d) % D) / (double)D;
+        t[(size_t)d * nkp + k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
+      }
+    if (hipMalloc(reinterpret_cast<void**>(&p->tdf), t.size() * sizeof(float2)) != hipSuccess ||
+        hipMemcpy(p->tdf, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+      if (p->tdf) (void)hipFree(p->tdf);
+      (void)hipFree(p->dmem);
+      delete p;
+      return hip_fail(hipGetLastError());
+    }
+    p->NKP = nkp;
+  }
   p->rset_h = needs_all(p->host.ax[0]) ? RS_ALL : RS_SMALL;
   p->rset_wd = (needs_all(p->host.ax[1]) || needs_all(p->host.ax[2])) ? RS_ALL : RS_SMALL;
   *out = p;
@@ -308,6 +337,7 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
 int tb_plan_destroy(tb_plan* plan) {
   if (!plan) return TB_OK;
   if (plan->dmem) (void)hipFree(plan->dmem);
+  if (plan->tdf) (void)hipFree(plan->tdf);
   delete plan;
   return TB_OK;
 }
@@ -353,6 +383,236 @@ static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, 
   return TB_OK;
 }
 
+// ------------------------------------------------------------ band-limited plans (band.h)
+// TEXBIAS_BAND=0 or tb_set_band_plans(0) forces the full-spectrum passes for every program.
+static bool g_band = [] {
+  const char* e = std::getenv("TEXBIAS_BAND");
+  return !(e && e[0] == '0');
+}();
+
+// A low-pass op that zeroes every coefficient outside a box around DC (all channels).
+static bool band_is_lowpass(const tb_op& op) {
+  if (op.chan != -1) return false;
+  if (op.kind == TB_OP_DISK) return op.i[1] == 0;       // inside_off = False: keeps the disk
+  if (op.kind == TB_OP_GIBBS) return true;
+  if (op.kind == TB_OP_LAYER) return op.l == 0;          // alpha known on the host
+  return false;
+}
+// The op's own keep-test on a total squared distance (apply_ops' arithmetic, fft_core.h).
+static bool band_keeps(const tb_op& op, int64_t sq) {
+  if (op.kind == TB_OP_DISK) return op.i[0] ? (sq < op.l) : ((float)sq < op.f[0]);
+  if (op.kind == TB_OP_GIBBS) return sq <= op.l;
+  return layer_in(op, (int)sq);
+}
+// Largest |signed frequency| on an axis of length n that the op can keep, the other axes at their
+// smallest term `rest` (disk: 0; Gibbs / layer: 0 for odd n, 1 for even n -- the (n-1)/2 centre);
+// `half`: the D axis, stored kd in [0, n/2] only.  -1 when no coefficient survives.
+static int band_extent(const tb_op& op, int n, int64_t rest, bool half) {
+  int K = -1;
+  const int kmax = half ? n / 2 : n - 1;
+  for (int k = 0; k <= kmax; ++k) {
+    const AxisGeo g = axis_geo(k, n);
+    const int64_t term = op.kind == TB_OP_DISK ? g.dsq : (g.ef < g.en ? g.ef : g.en);
+    if (!band_keeps(op, term + rest)) continue;
+    const int m = (half || k <= (n - 1) / 2) ? k : n - k;
+    K = m > K ? m : K;
+  }
+  return K;
+}
+static int band_minterm(const tb_op& op, int n) { return (op.kind == TB_OP_DISK || (n & 1)) ? 0 : 1; }
+
+// Box of one sample's program (false: no low-pass, the full passes run).
+static bool band_box(const tb_sample_ops& so, int H, int W, int D, int& KH, int& KW, int& KD) {
+  for (int o = 0; o < so.n; ++o) {
+    const tb_op& op = so.op[o];
+    if (!band_is_lowpass(op)) continue;
+    const int mh = band_minterm(op, H), mw = band_minterm(op, W), md = band_minterm(op, D);
+    KH = band_extent(op, H, mw + md, false);
+    KW = band_extent(op, W, mh + md, false);
+    KD = band_extent(op, D, mh + mw, true);
+    if (KH < 0 || KW < 0 || KD < 0) KH = KW = KD = 0;  // nothing kept: the box degenerates to DC
+    return true;
+  }
+  return false;
+}
+// Stored (kd <= D/2) coefficients of the program's spikes that fall outside the box.
+static bool band_points(const tb_sample_ops& so, int H, int W, int D, int KH, int KW, int KD, BandSamplePts& sp) {
+  sp.n = 0;
+  for (int o = 0; o < so.n; ++o) {
+    const tb_op& op = so.op[o];
+    if (op.kind != TB_OP_SPIKE) continue;
+    const int f[2][3] = {{op.i[0], op.i[1], op.i[2]},
+                         {(H - op.i[0]) % H, (W - op.i[1]) % W, (D - op.i[2]) % D}};
+    for (int q = 0; q < 2; ++q) {
+      const int kh = f[q][0], kw = f[q][1], kd = f[q][2];
+      if (kd > D / 2) continue;
+      const int mh = kh <= (H - 1) / 2 ? kh : H - kh, mw = kw <= (W - 1) / 2 ? kw : W - kw;
+      if (mh <= KH && mw <= KW && kd <= KD) continue;  // inside the box: handled by pass B'
+      bool dup = false;
+      for (int j = 0; j < sp.n; ++j) dup |= sp.p[j].kh == kh && sp.p[j].kw == kw && sp.p[j].kd == kd;
+      if (dup) continue;
+      if (sp.n == BAND_MAX_PTS) return false;
+      sp.p[sp.n].kh = (int16_t)kh;
+      sp.p[sp.n].kw = (int16_t)kw;
+      sp.p[sp.n].kd = (int16_t)kd;
+      sp.p[sp.n].pad = 0;
+      ++sp.n;
+    }
+  }
+  return true;
+}
+
+// Band geometry shared by samples [s0, s1) of `ops`, or false when the run must use the full passes.
+static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1, int y_pad, size_t ws_bytes, int bcn,
+                      BandGeo& g, BandSamplePts* sp) {
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  int KH = 0, KW = 0, KD = 0, npt = 0;
+  for (int s = s0; s < s1; ++s) {
+    int kh, kw, kd;
+    if (!band_box(ops[s], H, W, D, kh, kw, kd)) return false;
+    KH = kh > KH ? kh : KH;
+    KW = kw > KW ? kw : KW;
+    KD = kd > KD ? kd : KD;
+  }
+  for (int s = s0; s < s1; ++s) {
+    if (!band_points(ops[s], H, W, D, KH, KW, KD, sp[s - s0])) return false;
+    npt = sp[s - s0].n > npt ? sp[s - s0].n : npt;
+  }
+  g.KH = KH;
+  g.KW = KW;
+  g.NDk = KD + 1;
+  g.NW = 2 * KW + 1;
+  g.ncol = g.NW * g.NDk;
+  g.KS = g.NDk + npt;
+  g.NCOL = 32 * ((D + y_pad + 31) / 32);
+  if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || (KW + 1) * g.NDk > 4 * BAND_NT) return false;
+  // worth it only when the box is a small part of the half spectrum
+  if ((double)(2 * KH + 1) * g.ncol * 4.0 > (double)H * W * (D / 2 + 1)) return false;
+  if (band_lds_fwd(g, W, D) > 160000 || band_inv_carve(g, W).total > 160000) return false;
+  if (band_ws(g, H, bcn).total > ws_bytes) return false;
+  return true;
+}
+
+enum { RUN_COPY = 0, RUN_FULL = 1, RUN_BAND = 2 };
+
+template <int RA, int RB>
+static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad, cf* S,
+                    int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax, hipStream_t st) {
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  const int Dh = D / 2 + 1;
+  const float scale = (float)(1.0 / ((double)H * (double)W * (double)D));
+  const int T = pick_tile(H, p->lds_max);
+  const int ntiles = (W * Dh + T - 1) / T;
+  const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
+  const size_t lds_s = (size_t)slab_geo(W, D).total_cf * sizeof(cf);
+  BatchOps bo;
+  std::memset(&bo, 0, sizeof(bo));
+  for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
+  // A -> B -> C per chunk of channel-volumes: a chunk's half spectrum is re-read by B and C while
+  // it is still in the 256 MiB Infinity Cache (chunk_bc(); 0 = the whole group in one chain)
+  const int nbc = nb * C;
+  const int g = chunk_bc(p) > 0 ? chunk_bc(p) : nbc;
+  for (int c0 = 0; c0 < nbc; c0 += g) {
+    const int ng = (nbc - c0) < g ? (nbc - c0) : g;
+    const int bc0 = b0 * C + c0;
+    const double vox = (double)ng * H * W * D, spec = (double)ng * H * W * Dh * 8.0;
+    {
+      Timer t(0, st, vox * 4.0 + spec, use_ct_slab(p) ? "k_slab_fwd_ct16" : "k_slab_fwd");
+      const int rc = launch_slab_fwd<RA>(p, x, xs, S, bc0, ng, st);
+      if (rc) return rc;
+    }
+    {
+      Timer t(1, st, 2.0 * spec, (g_compiled_plans && p->ct_tile) ? "k_kspace_ct2" : "k_kspace");
+      if (g_compiled_plans && p->ct_tile) {
+        const int Tc = tb::kspace_ct_tile(W * Dh);
+        KspaceArgs ka{p->dev, S, bc0, C, Tc, c0, bo};
+        TB_HIP(tb::launch_kspace_ct(ka, dim3((W * Dh + Tc - 1) / Tc, ng), st));
+      } else {
+        KspaceArgs ka{p->dev, S, bc0, C, T, c0, bo};
+        TB_HIP(launch_kspace<RB>(ka, dim3(ntiles, ng), lds_b, st));
+      }
+    }
+    {
+      Timer t(2, st, spec + (double)ng * H * W * (D + y_pad) * 4.0, use_ct_slab(p) ? "k_slab_inv_ct" : "k_slab_inv");
+      SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, bc0, C, scale, minmax, ng};
+      if (use_ct_slab(p))
+        TB_HIP(tb::launch_slab_inv_ct(ia, p->ncu, st));
+      else
+        TB_HIP(launch_slab_inv<RA>(ia, dim3(H, ng), lds_s, st));
+    }
+  }
+  return TB_OK;
+}
+
+static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
+                    char* ws, int bcn_total, int b0, int nb, int C, const tb_sample_ops* ops, const BandGeo& g,
+                    const BandSamplePts* sp, uint32_t* minmax, hipStream_t st) {
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  const BandWs wl = band_ws(g, H, bcn_total);
+  cf* P = reinterpret_cast<cf*>(ws + wl.off_P);
+  float4* AB = reinterpret_cast<float4*>(ws + wl.off_AB);
+  cf* pts = reinterpret_cast<cf*>(ws + wl.off_pts);
+  const int nbc = nb * C, bc0 = b0 * C;
+  const double pbytes = (double)nbc * H * g.ncol * 8.0, abytes = (double)nbc * (g.KH + 1) * g.ncol * 16.0;
+  {
+    Timer t(0, st, (double)nbc * H * W * D * 4.0 + pbytes, "k_band_fwd");
+    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g};
+    TB_HIP(tb::launch_band_fwd(fa, p->ncu, st));
+  }
+  {
+    Timer t(1, st, pbytes + abytes, "k_band_mid");
+    BandMidArgs ma;
+    std::memset(&ma, 0, sizeof(ma));
+    ma.pl = p->dev;
+    ma.P = P;
+    ma.AB = AB;
+    ma.pts = pts;
+    ma.bc0 = bc0;
+    ma.C = C;
+    ma.cofs = 0;
+    ma.nbc = nbc;
+    ma.g = g;
+    for (int i = 0; i < nb; ++i) {
+      ma.sp[i] = sp[i];
+      ma.ops.s[i] = ops[b0 + i];
+    }
+    TB_HIP(tb::launch_band_mid(ma, st));
+  }
+  {
+    Timer t(2, st, abytes + (double)nbc * H * W * (D + y_pad) * 4.0, "k_band_inv");
+    BandInvArgs ia;
+    std::memset(&ia, 0, sizeof(ia));
+    ia.pl = p->dev;
+    ia.AB = AB;
+    ia.pts = pts;
+    ia.y = y;
+    ia.sbc = ys[0];
+    ia.sh = ys[1];
+    ia.sw = ys[2];
+    ia.ypad = y_pad;
+    ia.bc0 = bc0;
+    ia.C = C;
+    ia.cofs = 0;
+    ia.nbc = nbc;
+    ia.scale = (float)(1.0 / ((double)H * (double)W * (double)D));
+    ia.mm = minmax;
+    ia.g = g;
+    for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
+    TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
+  }
+  return TB_OK;
+}
+
+static int run_copy(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad, int b0,
+                    int nb, int C, uint32_t* minmax, hipStream_t st) {
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  const int nbc = nb * C;
+  Timer t(2, st, (double)nbc * H * W * (2.0 * D + y_pad) * 4.0, "k_copy_pad");
+  CopyArgs ca{x, xs[0], xs[1], xs[2], y, ys[0], ys[1], ys[2], H, W, D, y_pad, b0 * C, C, nbc, minmax};
+  TB_HIP(tb::launch_copy_pad(ca, st));
+  return TB_OK;
+}
+
 template <int RA, int RB>
 static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
                          void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops, uint32_t* minmax,
@@ -362,55 +622,35 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
   for (int b = 0; b < B; ++b)
     if (ops[b].n < 0 || ops[b].n > TB_MAX_OPS) return TB_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  cf* S = static_cast<cf*>(ws);
-  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
-  const float scale = (float)(1.0 / ((double)H * (double)W * (double)D));
   if (minmax) {
     hipLaunchKernelGGL(k_minmax_init, dim3((B + 255) / 256), dim3(256), 0, st, minmax, B);
     TB_HIP(hipGetLastError());
   }
-  const int T = pick_tile(H, p->lds_max);
-  const int ntiles = (W * (D / 2 + 1) + T - 1) / T;
-  const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
-  const size_t lds_s = (size_t)slab_geo(W, D).total_cf * sizeof(cf);
-  int rc = TB_OK;
-  // launch groups of <= TB_MAX_BATCH samples (the op programs travel in the kernel arguments)
+  // Runs of consecutive samples with the same route, in launch groups of <= TB_MAX_BATCH samples
+  // (the op programs travel in the kernel arguments): empty programs are copied through (the
+  // reference returns the input untouched), low-pass programs take the band passes A'/B'/C',
+  // the rest the full-spectrum passes A/B/C.
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
-    BatchOps bo;
-    std::memset(&bo, 0, sizeof(bo));
-    for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
-    // A -> B -> C per chunk of channel-volumes: a chunk's half spectrum is re-read by B and C while
-    // it is still in the 256 MiB Infinity Cache (chunk_bc(); 0 = the whole group in one chain)
-    const int nbc = nb * C;
-    const int g = chunk_bc(p) > 0 ? chunk_bc(p) : nbc;
-    for (int c0 = 0; c0 < nbc; c0 += g) {
-      const int ng = (nbc - c0) < g ? (nbc - c0) : g;
-      const int bc0 = b0 * C + c0;
-      {
-        Timer t(0, st);
-        rc = launch_slab_fwd<RA>(p, x, xs, S, bc0, ng, st);
-        if (rc) return rc;
-      }
-      {
-        Timer t(1, st);
-        if (g_compiled_plans && p->ct_tile) {
-          const int Tc = tb::kspace_ct_tile(W * (D / 2 + 1));
-          KspaceArgs ka{p->dev, S, bc0, C, Tc, c0, bo};
-          TB_HIP(tb::launch_kspace_ct(ka, dim3((W * (D / 2 + 1) + Tc - 1) / Tc, ng), st));
-        } else {
-          KspaceArgs ka{p->dev, S, bc0, C, T, c0, bo};
-          TB_HIP(launch_kspace<RB>(ka, dim3(ntiles, ng), lds_b, st));
-        }
-      }
-      {
-        Timer t(2, st);
-        SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, bc0, C, scale, minmax, ng};
-        if (use_ct_slab(p))
-          TB_HIP(tb::launch_slab_inv_ct(ia, p->ncu, st));
+    int i = 0;
+    while (i < nb) {
+      auto route = [&](int s) { return ops[s].n == 0 ? RUN_COPY : RUN_FULL; };
+      const int r = route(b0 + i);
+      int j = i + 1;
+      while (j < nb && route(b0 + j) == r) ++j;
+      int rc = TB_OK;
+      if (r == RUN_COPY) {
+        rc = run_copy(p, x, xs, y, ys, y_pad, b0 + i, j - i, C, minmax, st);
+      } else {
+        BandGeo g;
+        BandSamplePts sp[TB_MAX_BATCH];
+        if (g_band && band_plan(p, ops, b0 + i, b0 + j, y_pad, ws_bytes, B * C, g, sp))
+          rc = run_band(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, b0 + i, j - i, C, ops, g, sp, minmax, st);
         else
-          TB_HIP(launch_slab_inv<RA>(ia, dim3(H, ng), lds_s, st));
+          rc = run_full<RA, RB>(p, x, xs, y, ys, y_pad, static_cast<cf*>(ws), b0 + i, j - i, C, ops, minmax, st);
       }
+      if (rc) return rc;
+      i = j;
     }
   }
   return TB_OK;
@@ -466,7 +706,7 @@ int tb_kspace_logabs_sum_f32(const tb_plan* p, const float* x, const int64_t* xs
 int tb_minmax_f32(const float* x, uint32_t* mm, int B, int64_t rows, int len, int64_t ld, int64_t sb, void* stream) {
   if (!x || !mm || B < 1 || rows < 1 || len < 1 || ld < len) return TB_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  Timer t(3, st);
+  Timer t(3, st, (double)B * rows * len * 4.0, "k_minmax");
   hipLaunchKernelGGL(k_minmax_init, dim3((B + 255) / 256), dim3(256), 0, st, mm, B);
   const int64_t n = rows * len;
   int64_t blocks = (n + 256 * 8 - 1) / (256 * 8);
@@ -485,7 +725,8 @@ int tb_salt_pepper_f32(const float* x, float* y, int8_t* cls, const float* u_in,
   const int64_t n = rows * len;
   int64_t blocks = ((n + 3) / 4 + NT_SAP - 1) / NT_SAP;
   if (blocks > 2048) blocks = 2048;
-  Timer t(3, st);
+  // sparse in-place: only ~p of the voxels are stored (no algorithmic byte count is claimed)
+  Timer t(3, st, sparse ? 0.0 : (double)B * n * (8.0 + (u_in ? 4.0 : 0.0) + (cls ? 1.0 : 0.0)), "k_salt_pepper");
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
     SapThr th;
@@ -525,6 +766,11 @@ int tb_set_compiled_plans(int enable) {
   return TB_OK;
 }
 
+int tb_set_band_plans(int enable) {
+  g_band = enable != 0;
+  return TB_OK;
+}
+
 int tb_set_pass_timing(int enable) {
   std::lock_guard<std::mutex> lk(g_tmu);
   g_timing = enable != 0;
@@ -533,19 +779,32 @@ int tb_set_pass_timing(int enable) {
   return TB_OK;
 }
 
-int tb_get_pass_times_ms(float* ms, int* cnt) {
+int tb_get_pass_stats(float* ms, int* cnt, double* bytes) {
   if (!ms || !cnt) return TB_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(g_tmu);
-  for (int i = 0; i < 4; ++i) { ms[i] = 0.f; cnt[i] = 0; }
+  for (int i = 0; i < 4; ++i) {
+    ms[i] = 0.f;
+    cnt[i] = 0;
+    if (bytes) bytes[i] = 0.0;
+  }
   for (auto& r : g_recs) {
     TB_HIP(hipEventSynchronize(r.b));
     float t = 0.f;
     TB_HIP(hipEventElapsedTime(&t, r.a, r.b));
     ms[r.slot] += t;
     cnt[r.slot] += 1;
+    if (bytes) bytes[r.slot] += r.bytes;
     g_pool.push_back(r.a);
     g_pool.push_back(r.b);
   }
   g_recs.clear();
   return TB_OK;
+}
+
+int tb_get_pass_times_ms(float* ms, int* cnt) { return tb_get_pass_stats(ms, cnt, nullptr); }
+
+const char* tb_pass_kernel(int slot) {
+  if (slot < 0 || slot > 3) return "";
+  std::lock_guard<std::mutex> lk(g_tmu);
+  return g_slot_kernel[slot];
 }

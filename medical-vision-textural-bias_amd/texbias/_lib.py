@@ -51,6 +51,9 @@ def _proto(L):
         "tb_set_chain_chunk": (I, [I]),
         "tb_set_pass_timing": (I, [I]),
         "tb_get_pass_times_ms": (I, [P, P]),
+        "tb_get_pass_stats": (I, [P, P, P]),
+        "tb_pass_kernel": (C.c_char_p, [I]),
+        "tb_set_band_plans": (I, [I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -38,9 +38,16 @@ class FusedChain:
     """Compile ``transforms`` (instances from filters_and_operators) for batched device execution.
 
     ``__call__(x, pad=0)``: x [B, C, *spatial] float32 on a HIP device (spatial = 3 axes);
-    returns [B, C, *spatial[:-1], spatial[-1] + pad].  ``rngs``: optional per-sample list of
-    transform lists (independent RandomStates per sample, e.g. per rank); by default the same
-    transform objects draw for every sample in turn, exactly like a per-sample Compose.
+    returns [B, C, *spatial[:-1], spatial[-1] + pad].  The same transform objects draw for every
+    sample in turn, exactly like a per-sample Compose (per-rank streams: seed the transforms per
+    rank with ``set_random_state``).
+
+    Parity hooks (the reference's draws that a device run cannot reproduce):
+    ``phases`` -- per sample, the per-channel phase of the plane-wave spike coefficient as the
+    reference measured it (``angle(K[idx])`` after the low-pass is rounding noise); ``u`` -- the
+    salt-and-pepper uniform field [B, C, *spatial] (the reference's ``torch.rand``, :472);
+    ``cls`` -- int8 [B, C, *spatial] receiving the salt-and-pepper class map (0 keep, 1 MIN, 2 MAX).
+    After a call, ``last_minmax`` holds the per-sample (min, max) the salt-and-pepper stage used.
     """
 
     def __init__(self, transforms: Sequence, key: str = "image"):
@@ -50,9 +57,16 @@ class FusedChain:
         self.transforms = list(transforms)
         self.key = key
         self._mm: Optional[torch.Tensor] = None
+        self._mm_b = 0
+
+    @property
+    def last_minmax(self) -> Optional[np.ndarray]:
+        """float32 [B, 2] (min, max) per sample that the last call's salt-and-pepper stage used
+        (decoded on demand: reading it synchronises), or None when no such stage ran."""
+        return rt.keys_to_float(self._mm[: self._mm_b]) if self._mm_b else None
 
     # --- host side: one sample's draws, in Compose order --------------------------------
-    def _sample_plan(self, spatial) -> List:
+    def _sample_plan(self, spatial, phase: Optional[Sequence[float]] = None) -> List:
         """Returns a list of stages: ('k', program) or ('sap', p) for one sample."""
         stages: List = []
         prog: List = []
@@ -67,7 +81,10 @@ class FusedChain:
             elif k == "RandPlaneWaves_ellipsoid":
                 t.randomize(None)
                 if t._do_transform:
-                    prog += t.program_for(spatial)
+                    ops = t.program_for(spatial, phase)
+                    for op in ops[1:]:
+                        op.reserved = 1   # one plane-wave call: all channels read the pre-call spectrum
+                    prog += ops
             elif k == "WrapArtifactd":
                 prog += t.transform.program()
             elif k == "WrapArtifact":
@@ -92,23 +109,31 @@ class FusedChain:
             stages.append(("k", prog))
         return stages
 
-    def plan(self, B: int, spatial) -> List[List]:
-        return [self._sample_plan(spatial) for _ in range(B)]
+    def plan(self, B: int, spatial, phases: Optional[Sequence[Sequence[float]]] = None) -> List[List]:
+        if phases is not None and len(phases) != B:
+            raise ValueError("one phase list per sample")
+        return [self._sample_plan(spatial, None if phases is None else phases[b]) for b in range(B)]
 
     # --- device side --------------------------------------------------------------------
-    def __call__(self, x: torch.Tensor, pad: int = 0, plans: Optional[List[List]] = None) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, pad: int = 0, plans: Optional[List[List]] = None,
+                 phases: Optional[Sequence[Sequence[float]]] = None, u: Optional[torch.Tensor] = None,
+                 cls: Optional[torch.Tensor] = None) -> torch.Tensor:
         rt.require_hip(x, "FusedChain")
         if x.dim() != 5:
             raise ValueError("FusedChain expects [B, C, H, W, D]")
         B, C = x.shape[:2]
         spatial = tuple(x.shape[2:])
-        plans = plans if plans is not None else self.plan(B, spatial)
+        for t, nm in ((u, "u"), (cls, "cls")):
+            if t is not None and tuple(t.shape) != tuple(x.shape):
+                raise ValueError(f"{nm} must have the input's shape {tuple(x.shape)}")
+        plans = plans if plans is not None else self.plan(B, spatial, phases)
         nst = len(plans[0])
         if any(len(p) != nst or [s[0] for s in p] != [s[0] for s in plans[0]] for p in plans):
             raise ValueError("all samples of a batch must share the stage structure")
         if self._mm is None or self._mm.shape[0] < B or self._mm.device != x.device:
             self._mm = torch.empty((max(B, 8), 2), dtype=torch.int32, device=x.device)
         mm = self._mm[:B]
+        self._mm_b = 0
         cur = x
         padded = False
         mm_valid = False
@@ -137,8 +162,26 @@ class FusedChain:
                 if not mm_valid:
                     rt.minmax_keys(view, 4, out=mm)
                 thr = [((np.float32(p / 2), np.float32(p)) if p is not None else (-1.0, -1.0)) for p in ps]
-                seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
-                rt.salt_and_pepper(view, 4, thr, mm, out=view, seed=seed)
+                if u is None and cls is None:
+                    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+                    rt.salt_and_pepper(view, 4, thr, mm, out=view, seed=seed)
+                else:
+                    # parity mode: the explicit field / class map share the (padded) view's strides
+                    def like_view(t, dtype):
+                        if t is None:
+                            return None
+                        if not padded:
+                            return t.to(device=x.device, dtype=dtype).contiguous()
+                        full = torch.zeros(cur.shape, dtype=dtype, device=x.device)
+                        full[..., : spatial[-1]] = t.to(device=x.device, dtype=dtype)
+                        return full[..., : spatial[-1]]
+                    uv = like_view(u, torch.float32)
+                    cv = like_view(cls, torch.int8) if cls is not None else None
+                    seed = 0 if u is not None else int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+                    rt.salt_and_pepper(view, 4, thr, mm, out=view, u=uv, cls=cv, seed=seed)
+                    if cls is not None:
+                        cls.copy_(cv)
+                self._mm_b = B
                 mm_valid = False
         if cur is x:
             cur = x.clone() if not pad else torch.nn.functional.pad(x, (0, pad))

@@ -310,6 +310,12 @@ def set_compiled_plans(enable: bool) -> None:
     check(lib().tb_set_compiled_plans(1 if enable else 0))
 
 
+def set_band_plans(enable: bool) -> None:
+    """Band-limited passes A'/B'/C' for low-pass programs when True (default), else the full
+    spectrum passes for every program (tb_set_band_plans)."""
+    check(lib().tb_set_band_plans(1 if enable else 0))
+
+
 def set_chain_chunk(n: int) -> None:
     """Channel-volumes per pass A -> B -> C chain (tb_set_chain_chunk): n > 0 chunks, 0 = whole
     batch group per pass, n < 0 = default (Infinity-Cache-sized chunks)."""
@@ -325,3 +331,14 @@ def pass_times_ms() -> Tuple[List[float], List[int]]:
     cnt = (C.c_int * 4)()
     check(lib().tb_get_pass_times_ms(ms, cnt))
     return list(ms), list(cnt)
+
+
+def pass_stats() -> Tuple[List[float], List[int], List[float], List[str]]:
+    """Per pass slot (0 forward, 1 k-space, 2 inverse, 3 salt-and-pepper / min-max) since timing
+    was enabled: summed ms, launch count, summed algorithmic bytes, last kernel name; clears."""
+    ms = (C.c_float * 4)()
+    cnt = (C.c_int * 4)()
+    nb = (C.c_double * 4)()
+    names = [lib().tb_pass_kernel(i).decode() for i in range(4)]
+    check(lib().tb_get_pass_stats(ms, cnt, nb))
+    return list(ms), list(cnt), list(nb), names

@@ -35,8 +35,9 @@ def run(rt, x, n_dims, prog, pad=0):
 @pytest.mark.parametrize("shape", [(2, 16, 16, 16), (1, 240, 240, 155), (4, 128, 128, 64), (1, 31, 17, 37 - 7),
                                    (3, 1, 1, 64), (2, 1, 256, 256), (1, 60, 1, 15)])
 def test_identity_roundtrip(rt, shape):
+    """Full-spectrum FFT round trip (wrap with alpha = 1 multiplies every coefficient by 1)."""
     x = np.random.default_rng(7).standard_normal(shape).astype(np.float32)
-    y, mm = run(rt, x, 3, [])
+    y, mm = run(rt, x, 3, [K.wrap_op(1.0)])
     assert relerr(y, x) < 2e-6
     assert mm[0] == x.min() or abs(mm[0] - x.min()) < 1e-5
     assert abs(mm[1] - x.max()) < 1e-5
@@ -197,12 +198,14 @@ def test_compiled_slab_plan_matches_generic(rt, shape):
     mm_c = torch.empty((B, 2), dtype=torch.int32, device="cuda")
     mm_g = torch.empty((B, 2), dtype=torch.int32, device="cuda")
     try:
+        rt.set_band_plans(False)   # this test is about the full-spectrum passes
         rt.set_compiled_plans(True)
         yc = rt.kspace_filter(x, 3, [prog] * B, shape[1], pad=5, minmax=mm_c)
         rt.set_compiled_plans(False)
         yg = rt.kspace_filter(x, 3, [prog] * B, shape[1], pad=5, minmax=mm_g)
     finally:
         rt.set_compiled_plans(True)
+        rt.set_band_plans(True)
     torch.cuda.synchronize()
     assert torch.all(yc[..., shape[-1]:] == 0)
     assert (yc - yg).abs().max().item() / yg.abs().max().item() < 2e-6
@@ -228,6 +231,7 @@ def test_chain_chunking_is_bit_identical(rt, shape):
              for b in range(B)]
     outs = []
     try:
+        rt.set_band_plans(False)   # chunking applies to the full-spectrum passes
         for n in (0, 1, 3):
             rt.set_chain_chunk(n)
             mm = torch.empty((B, 2), dtype=torch.int32, device="cuda")
@@ -235,6 +239,7 @@ def test_chain_chunking_is_bit_identical(rt, shape):
             outs.append((y, mm))
     finally:
         rt.set_chain_chunk(-1)
+        rt.set_band_plans(True)
     torch.cuda.synchronize()
     for y, mm in outs[1:]:
         assert torch.equal(y, outs[0][0])
