@@ -34,7 +34,6 @@ namespace tb {
 constexpr int BAND_NT = 256;
 constexpr int BAND_MAX_PTS = 8;    // out-of-box half-spectrum spike points per sample
 constexpr int BAND_ROWS_A = 64;    // image rows per pass-A' chunk (one per lane)
-constexpr int BAND_ROWS_C = 128;   // image rows per pass-C' chunk (4 waves x one 32-row MFMA tile)
 constexpr int BAND_MAX_NDK = 32;
 
 struct BandPt {
@@ -61,6 +60,7 @@ struct BandFwdArgs {
   int NKP;
   int bc0, nbc;
   BandGeo g;
+  int diag;         // measurement only (TEXBIAS_BAND_DIAG): skip stages, results invalid
 };
 
 struct BandMidArgs {
@@ -85,6 +85,7 @@ struct BandInvArgs {
   uint32_t* mm;
   BandGeo g;
   BandSamplePts sp[TB_MAX_BATCH];
+  int diag;
 };
 
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels
@@ -104,20 +105,24 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
 // LDS bytes of the two slab kernels
 TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
   const int P = (D & 1) ? D : D + 1;
-  return (size_t)BAND_ROWS_A * P * 4 + (size_t)g.NDk * (BAND_ROWS_A + 1) * 8 + (size_t)W * 8;
+  const int KSd = (D / 2 + 1 + 3) / 4, NT2 = g.NDk <= 16 ? 1 : 2;
+  return (size_t)(BAND_ROWS_A * P + 8) * 4 + (size_t)g.NDk * (BAND_ROWS_A + 1) * 8 + (size_t)W * 8 +
+         (size_t)NT2 * KSd * 128 * 4;
 }
 struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
   int bimg, va, zb, awbw, tww, total;
 };
 TB_HD int band_al16(int b) { return (b + 15) & ~15; }
+TB_HD int band_vt(const BandGeo& g) { return 2 * g.KS <= 32 ? 1 : 2; }  // 32-row tiles of V
 TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W) {
-  const int KC2 = 2 * g.KS;
+  const int NVR = 32 * band_vt(g);
+  const int KV = g.KW + 1 + (g.KS - g.NDk);
   BandInvCarve c;
-  c.bimg = 0;
-  c.va = band_al16(c.bimg + KC2 * g.NCOL * 4);
-  c.zb = band_al16(c.va + BAND_ROWS_C * (KC2 + 1) * 4);
-  c.awbw = band_al16(c.zb + g.ncol * 8);
-  c.tww = band_al16(c.awbw + (g.KW + 1) * g.NDk * 16);
+  c.bimg = 0;                                                // [NVR][NCOL] synthesis table
+  c.va = band_al16(c.bimg + NVR * g.NCOL * 4);               // [NVR][2 KV + 1] V-product matrix
+  c.zb = band_al16(c.va + NVR * (2 * KV + 1) * 4);           // [ncol] Z_h
+  c.awbw = c.zb;
+  c.tww = band_al16(c.zb + g.ncol * 8);                      // [W] twiddles
   c.total = band_al16(c.tww + W * 8);
   return c;
 }

@@ -22,75 +22,111 @@ __device__ __forceinline__ float2 ld2(const cf* p) {
 }
 
 // ----------------------------------------------------------------------------- pass A'
-// Copy n image rows (global rows g0.., row pitch sw, D floats each) into LDS rows 0.. of pitch
-// P.  Contiguous rows (sw == D) stream as 16-B lanes from the 16-B-aligned address at or below
-// the first element; the few out-of-range elements of the first/last vector are dropped.
-template <int U>
-__device__ __forceinline__ void band_load_rows(float* xs, int P, const float* __restrict__ xb, int64_t sw, int g0,
-                                               int n, int D, const FastDiv& fd, int tid) {
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  const float* src = xb + (int64_t)g0 * sw;
-  const int total = n * D;
-  if (sw == D) {
-    const int off = (int)((reinterpret_cast<uintptr_t>(src) >> 2) & 3);
-    const f32x4* s4 = reinterpret_cast<const f32x4*>(src - off);
-    const int nq = (total + off + 3) >> 2;
-    const bool odd = (D & 1) != 0;
-    for (int q0 = tid; q0 < nq; q0 += BAND_NT * U) {
-      f32x4 v[U];  // U independent 16-B loads in flight per lane before the first LDS store
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int BAND_PF = 10;  // 16-B (or 4-B) prefetch registers per lane: 64 rows x D <= 2560 floats
+
+// One 64-row chunk of a slab: where its rows start and how they are laid out in memory.
+struct ChunkSrc {
+  const float* src;  // first element of the chunk's first row
+  int total;         // rows * D
+  int off;           // contiguous rows: src - (16-B aligned start), in floats
+  int nq;            // contiguous rows: 16-B vectors covering the chunk
+};
+__device__ __forceinline__ ChunkSrc chunk_src(const float* xb, int64_t sw, int w0, int nr, int D) {
+  ChunkSrc c;
+  c.src = xb + (int64_t)w0 * sw;
+  c.total = nr * D;
+  c.off = (int)((reinterpret_cast<uintptr_t>(c.src) >> 2) & 3);
+  c.nq = (c.total + c.off + 3) >> 2;
+  return c;
+}
+// Issue the chunk's global loads into registers (no LDS traffic): every lane keeps up to
+// BAND_PF independent 16-B loads in flight while the current chunk is computed (contiguous rows).
+__device__ __forceinline__ void chunk_load(f32x4 (&v)[BAND_PF], const ChunkSrc& c, int tid) {
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(c.src - c.off);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int q = q0 + u * BAND_NT;
-        if (q < nq) v[u] = __builtin_nontemporal_load(s4 + q);
-      }
+  for (int u = 0; u < BAND_PF; ++u) {
+    const int q = tid + u * BAND_NT;
+    if (q < c.nq) v[u] = __builtin_nontemporal_load(s4 + q);
+  }
+}
+// Odd D (LDS pitch = D): the chunk is one contiguous run in LDS too, laid out so that element e
+// sits at X[off + e] -- every 16-B global vector lands 16-B aligned in LDS (one ds_write_b128,
+// no per-element index math); the chunk's base pointer is then X + off.  Even D (pitch D + 1 for
+// conflict-free row reads) inserts one pad float per row.
+__device__ __forceinline__ const float* chunk_store(float* X, const f32x4 (&v)[BAND_PF], const ChunkSrc& c, int D,
+                                                    const FastDiv& fd, int tid) {
+  if (D & 1) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int q = q0 + u * BAND_NT;
-        if (q >= nq) break;
+    for (int u = 0; u < BAND_PF; ++u) {
+      const int q = tid + u * BAND_NT;
+      if (q < c.nq) *reinterpret_cast<f32x4*>(X + 4 * q) = v[u];
+    }
+    return X + c.off;
+  }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int e = 4 * q + k - off;
-          if (e >= 0 && e < total) xs[odd ? e : e + fd.div(e)] = v[u][k];
-        }
+  for (int u = 0; u < BAND_PF; ++u) {
+    const int e0 = 4 * (tid + u * BAND_NT) - c.off;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = e0 + k;
+      if (e >= 0 && e < c.total) X[e + fd.div(e)] = v[u][k];
+    }
+  }
+  return X;
+}
+// strided rows (e.g. the padded U-Net buffer filtered in place): plain copy, no prefetch
+__device__ __forceinline__ void chunk_copy_strided(float* xs, int P, const ChunkSrc& c, int64_t sw, int D,
+                                                   const FastDiv& fd, int tid) {
+  for (int e0 = tid; e0 < c.total; e0 += 8 * BAND_NT) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = e0 + k * BAND_NT;
+      if (e < c.total) {
+        const int r = fd.div(e);
+        v[k] = c.src[(int64_t)r * sw + (e - r * D)];
       }
     }
-  } else {
-    for (int e0 = tid; e0 < total; e0 += BAND_NT * U) {
-      float v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = e0 + u * BAND_NT;
-        if (e < total) {
-          const int r = fd.div(e);
-          v[u] = src[(int64_t)r * sw + (e - r * D)];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = e0 + u * BAND_NT;
-        if (e < total) {
-          const int r = fd.div(e);
-          xs[r * P + (e - r * D)] = v[u];
-        }
+    for (int k = 0; k < 8; ++k) {
+      const int e = e0 + k * BAND_NT;
+      if (e < c.total) {
+        const int r = fd.div(e);
+        xs[r * P + (e - r * D)] = v[k];
       }
     }
   }
 }
 
-// NK: kd values per wave (4 waves: NDk <= 4 NK); NI: stage-W items per thread ((KW+1) NDk <= 256 NI)
-template <int NK, int NI>
+// NT2: 16-wide kd tiles (NDk <= 16 NT2); NI: stage-W items per thread ((KW+1) NDk <= 256 NI)
+template <int NT2, int NI>
 __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   const BandFwdArgs& a = kargs<BandFwdArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int tid = (int)threadIdx.x, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
   const int NDk = a.g.NDk, KW = a.g.KW, ncol = a.g.ncol;
   const int P = (D & 1) ? D : D + 1;
-  float* xs = reinterpret_cast<float*>(smem);
-  float2* Rb = reinterpret_cast<float2*>(xs + BAND_ROWS_A * P);  // [kd][65]
-  float2* twW = Rb + NDk * (BAND_ROWS_A + 1);                     // (cos, -sin)(2 pi t / W)
+  const int Ld = D / 2 + 1;                 // folded d in [0, D/2]
+  const int KSd = (Ld + 3) / 4;             // 16x16x4 k-steps
+  float* X = reinterpret_cast<float*>(smem);                                    // [64][P] (+8 slack)
+  float2* Rb = reinterpret_cast<float2*>(X + BAND_ROWS_A * P + 8);              // [kd][65]
+  float2* twW = Rb + NDk * (BAND_ROWS_A + 1);                                   // (cos, -sin)(2 pi t / W)
+  float* Bt = reinterpret_cast<float*>(twW + W);                                // [NT2][KSd][2][64]
   for (int t = tid; t < W; t += BAND_NT) twW[t] = ld2(a.pl.tw[1] + t);
+  // B fragments of the folded D product: lane l of k-step ks holds d = 4 ks + l/16, kd = 16 nt + l%16
+  for (int e = tid; e < NT2 * KSd * 128; e += BAND_NT) {
+    const int ln = e & 63, part = (e >> 6) & 1, ks = (e >> 7) % KSd, nt = (e >> 7) / KSd;
+    const int d = 4 * ks + (ln >> 4), kd = 16 * nt + (ln & 15);
+    float v = 0.f;
+    if (d < Ld && kd < NDk) {
+      const cf tw = a.pl.tw[2][(int)(((int64_t)kd * d) % D)];  // (cos, -sin)
+      v = part ? -tw.y : tw.x;
+    }
+    Bt[e] = v;
+  }
   const FastDiv fd = FastDiv::make(D);
   const int nitems = (KW + 1) * NDk;
   int ikw[NI], ikd[NI];
@@ -102,87 +138,111 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   }
   const int units = H * a.nbc;
   const int nch = (W + BAND_ROWS_A - 1) / BAND_ROWS_A;
-  const int kd0 = wv * NK;
-  const bool dwave = kd0 < NDk;  // this wave owns at least one kd
-  const int npair = (D - 1) / 2;  // d in [1, npair] pairs with D - d
-  // twiddles are wave-uniform: read them through the constant address space so they arrive by
-  // scalar loads into SGPRs (a generic pointer gets per-lane vector loads of the same bytes)
-  typedef const __attribute__((address_space(4))) float cfloat;
-  const cfloat* tdf = (const cfloat*)(a.tdf + kd0);  // (cos, sin) pairs
-  const int NKP = a.NKP;
-  for (int u = (int)blockIdx.x; u < units; u += (int)gridDim.x) {
-    const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
-    const float* __restrict__ xb = a.x + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
-    float2 Ac[NI], As[NI];
+  const bool contig = a.sw == D;
+  // (unit, chunk) sequence of this workgroup
+  int u = (int)blockIdx.x, c = 0;
+  if (u >= units) return;
+  auto xbase = [&](int uu) {
+    const int bcl = uu / H, hh = uu - bcl * H;
+    return a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)hh * a.sh;
+  };
+  f32x4 pf[BAND_PF];
+  ChunkSrc cs = chunk_src(xbase(u), a.sw, 0, W < BAND_ROWS_A ? W : BAND_ROWS_A, D);
+  const int diag = a.diag;
+  if (contig) chunk_load(pf, cs, tid);
+  float2 Ac[NI], As[NI];
 #pragma unroll
-    for (int q = 0; q < NI; ++q) Ac[q] = As[q] = make_float2(0.f, 0.f);
-    for (int c = 0; c < nch; ++c) {
-      const int w0 = c * BAND_ROWS_A;
-      const int nr = (W - w0) < BAND_ROWS_A ? (W - w0) : BAND_ROWS_A;
-      __syncthreads();  // the previous chunk's readers of xs / Rb are done
-      band_load_rows<10>(xs, P, xb, a.sw, w0, nr, D, fd, tid);
-      __syncthreads();
-      // D stage: lane = row, this wave's kd group; X(kd) = x0 + sum_d s_d cos - i t_d sin
-      if (dwave) {
-        const float* row = xs + lane * P;
-        float re[NK], im[NK];
-        const float x0 = row[0];
+  for (int q = 0; q < NI; ++q) Ac[q] = As[q] = make_float2(0.f, 0.f);
+  const int rbase = 16 * wv;  // this wave's 16 rows of the chunk
+  for (;;) {
+    const int w0 = c * BAND_ROWS_A;
+    const int nr = (W - w0) < BAND_ROWS_A ? (W - w0) : BAND_ROWS_A;
+    const float* xs = X;
+    if (diag & 2)
+      xs = X;
+    else if (contig)
+      xs = chunk_store(X, pf, cs, D, fd, tid);
+    else
+      chunk_copy_strided(X, P, cs, a.sw, D, fd, tid);
+    __syncthreads();  // xs ready; every lane is past the previous chunk's W stage (Rb free)
+    // next (unit, chunk): its loads fly while this chunk is computed
+    int un = u, cn = c + 1;
+    if (cn == nch) { cn = 0; un = u + (int)gridDim.x; }
+    if (un < units) {
+      const int w0n = cn * BAND_ROWS_A;
+      cs = chunk_src(xbase(un), a.sw, w0n, (W - w0n) < BAND_ROWS_A ? (W - w0n) : BAND_ROWS_A, D);
+      if (contig && !(diag & 1)) chunk_load(pf, cs, tid);
+    }
+    // D stage on the matrix cores: R(row, kd) = sum_d s_d cos + i sum_d t_d sin (folded over d, D - d)
+    if (!(diag & 4)) {
+      const float* row = xs + (rbase + l15) * P;
+      f32x4 accc[NT2], accs[NT2];
 #pragma unroll
-        for (int k = 0; k < NK; ++k) { re[k] = x0; im[k] = 0.f; }
-#pragma unroll 4
-        for (int d = 1; d <= npair; ++d) {
-          const float xa = row[d], xm = row[D - d];
-          const float s = xa + xm, t = xm - xa;
-          const cfloat* tt = tdf + 2 * d * NKP;
+      for (int nt = 0; nt < NT2; ++nt)
 #pragma unroll
-          for (int k = 0; k < NK; ++k) {
-            re[k] = fmaf(s, tt[2 * k], re[k]);
-            im[k] = fmaf(t, tt[2 * k + 1], im[k]);
-          }
+        for (int j = 0; j < 4; ++j) accc[nt][j] = accs[nt][j] = 0.f;
+      for (int ks = 0; ks < KSd; ++ks) {
+        const int d = 4 * ks + l4;
+        const bool has = d < Ld;
+        const bool pair = d >= 1 && 2 * d < D;
+        const float xa = has ? row[d] : 0.f;
+        const float xm = pair ? row[D - d] : 0.f;
+        const float sv = xa + xm, tv = pair ? xm - xa : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT2; ++nt) {
+          const float* bt = Bt + ((nt * KSd + ks) * 2) * 64 + lane;
+          accc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv, bt[0], accc[nt], 0, 0, 0);
+          accs[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv, bt[64], accs[nt], 0, 0, 0);
         }
-        if ((D & 1) == 0) {  // d = D/2 has no partner: cos = (-1)^kd, sin = 0
-          const float xh = row[D / 2];
-          const cfloat* tt = tdf + 2 * (D / 2) * NKP;
-#pragma unroll
-          for (int k = 0; k < NK; ++k) re[k] = fmaf(xh, tt[2 * k], re[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < NK; ++k)
-          if (kd0 + k < NDk) Rb[(kd0 + k) * (BAND_ROWS_A + 1) + lane] = make_float2(re[k], im[k]);
       }
-      __syncthreads();
-      // W stage: per (kw >= 0, kd): Ac += R_w cos, As += R_w sin (theta = 2 pi kw w / W)
+      // lane holds rows rbase + 4 (l/16) + j of kd = 16 nt + l%16
+#pragma unroll
+      for (int nt = 0; nt < NT2; ++nt) {
+        const int kd = 16 * nt + l15;
+        if (kd < NDk)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            Rb[kd * (BAND_ROWS_A + 1) + rbase + 4 * l4 + j] = make_float2(accc[nt][j], accs[nt][j]);
+      }
+    }
+    __syncthreads();  // Rb ready
+    // W stage: per (kw >= 0, kd): Ac += R_w cos, As += R_w sin (theta = 2 pi kw w / W)
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if (ikw[q] < 0 || (diag & 8)) continue;
+      const int kw = ikw[q];
+      const float2* Rk = Rb + ikd[q] * (BAND_ROWS_A + 1);
+      int t = (int)(((int64_t)kw * w0) % W);
+      float2 ac = Ac[q], as = As[q];
+#pragma unroll 4
+      for (int i = 0; i < nr; ++i) {
+        const float2 r = Rk[i];
+        const float2 tw = twW[t];
+        ac.x = fmaf(r.x, tw.x, ac.x);
+        ac.y = fmaf(r.y, tw.x, ac.y);
+        as.x = fmaf(r.x, -tw.y, as.x);
+        as.y = fmaf(r.y, -tw.y, as.y);
+        t += kw;
+        t = t >= W ? t - W : t;
+      }
+      Ac[q] = ac;
+      As[q] = as;
+    }
+    if (c == nch - 1) {  // P(kw) = Ac - i As, P(-kw) = Ac + i As
+      const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
+      cf* Pb = a.P + ((int64_t)bc * H + h) * ncol;
 #pragma unroll
       for (int q = 0; q < NI; ++q) {
         if (ikw[q] < 0) continue;
-        const int kw = ikw[q];
-        const float2* Rk = Rb + ikd[q] * (BAND_ROWS_A + 1);
-        int t = (int)(((int64_t)kw * w0) % W);
-        float2 ac = Ac[q], as = As[q];
-#pragma unroll 4
-        for (int i = 0; i < nr; ++i) {
-          const float2 r = Rk[i];
-          const float2 tw = twW[t];
-          ac.x = fmaf(r.x, tw.x, ac.x);
-          ac.y = fmaf(r.y, tw.x, ac.y);
-          as.x = fmaf(r.x, -tw.y, as.x);
-          as.y = fmaf(r.y, -tw.y, as.y);
-          t += kw;
-          t = t >= W ? t - W : t;
-        }
-        Ac[q] = ac;
-        As[q] = as;
+        const int kw = ikw[q], kd = ikd[q];
+        Pb[(KW + kw) * NDk + kd] = mk(Ac[q].x + As[q].y, Ac[q].y - As[q].x);
+        if (kw > 0) Pb[(KW - kw) * NDk + kd] = mk(Ac[q].x - As[q].y, Ac[q].y + As[q].x);
+        Ac[q] = As[q] = make_float2(0.f, 0.f);
       }
     }
-    // P(kw) = Ac - i As, P(-kw) = Ac + i As
-    cf* Pb = a.P + ((int64_t)bc * H + h) * ncol;
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (ikw[q] < 0) continue;
-      const int kw = ikw[q], kd = ikd[q];
-      Pb[(KW + kw) * NDk + kd] = mk(Ac[q].x + As[q].y, Ac[q].y - As[q].x);
-      if (kw > 0) Pb[(KW - kw) * NDk + kd] = mk(Ac[q].x - As[q].y, Ac[q].y + As[q].x);
-    }
+    if (un >= units) break;
+    u = un;
+    c = cn;
   }
 }
 
@@ -249,48 +309,59 @@ __global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
 }
 
 // ----------------------------------------------------------------------------- pass C'
+// Per (bc, h) slab, all on the matrix cores after a small VALU prologue:
+//   Z_h(kw, kd)  = A_0 + sum_kh>=1 (A cos + i B sin)           (VALU; AB from pass B')
+//   V^T(v, w)    = M2T(v, k) . CS(k, w)                        (MFMA 32x32x2; v = 2 kd + re/im and
+//                  two rows per out-of-box point, k = (kw, cos/sin) terms; w on the lane)
+//   Y^T(n, w)    = B^T(n, v) . V^T(v, w)                       (MFMA, V^T straight from the
+//                  accumulators: the k order of each step is the accumulator's row pair
+//                  (rho(s), rho(s) + 4), the same permutation indexes the B table)
+// so each lane ends with 4 consecutive output columns of one image row: 16-B stores.
+__device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
+
+template <int VT>  // 32-row tiles of V (2 (NDk + points) <= 32 VT)
 __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
   const BandInvArgs& a = kargs<BandInvArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float red[2 * BAND_NT / 64];
-  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int tid = (int)threadIdx.x, lane = tid & 63, hl = lane >> 5, l31 = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
-  const int NDk = a.g.NDk, KW = a.g.KW, KH = a.g.KH, ncol = a.g.ncol, KS = a.g.KS, NCOL = a.g.NCOL;
-  const int KC2 = 2 * KS, VP = KC2 + 1;
+  const int NDk = a.g.NDk, KW = a.g.KW, KH = a.g.KH, ncol = a.g.ncol, NCOL = a.g.NCOL;
+  const int npm = a.g.KS - NDk;        // point rows of the launch (max over its samples)
+  const int KV = KW + 1 + npm;         // k-steps of the V product
+  const int MP = 2 * KV + 1;           // M2T pitch
   const BandInvCarve cv = band_inv_carve(a.g, W);
-  float* Bimg = reinterpret_cast<float*>(smem + cv.bimg);    // [KC2][NCOL]
-  float* Va = reinterpret_cast<float*>(smem + cv.va);        // [128][VP]
-  float2* Zb = reinterpret_cast<float2*>(smem + cv.zb);      // [ncol]
-  float4* AwBw = reinterpret_cast<float4*>(smem + cv.awbw);  // [KW+1][NDk]
-  float2* twW = reinterpret_cast<float2*>(smem + cv.tww);    // (cos, -sin)(2 pi t / W)
+  float* Bimg = reinterpret_cast<float*>(smem + cv.bimg);  // [32 VT][NCOL]
+  float* M2T = reinterpret_cast<float*>(smem + cv.va);     // [32 VT][MP]
+  float2* Zb = reinterpret_cast<float2*>(smem + cv.zb);    // [ncol]
+  float2* twW = reinterpret_cast<float2*>(smem + cv.tww);  // (cos, -sin)(2 pi t / W)
   const cf* twD = a.pl.tw[2];
   for (int t = tid; t < W; t += BAND_NT) twW[t] = ld2(a.pl.tw[1] + t);
-  for (int t = tid; t < BAND_ROWS_C * VP; t += BAND_NT) Va[t] = 0.f;
-  // band rows of the D-synthesis table: B[2k][n] = cos(2 pi k n / D), B[2k+1][n] = -sin, 0 for n >= D
-  for (int e = tid; e < 2 * NDk * NCOL; e += BAND_NT) {
+  // synthesis table rows v: 2k -> cos(2 pi kd_k n / D), 2k + 1 -> -sin; 0 for n >= D and unused rows
+  for (int e = tid; e < 32 * VT * NCOL; e += BAND_NT) {
     const int r = e / NCOL, n = e - r * NCOL, k = r >> 1;
     float v = 0.f;
-    if (n < D) {
+    if (k < NDk && n < D) {
       const cf tw = twD[(int)(((int64_t)k * n) % D)];
       v = (r & 1) ? tw.y : tw.x;
     }
     Bimg[e] = v;
   }
   const int units = H * a.nbc;
-  const int npt_rows = KS - NDk;  // point columns of the table (the launch's max points)
+  const int ntw = (W + 31) / 32;     // 32-row tiles of the slab
+  const int ntn = NCOL / 32;         // 32-column tiles of the output row
+  const int ycols = D + a.ypad;
+  const int diag = a.diag;
   int cur_s = -1;
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  const int ncnk = (W + BAND_ROWS_C - 1) / BAND_ROWS_C;
-  const int ntile = NCOL / 32;
-  const int ycols = D + a.ypad;
   for (int u = (int)blockIdx.x; u < units; u += (int)gridDim.x) {
     const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
-    const int lb = a.cofs + bcl, s = lb / a.C;
+    const int s = (a.cofs + bcl) / a.C;
     const BandSamplePts& sp = a.sp[s];
-    __syncthreads();  // previous unit done with Zb / AwBw / Va / Bimg
-    if (s != cur_s && npt_rows > 0) {  // the sample's point rows of the table
-      for (int e = tid; e < 2 * npt_rows * NCOL; e += BAND_NT) {
+    __syncthreads();  // the previous unit is done with Zb / M2T / the point rows of Bimg
+    if (s != cur_s && npm > 0) {
+      for (int e = tid; e < 2 * npm * NCOL; e += BAND_NT) {
         const int r = e / NCOL, n = e - r * NCOL, j = r >> 1;
         float v = 0.f;
         if (j < sp.n && n < D) {
@@ -301,117 +372,135 @@ __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
       }
     }
     cur_s = s;
-    // Z_h(col) = A_0 + sum_kh>=1 (A cos + i B sin), theta = 2 pi kh h / H
+    // Z_h(col) = A_0 + sum_kh>=1 (A cos + i B sin), theta = 2 pi kh h / H; loads issued 4 at a time
     const float4* ABb = a.AB + (int64_t)bc * (KH + 1) * ncol;
-    for (int col = tid; col < ncol; col += BAND_NT) {
+    for (int col = (diag & 1) ? ncol : tid; col < ncol; col += BAND_NT) {
       const float4 a0 = ABb[col];
       float zx = a0.x, zy = a0.y;
       int t = 0;
-      for (int k = 1; k <= KH; ++k) {
-        t += h;
-        t = t >= H ? t - H : t;
-        const float4 ab = ABb[(int64_t)k * ncol + col];
-        const cf tw = a.pl.tw[0][t];  // (cos, -sin)
-        zx = fmaf(ab.x, tw.x, fmaf(ab.w, tw.y, zx));   // - B.y sin
-        zy = fmaf(ab.y, tw.x, fmaf(-ab.z, tw.y, zy));  // + B.x sin
+      for (int k0 = 1; k0 <= KH; k0 += 4) {
+        float4 ab[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (k0 + q <= KH) ab[q] = ABb[(int64_t)(k0 + q) * ncol + col];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (k0 + q > KH) break;
+          t += h;
+          t = t >= H ? t - H : t;
+          const cf tw = a.pl.tw[0][t];  // (cos, -sin)
+          zx = fmaf(ab[q].x, tw.x, fmaf(ab[q].w, tw.y, zx));   // - B.y sin
+          zy = fmaf(ab[q].y, tw.x, fmaf(-ab[q].z, tw.y, zy));  // + B.x sin
+        }
       }
       Zb[col] = make_float2(zx, zy);
     }
-    __syncthreads();
-    // W-pair sums: A_kw = Z(kw) + Z(-kw), B_kw = Z(kw) - Z(-kw)
-    for (int it = tid; it < (KW + 1) * NDk; it += BAND_NT) {
-      const int kw = it / NDk, kd = it - kw * NDk;
-      const float2 zp = Zb[(KW + kw) * NDk + kd];
-      if (kw == 0) {
-        AwBw[it] = make_float4(zp.x, zp.y, 0.f, 0.f);
-      } else {
-        const float2 zm = Zb[(KW - kw) * NDk + kd];
-        AwBw[it] = make_float4(zp.x + zm.x, zp.y + zm.y, zp.x - zm.x, zp.y - zm.y);
-      }
-    }
-    // the sample's point coefficients, rotated to this slab's h: c e^{+2 pi i kh_p h / H} wt / N
+    // the sample's point coefficients rotated to this slab: ph_j = c_j e^{+2 pi i kh_j h / H} wt / N
     float2 ph[BAND_MAX_PTS];
 #pragma unroll
     for (int j = 0; j < BAND_MAX_PTS; ++j) {
       ph[j] = make_float2(0.f, 0.f);
-      if (j < sp.n && j < npt_rows) {
+      if (j < sp.n && j < npm) {
         const cf c = a.pts[(int64_t)bc * BAND_MAX_PTS + j];
         const cf tw = a.pl.tw[0][(int)(((int64_t)sp.p[j].kh * h) % H)];
         const float wt = ((sp.p[j].kd == 0 || 2 * sp.p[j].kd == D) ? 1.f : 2.f) * a.scale;
-        // c * conj(tw) = c e^{+i theta}  (tw = e^{-i theta})
         ph[j] = make_float2((c.x * tw.x + c.y * tw.y) * wt, (c.y * tw.x - c.x * tw.y) * wt);
       }
     }
     __syncthreads();
-    float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
-    for (int cc = 0; cc < ncnk; ++cc) {
-      const int w0 = cc * BAND_ROWS_C;
-      const int nr = (W - w0) < BAND_ROWS_C ? (W - w0) : BAND_ROWS_C;
-      if (cc > 0) __syncthreads();  // the previous chunk's MFMA reads of Va are done
-      // V_w(kd) = sum_kw>=0 (A cos + i B sin), theta = 2 pi kw w / W; scaled by wt(kd) / N
-      for (int it = tid; it < nr * NDk; it += BAND_NT) {
-        const int i = it / NDk, kd = it - i * NDk;
-        const int w = w0 + i;
-        float sx = 0.f, sy = 0.f;
-        int t = 0;
-        const float4* ab = AwBw + kd;
-        for (int kw = 0; kw <= KW; ++kw) {
-          const float4 v = ab[kw * NDk];
-          const float2 tw = twW[t];  // (cos, -sin)
-          sx = fmaf(v.x, tw.x, fmaf(v.w, tw.y, sx));
-          sy = fmaf(v.y, tw.x, fmaf(-v.z, tw.y, sy));
-          t += w;
-          t = t >= W ? t - W : t;
+    // M2T(v, k): Vr = sum (Ar cos - Bi sin), Vi = sum (Ai cos + Br sin) over kw; points: ph e^{+i phi}
+    for (int e = (diag & 2) ? 32 * VT * 2 * KV : tid; e < 32 * VT * 2 * KV; e += BAND_NT) {
+      const int r = e / (2 * KV), k = e - r * (2 * KV);
+      const int ks = k >> 1, sn = k & 1, im = r & 1, kd = r >> 1;
+      float v = 0.f;
+      if (kd < NDk) {
+        if (ks <= KW) {
+          const float2 zp = Zb[(KW + ks) * NDk + kd];
+          float2 A = zp, B = make_float2(0.f, 0.f);
+          if (ks > 0) {
+            const float2 zm = Zb[(KW - ks) * NDk + kd];
+            A = make_float2(zp.x + zm.x, zp.y + zm.y);
+            B = make_float2(zp.x - zm.x, zp.y - zm.y);
+          }
+          const float wt = ((kd == 0 || 2 * kd == D) ? 1.f : 2.f) * a.scale;
+          v = (im ? (sn ? B.x : A.y) : (sn ? -B.y : A.x)) * wt;
         }
-        const float wt = ((kd == 0 || 2 * kd == D) ? 1.f : 2.f) * a.scale;
-        Va[i * VP + 2 * kd] = sx * wt;
-        Va[i * VP + 2 * kd + 1] = sy * wt;
-      }
-      // point columns: ph_j e^{+2 pi i kw_p w / W}
-      for (int it = tid; it < nr * npt_rows; it += BAND_NT) {
-        const int i = it / npt_rows, j = it - i * npt_rows;
-        float vx = 0.f, vy = 0.f;
-        if (j < sp.n) {
-          const int w = w0 + i;
-          const float2 tw = twW[(int)(((int64_t)sp.p[j].kw * w) % W)];
+      } else if (kd - NDk < npm) {
+        const int j = kd - NDk;
+        if (ks == KW + 1 + j) {
           float2 c = make_float2(0.f, 0.f);
 #pragma unroll
           for (int jj = 0; jj < BAND_MAX_PTS; ++jj)
             if (jj == j) c = ph[jj];
-          vx = c.x * tw.x + c.y * tw.y;
-          vy = c.y * tw.x - c.x * tw.y;
+          v = im ? (sn ? c.x : c.y) : (sn ? -c.y : c.x);
         }
-        Va[i * VP + 2 * (NDk + j)] = vx;
-        Va[i * VP + 2 * (NDk + j) + 1] = vy;
       }
-      __syncthreads();
-      // D synthesis on the matrix cores: y[m][n] = sum_k Va[m][k] B[k][n]; wave = 32-row tile
-      const int mrow0 = wv * 32;
-      if (mrow0 < nr) {
-        const float* va = Va + (mrow0 + (lane & 31)) * VP + (lane >> 5);
-        for (int nt = 0; nt < ntile; ++nt) {
-          f32x16 acc;
+      M2T[r * MP + k] = v;
+    }
+    __syncthreads();
+    const float* afr = M2T + l31 * MP + hl;  // A fragment of k-step ks, tile vt: afr[32 vt MP + 2 ks]
+    float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
+    const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
+    for (int tw_ = wv; tw_ < ntw; tw_ += 4) {
+      const int w = 32 * tw_ + l31;
+      const bool wok = w < W;
+      const int wm = w % W;
+      // V^T(:, w) for this lane's row w
+      f32x16 vacc[VT];
 #pragma unroll
-          for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-          const float* bb = Bimg + (lane >> 5) * NCOL + nt * 32 + (lane & 31);
-          for (int ks = 0; ks < KS; ++ks)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(va[2 * ks], bb[2 * ks * NCOL], acc, 0, 0, 0);
-          const int n = nt * 32 + (lane & 31);
-          if (n < ycols) {
-            const bool real = n < D;
+      for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              const int m = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
-              if (mrow0 + m < nr) {
-                const float v = acc[j];
-                yb[(int64_t)(w0 + mrow0 + m) * a.sw + n] = v;
-                if (real) {
-                  lo = fminf(lo, v);
-                  hi = fmaxf(hi, v);
-                }
-              }
-            }
+        for (int j = 0; j < 16; ++j) vacc[vt][j] = 0.f;
+      int t = 0;
+      for (int ks = 0; ks <= ((diag & 4) ? -1 : KW); ++ks) {
+        const float2 c = twW[t];
+        const float b = hl ? -c.y : c.x;
+#pragma unroll
+        for (int vt = 0; vt < VT; ++vt)
+          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(afr[32 * vt * MP + 2 * ks], b, vacc[vt], 0, 0, 0);
+        t += wm;
+        t = t >= W ? t - W : t;
+      }
+      for (int j = 0; j < npm; ++j) {
+        const int kw = j < sp.n ? sp.p[j].kw : 0;
+        const float2 c = twW[(int)(((int64_t)kw * wm) % W)];
+        const float b = hl ? -c.y : c.x;
+#pragma unroll
+        for (int vt = 0; vt < VT; ++vt)
+          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(afr[32 * vt * MP + 2 * (KW + 1 + j)], b, vacc[vt], 0, 0, 0);
+      }
+      float* yr = yb + (int64_t)w * a.sw;
+      for (int nt = 0; nt < ntn; ++nt) {
+        f32x16 y;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) y[j] = 0.f;
+        const float* bb = Bimg + (4 * hl) * NCOL + nt * 32 + l31;
+        if (!(diag & 8))
+#pragma unroll
+          for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+            for (int sI = 0; sI < 16; ++sI)
+              y = __builtin_amdgcn_mfma_f32_32x32x2f32(bb[(32 * vt + acc_row(sI)) * NCOL], vacc[vt][sI], y, 0, 0, 0);
+        if (!wok || (diag & 16)) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n0 = nt * 32 + 8 * g + 4 * hl;
+          const float v0 = y[4 * g], v1 = y[4 * g + 1], v2 = y[4 * g + 2], v3 = y[4 * g + 3];
+          if (vec && n0 + 4 <= ycols) {
+            *reinterpret_cast<float4*>(yr + n0) = make_float4(v0, v1, v2, v3);
+          } else {
+            const float vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (n0 + q < ycols) yr[n0 + q] = vv[q];
           }
+          const float vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (n0 + q < D) {
+              lo = fminf(lo, vv[q]);
+              hi = fmaxf(hi, vv[q]);
+            }
         }
       }
     }
@@ -467,9 +556,9 @@ int band_grid(int units, size_t lds, int ncu) {
   return units < g ? units : g;
 }
 
-template <int NK, int NI>
+template <int NT2, int NI>
 hipError_t launch_fwd_t(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
-  auto kern = k_band_fwd<NK, NI>;
+  auto kern = k_band_fwd<NT2, NI>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
   const int units = a.pl.H * a.nbc;
@@ -477,23 +566,30 @@ hipError_t launch_fwd_t(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t s
   return hipGetLastError();
 }
 
-template <int NK>
-hipError_t launch_fwd_nk(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
+template <int NT2>
+hipError_t launch_fwd_nt(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
   const int items = (a.g.KW + 1) * a.g.NDk;
-  if (items <= BAND_NT) return launch_fwd_t<NK, 1>(a, lds, ncu, st);
-  if (items <= 2 * BAND_NT) return launch_fwd_t<NK, 2>(a, lds, ncu, st);
-  return launch_fwd_t<NK, 4>(a, lds, ncu, st);
+  if (items <= BAND_NT) return launch_fwd_t<NT2, 1>(a, lds, ncu, st);
+  if (items <= 2 * BAND_NT) return launch_fwd_t<NT2, 2>(a, lds, ncu, st);
+  return launch_fwd_t<NT2, 4>(a, lds, ncu, st);
+}
+
+template <int VT>
+hipError_t launch_inv_t(const BandInvArgs& a, int ncu, hipStream_t st) {
+  const size_t lds = band_inv_carve(a.g, a.pl.W).total;
+  auto kern = k_band_inv<VT>;
+  hipError_t e = allow_lds(kern, lds);
+  if (e != hipSuccess) return e;
+  const int units = a.pl.H * a.nbc;
+  hipLaunchKernelGGL(kern, dim3(band_grid(units, lds, ncu)), dim3(BAND_NT), lds, st, a);
+  return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_band_fwd(const BandFwdArgs& a, int ncu, hipStream_t st) {
   const size_t lds = band_lds_fwd(a.g, a.pl.W, a.pl.D);
-  const int nk = (a.g.NDk + 3) / 4;
-  if (nk <= 1) return launch_fwd_nk<1>(a, lds, ncu, st);
-  if (nk <= 2) return launch_fwd_nk<2>(a, lds, ncu, st);
-  if (nk <= 4) return launch_fwd_nk<4>(a, lds, ncu, st);
-  return launch_fwd_nk<8>(a, lds, ncu, st);
+  return a.g.NDk <= 16 ? launch_fwd_nt<1>(a, lds, ncu, st) : launch_fwd_nt<2>(a, lds, ncu, st);
 }
 
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
@@ -501,13 +597,10 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+
+
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
-  const size_t lds = band_inv_carve(a.g, a.pl.W).total;
-  hipError_t e = allow_lds(k_band_inv, lds);
-  if (e != hipSuccess) return e;
-  const int units = a.pl.H * a.nbc;
-  hipLaunchKernelGGL(k_band_inv, dim3(band_grid(units, lds, ncu)), dim3(BAND_NT), lds, st, a);
-  return hipGetLastError();
+  return 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
 }
 
 hipError_t launch_copy_pad(const CopyArgs& a, hipStream_t st) {

@@ -389,6 +389,11 @@ static bool g_band = [] {
   const char* e = std::getenv("TEXBIAS_BAND");
   return !(e && e[0] == '0');
 }();
+// measurement only: TEXBIAS_BAND_DIAG=0xIIFF skips stages of A' (FF) / C' (II); results invalid
+static int g_band_diag = [] {
+  const char* e = std::getenv("TEXBIAS_BAND_DIAG");
+  return e ? (int)std::strtol(e, nullptr, 0) : 0;
+}();
 
 // A low-pass op that zeroes every coefficient outside a box around DC (all channels).
 static bool band_is_lowpass(const tb_op& op) {
@@ -486,6 +491,7 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   g.KS = g.NDk + npt;
   g.NCOL = 32 * ((D + y_pad + 31) / 32);
   if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || (KW + 1) * g.NDk > 4 * BAND_NT) return false;
+  if (2 * g.KS > 64) return false;  // pass C' holds V in at most two 32-row MFMA tiles
   // worth it only when the box is a small part of the half spectrum
   if ((double)(2 * KH + 1) * g.ncol * 4.0 > (double)H * W * (D / 2 + 1)) return false;
   if (band_lds_fwd(g, W, D) > 160000 || band_inv_carve(g, W).total > 160000) return false;
@@ -556,7 +562,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
   const double pbytes = (double)nbc * H * g.ncol * 8.0, abytes = (double)nbc * (g.KH + 1) * g.ncol * 16.0;
   {
     Timer t(0, st, (double)nbc * H * W * D * 4.0 + pbytes, "k_band_fwd");
-    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g};
+    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g, g_band_diag & 0xff};
     TB_HIP(tb::launch_band_fwd(fa, p->ncu, st));
   }
   {
@@ -597,6 +603,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.scale = (float)(1.0 / ((double)H * (double)W * (double)D));
     ia.mm = minmax;
     ia.g = g;
+    ia.diag = (g_band_diag >> 8) & 0xff;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
     TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
   }
