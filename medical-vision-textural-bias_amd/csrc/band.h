@@ -35,6 +35,8 @@ constexpr int BAND_NT = 256;
 constexpr int BAND_MAX_PTS = 8;    // out-of-box half-spectrum spike points per sample
 constexpr int BAND_ROWS_A = 64;    // image rows per pass-A' chunk (one per lane)
 constexpr int BAND_MAX_NDK = 32;
+constexpr int BAND_MAX_KH = 31;    // box half-height
+constexpr int BAND_MAX_ZCOL = 1024; // box columns (kw, kd) per slab held in pass B2''s LDS
 
 struct BandPt {
   int16_t kh, kw, kd, pad;  // unsigned frequency of the stored (kd <= D/2) coefficient
@@ -48,7 +50,7 @@ struct BandGeo {
   int KH, KW, NDk;  // box: signed kh in [-KH, KH], signed kw in [-KW, KW], kd in [0, NDk)
   int NW, ncol;     // 2 KW + 1, NW * NDk  (a "column" = one (kw, kd) pair of the box)
   int KS;           // k-steps of the inverse D MFMA: NDk band columns + the launch's max points
-  int NCOL;         // output columns of the MFMA n-tiles: 32 * ceil((D + pad) / 32)
+  int NCOL;         // folded output columns of the MFMA n-tiles: 32 * ceil((D/2 + 1) / 32)
 };
 
 struct BandFwdArgs {
@@ -61,6 +63,7 @@ struct BandFwdArgs {
   int bc0, nbc;
   BandGeo g;
   int diag;         // measurement only (TEXBIAS_BAND_DIAG): skip stages, results invalid
+  const float* tbt; // [2][KSd][2][64] B fragments of the folded D product (plan table)
 };
 
 struct BandMidArgs {
@@ -68,6 +71,8 @@ struct BandMidArgs {
   const cf* P;
   float4* AB;       // [bc][KH + 1][ncol]: (Q'(kh) + Q'(-kh), Q'(kh) - Q'(-kh))
   cf* pts;          // [bc][BAND_MAX_PTS]
+  float* M2F;       // [bc][H][VT][KV][64]: pass C''s V-product A fragments (written by B2')
+  float scale;      // 1 / (H W D)
   int bc0, C, cofs, nbc;
   BandGeo g;
   BandSamplePts sp[TB_MAX_BATCH];
@@ -76,21 +81,54 @@ struct BandMidArgs {
 
 struct BandInvArgs {
   tb_plan_dev pl;
+  const float* M2F; // [bc][H][VT][KV][64] V-product A fragments (pass B2')
   const float4* AB;
   const cf* pts;
   float* y;
   int64_t sbc, sh, sw;
   int ypad, bc0, C, cofs, nbc;
   float scale;      // 1 / (H W D)
-  uint32_t* mm;
+  uint32_t* mm;     // per-sample min/max keys (written, not accumulated: whole samples per launch)
+  float2* mmp;      // [b][C H ntw] per-(slab, 32-row tile) (min, max) partials
   BandGeo g;
   BandSamplePts sp[TB_MAX_BATCH];
   int diag;
+  const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
 };
+
+// LDS bytes of the two slab kernels
+TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
+  const int P = (D & 1) ? D : D + 1;
+  const int KSd = (D / 2 + 1 + 3) / 4, NT2 = g.NDk <= 16 ? 1 : 2, KWT = g.KW < 16 ? 1 : 2;
+  int xn = BAND_ROWS_A * P + 8;                     // the chunk, and the waves' O partials at slab end
+  const int ob = 4 * 2 * 2 * KWT * NT2 * 64 * 4;
+  xn = xn > ob ? xn : ob;
+  return (size_t)xn * 4 + (size_t)W * 8 + (size_t)NT2 * KSd * 128 * 4;
+}
+constexpr int BAND_STG_P = 68;  // pitch (floats) of a wave's staged 32 x (32 + 32) output tile
+constexpr int BAND_SLOTS = 4;   // slabs whose pass-C' inputs a workgroup holds in LDS at once
+struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
+  int bimg, tww, frag, prow, stg, total;
+};
+TB_HD int band_al16(int b) { return (b + 15) & ~15; }
+TB_HD int band_vt(const BandGeo& g) { return 2 * g.KS <= 32 ? 1 : 2; }  // 32-row tiles of V
+TB_HD int band_kv(const BandGeo& g) { return g.KW + 1 + (g.KS - g.NDk); }
+TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
+  (void)D;
+  const int npm = g.KS - g.NDk;
+  BandInvCarve c;
+  c.bimg = 0;                                         // [2 NDk][NCOL] band rows of the synthesis table
+  c.tww = band_al16(c.bimg + 2 * g.NDk * g.NCOL * 4); // [W] twiddles
+  c.frag = band_al16(c.tww + W * 8);                  // [SLOTS][VT KV 64] V-product fragments
+  c.prow = band_al16(c.frag + BAND_SLOTS * band_vt(g) * band_kv(g) * 64 * 4);  // [SLOTS][2 npm][NCOL]
+  c.stg = band_al16(c.prow + BAND_SLOTS * 2 * npm * g.NCOL * 4);  // [4 waves][32][BAND_STG_P] staging
+  c.total = band_al16(c.stg + 4 * 32 * BAND_STG_P * 4);
+  return c;
+}
 
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels
 struct BandWs {
-  size_t off_P, off_AB, off_pts, total;
+  size_t off_P, off_AB, off_pts, off_mmp, off_m2f, total;
 };
 TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   BandWs w;
@@ -98,33 +136,11 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   w.off_AB = (size_t)bcn * H * g.ncol * 8;
   w.off_AB = (w.off_AB + 255) & ~(size_t)255;
   w.off_pts = w.off_AB + (size_t)bcn * (g.KH + 1) * g.ncol * 16;
-  w.total = w.off_pts + (size_t)bcn * BAND_MAX_PTS * 8;
+  w.off_mmp = w.off_pts + (size_t)bcn * BAND_MAX_PTS * 8;
+  w.off_m2f = w.off_mmp + (size_t)bcn * H * 32 * 8;  // (min, max) per (slab, 32-row tile), W <= 1024
+  w.off_m2f = (w.off_m2f + 255) & ~(size_t)255;
+  w.total = w.off_m2f + (size_t)bcn * H * band_vt(g) * band_kv(g) * 64 * 4;
   return w;
-}
-
-// LDS bytes of the two slab kernels
-TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
-  const int P = (D & 1) ? D : D + 1;
-  const int KSd = (D / 2 + 1 + 3) / 4, NT2 = g.NDk <= 16 ? 1 : 2;
-  return (size_t)(BAND_ROWS_A * P + 8) * 4 + (size_t)g.NDk * (BAND_ROWS_A + 1) * 8 + (size_t)W * 8 +
-         (size_t)NT2 * KSd * 128 * 4;
-}
-struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
-  int bimg, va, zb, awbw, tww, total;
-};
-TB_HD int band_al16(int b) { return (b + 15) & ~15; }
-TB_HD int band_vt(const BandGeo& g) { return 2 * g.KS <= 32 ? 1 : 2; }  // 32-row tiles of V
-TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W) {
-  const int NVR = 32 * band_vt(g);
-  const int KV = g.KW + 1 + (g.KS - g.NDk);
-  BandInvCarve c;
-  c.bimg = 0;                                                // [NVR][NCOL] synthesis table
-  c.va = band_al16(c.bimg + NVR * g.NCOL * 4);               // [NVR][2 KV + 1] V-product matrix
-  c.zb = band_al16(c.va + NVR * (2 * KV + 1) * 4);           // [ncol] Z_h
-  c.awbw = c.zb;
-  c.tww = band_al16(c.zb + g.ncol * 8);                      // [W] twiddles
-  c.total = band_al16(c.tww + W * 8);
-  return c;
 }
 
 // Launchers (kern_band.hip).  ncu = compute units (persistent slab grids).

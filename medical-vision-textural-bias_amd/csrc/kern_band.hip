@@ -99,8 +99,13 @@ __device__ __forceinline__ void chunk_copy_strided(float* xs, int P, const Chunk
   }
 }
 
-// NT2: 16-wide kd tiles (NDk <= 16 NT2); NI: stage-W items per thread ((KW+1) NDk <= 256 NI)
-template <int NT2, int NI>
+// NT2: 16-wide kd tiles (NDk <= 16 NT2); KWT: 16-wide kw tiles (KW < 16 KWT).
+// Per 64-row chunk each wave owns 16 rows:
+//   D product  R(row, kd) = sum_d s_d cos + i sum_d t_d sin      16x16x4 MFMA, folded over (d, D-d)
+//   W product  O(kw, kd) += sum_rows {cos, sin}(2 pi kw w / W) R  16x16x4 MFMA; the B operand is the
+//              D product's accumulator register j (its rows 4 (l/16) + j are the k index), so R never
+//              leaves the registers.  The four waves' O are summed once per slab through LDS.
+template <int NT2, int KWT>
 __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   const BandFwdArgs& a = kargs<BandFwdArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -110,36 +115,19 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   const int NDk = a.g.NDk, KW = a.g.KW, ncol = a.g.ncol;
   const int P = (D & 1) ? D : D + 1;
   const int Ld = D / 2 + 1;                 // folded d in [0, D/2]
-  const int KSd = (Ld + 3) / 4;             // 16x16x4 k-steps
-  float* X = reinterpret_cast<float*>(smem);                                    // [64][P] (+8 slack)
-  float2* Rb = reinterpret_cast<float2*>(X + BAND_ROWS_A * P + 8);              // [kd][65]
-  float2* twW = Rb + NDk * (BAND_ROWS_A + 1);                                   // (cos, -sin)(2 pi t / W)
-  float* Bt = reinterpret_cast<float*>(twW + W);                                // [NT2][KSd][2][64]
+  const int KSd = (Ld + 3) / 4;             // 16x16x4 k-steps of the D product
+  const int XN = BAND_ROWS_A * P + 8;
+  float* X = reinterpret_cast<float*>(smem);                     // [64][P] (+8 slack); O partials at slab end
+  float2* twW = reinterpret_cast<float2*>(X + XN);               // (cos, -sin)(2 pi t / W)
+  float* Bt = reinterpret_cast<float*>(twW + W);                 // [NT2][KSd][2][64]
   for (int t = tid; t < W; t += BAND_NT) twW[t] = ld2(a.pl.tw[1] + t);
-  // B fragments of the folded D product: lane l of k-step ks holds d = 4 ks + l/16, kd = 16 nt + l%16
-  for (int e = tid; e < NT2 * KSd * 128; e += BAND_NT) {
-    const int ln = e & 63, part = (e >> 6) & 1, ks = (e >> 7) % KSd, nt = (e >> 7) / KSd;
-    const int d = 4 * ks + (ln >> 4), kd = 16 * nt + (ln & 15);
-    float v = 0.f;
-    if (d < Ld && kd < NDk) {
-      const cf tw = a.pl.tw[2][(int)(((int64_t)kd * d) % D)];  // (cos, -sin)
-      v = part ? -tw.y : tw.x;
-    }
-    Bt[e] = v;
-  }
+  for (int t = tid; t < XN; t += BAND_NT) X[t] = 0.f;   // rows past W in a short last chunk stay finite
+  for (int e = tid; e < NT2 * KSd * 128; e += BAND_NT) Bt[e] = a.tbt[e];  // plan table (host double precision)
   const FastDiv fd = FastDiv::make(D);
-  const int nitems = (KW + 1) * NDk;
-  int ikw[NI], ikd[NI];
-#pragma unroll
-  for (int q = 0; q < NI; ++q) {
-    const int it = tid + q * BAND_NT;
-    ikw[q] = it < nitems ? it / NDk : -1;
-    ikd[q] = it < nitems ? it - (it / NDk) * NDk : 0;
-  }
   const int units = H * a.nbc;
   const int nch = (W + BAND_ROWS_A - 1) / BAND_ROWS_A;
   const bool contig = a.sw == D;
-  // (unit, chunk) sequence of this workgroup
+  const int diag = a.diag;
   int u = (int)blockIdx.x, c = 0;
   if (u >= units) return;
   auto xbase = [&](int uu) {
@@ -148,15 +136,23 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   };
   f32x4 pf[BAND_PF];
   ChunkSrc cs = chunk_src(xbase(u), a.sw, 0, W < BAND_ROWS_A ? W : BAND_ROWS_A, D);
-  const int diag = a.diag;
   if (contig) chunk_load(pf, cs, tid);
-  float2 Ac[NI], As[NI];
+  // O accumulators: [cos/sin][re/im][kw tile][kd tile]
+  f32x4 oacc[2][2][KWT][NT2];
 #pragma unroll
-  for (int q = 0; q < NI; ++q) Ac[q] = As[q] = make_float2(0.f, 0.f);
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int kt = 0; kt < KWT; ++kt)
+#pragma unroll
+        for (int nt = 0; nt < NT2; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) oacc[m][r][kt][nt][j] = 0.f;
   const int rbase = 16 * wv;  // this wave's 16 rows of the chunk
+  __syncthreads();            // X zeroed before the first chunk lands
   for (;;) {
     const int w0 = c * BAND_ROWS_A;
-    const int nr = (W - w0) < BAND_ROWS_A ? (W - w0) : BAND_ROWS_A;
     const float* xs = X;
     if (diag & 2)
       xs = X;
@@ -164,81 +160,111 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
       xs = chunk_store(X, pf, cs, D, fd, tid);
     else
       chunk_copy_strided(X, P, cs, a.sw, D, fd, tid);
-    __syncthreads();  // xs ready; every lane is past the previous chunk's W stage (Rb free)
-    // next (unit, chunk): its loads fly while this chunk is computed
+    __syncthreads();  // the chunk is in LDS
     int un = u, cn = c + 1;
     if (cn == nch) { cn = 0; un = u + (int)gridDim.x; }
-    if (un < units) {
+    if (un < units) {  // next (unit, chunk): its loads fly while this chunk is computed
       const int w0n = cn * BAND_ROWS_A;
       cs = chunk_src(xbase(un), a.sw, w0n, (W - w0n) < BAND_ROWS_A ? (W - w0n) : BAND_ROWS_A, D);
       if (contig && !(diag & 1)) chunk_load(pf, cs, tid);
     }
-    // D stage on the matrix cores: R(row, kd) = sum_d s_d cos + i sum_d t_d sin (folded over d, D - d)
+    f32x4 accc[NT2], accs[NT2];
+#pragma unroll
+    for (int nt = 0; nt < NT2; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accc[nt][j] = accs[nt][j] = 0.f;
     if (!(diag & 4)) {
       const float* row = xs + (rbase + l15) * P;
-      f32x4 accc[NT2], accs[NT2];
+      for (int k0 = 0; k0 < KSd; k0 += 4) {
+        float sv[4], tv[4];
 #pragma unroll
-      for (int nt = 0; nt < NT2; ++nt)
+        for (int q = 0; q < 4; ++q) {  // all LDS reads of 4 k-steps first
+          const int d = 4 * (k0 + q) + l4;
+          const bool has = d < Ld;
+          const bool pair = d >= 1 && 2 * d < D;
+          const float xa = has ? row[d] : 0.f;
+          const float xm = pair ? row[D - d] : 0.f;
+          sv[q] = xa + xm;
+          tv[q] = pair ? xm - xa : 0.f;
+        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) accc[nt][j] = accs[nt][j] = 0.f;
-      for (int ks = 0; ks < KSd; ++ks) {
-        const int d = 4 * ks + l4;
-        const bool has = d < Ld;
-        const bool pair = d >= 1 && 2 * d < D;
-        const float xa = has ? row[d] : 0.f;
-        const float xm = pair ? row[D - d] : 0.f;
-        const float sv = xa + xm, tv = pair ? xm - xa : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          if (k0 + q >= KSd) break;
 #pragma unroll
-        for (int nt = 0; nt < NT2; ++nt) {
-          const float* bt = Bt + ((nt * KSd + ks) * 2) * 64 + lane;
-          accc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv, bt[0], accc[nt], 0, 0, 0);
-          accs[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv, bt[64], accs[nt], 0, 0, 0);
+          for (int nt = 0; nt < NT2; ++nt) {
+            const float* bt = Bt + ((nt * KSd + k0 + q) * 2) * 64 + lane;
+            accc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv[q], bt[0], accc[nt], 0, 0, 0);
+            accs[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv[q], bt[64], accs[nt], 0, 0, 0);
+          }
         }
       }
-      // lane holds rows rbase + 4 (l/16) + j of kd = 16 nt + l%16
+    }
+    __syncthreads();  // every wave is done reading the chunk in LDS
+    if (!(diag & 8)) {
+      // W product: rows w = w0 + rbase + 4 (l/16) + j of this wave; rows >= W weigh 0
+      const int wl = w0 + rbase + 4 * l4;
 #pragma unroll
-      for (int nt = 0; nt < NT2; ++nt) {
-        const int kd = 16 * nt + l15;
-        if (kd < NDk)
+      for (int kt = 0; kt < KWT; ++kt) {
+        const int kw = 16 * kt + l15;
+        int t = (int)(((int64_t)kw * wl) % W);
+        const int step = kw % W;
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            Rb[kd * (BAND_ROWS_A + 1) + rbase + 4 * l4 + j] = make_float2(accc[nt][j], accs[nt][j]);
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = wl + j < W && kw <= KW;
+          const float2 tw = twW[t];
+          const float ca = ok ? tw.x : 0.f, sa = ok ? -tw.y : 0.f;
+#pragma unroll
+          for (int nt = 0; nt < NT2; ++nt) {
+            oacc[0][0][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca, accc[nt][j], oacc[0][0][kt][nt], 0, 0, 0);
+            oacc[0][1][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca, accs[nt][j], oacc[0][1][kt][nt], 0, 0, 0);
+            oacc[1][0][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sa, accc[nt][j], oacc[1][0][kt][nt], 0, 0, 0);
+            oacc[1][1][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sa, accs[nt][j], oacc[1][1][kt][nt], 0, 0, 0);
+          }
+          t += step;
+          t = t >= W ? t - W : t;
+        }
       }
     }
-    __syncthreads();  // Rb ready
-    // W stage: per (kw >= 0, kd): Ac += R_w cos, As += R_w sin (theta = 2 pi kw w / W)
+    if (c == nch - 1) {
+      // slab done: the four waves' O through LDS (X is free until the next chunk is stored)
+      float* Ob = X;  // [wave][m][r][kt][nt][64 lanes][4]
+      constexpr int NB = 2 * 2 * KWT * NT2;
 #pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (ikw[q] < 0 || (diag & 8)) continue;
-      const int kw = ikw[q];
-      const float2* Rk = Rb + ikd[q] * (BAND_ROWS_A + 1);
-      int t = (int)(((int64_t)kw * w0) % W);
-      float2 ac = Ac[q], as = As[q];
-#pragma unroll 4
-      for (int i = 0; i < nr; ++i) {
-        const float2 r = Rk[i];
-        const float2 tw = twW[t];
-        ac.x = fmaf(r.x, tw.x, ac.x);
-        ac.y = fmaf(r.y, tw.x, ac.y);
-        as.x = fmaf(r.x, -tw.y, as.x);
-        as.y = fmaf(r.y, -tw.y, as.y);
-        t += kw;
-        t = t >= W ? t - W : t;
-      }
-      Ac[q] = ac;
-      As[q] = as;
-    }
-    if (c == nch - 1) {  // P(kw) = Ac - i As, P(-kw) = Ac + i As
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int kt = 0; kt < KWT; ++kt)
+#pragma unroll
+            for (int nt = 0; nt < NT2; ++nt) {
+              const int blk = ((m * 2 + r) * KWT + kt) * NT2 + nt;
+              *reinterpret_cast<f32x4*>(Ob + ((wv * NB + blk) * 64 + lane) * 4) = oacc[m][r][kt][nt];
+              oacc[m][r][kt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+      __syncthreads();
       const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
       cf* Pb = a.P + ((int64_t)bc * H + h) * ncol;
+      for (int it = tid; it < (KW + 1) * NDk; it += BAND_NT) {
+        const int kw = it / NDk, kd = it - kw * NDk;
+        const int kt = kw >> 4, nt = kd >> 4;
+        // C layout: lane = 16 (row / 4) + col, register = row % 4 (row = kw % 16, col = kd % 16)
+        const int ln = 16 * ((kw & 15) >> 2) + (kd & 15), rg = kw & 3;
+        float o[2][2];
 #pragma unroll
-      for (int q = 0; q < NI; ++q) {
-        if (ikw[q] < 0) continue;
-        const int kw = ikw[q], kd = ikd[q];
-        Pb[(KW + kw) * NDk + kd] = mk(Ac[q].x + As[q].y, Ac[q].y - As[q].x);
-        if (kw > 0) Pb[(KW - kw) * NDk + kd] = mk(Ac[q].x - As[q].y, Ac[q].y + As[q].x);
-        Ac[q] = As[q] = make_float2(0.f, 0.f);
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int blk = ((m * 2 + r) * KWT + kt) * NT2 + nt;
+            float sum = 0.f;
+#pragma unroll
+            for (int w_ = 0; w_ < 4; ++w_) sum += Ob[((w_ * NB + blk) * 64 + ln) * 4 + rg];
+            o[m][r] = sum;
+          }
+        // P(kw) = Ac - i As, P(-kw) = Ac + i As
+        Pb[(KW + kw) * NDk + kd] = mk(o[0][0] + o[1][1], o[0][1] - o[1][0]);
+        if (kw > 0) Pb[(KW - kw) * NDk + kd] = mk(o[0][0] - o[1][1], o[0][1] + o[1][0]);
       }
+      __syncthreads();  // Ob (X) read before the next chunk is stored
     }
     if (un >= units) break;
     u = un;
@@ -308,144 +334,160 @@ __global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
   }
 }
 
+// ----------------------------------------------------------------------------- pass B2'
+// Z_h(col) = A_0 + sum_kh>=1 (A cos + i B sin), theta = 2 pi kh h / H, for every slab h: lanes =
+// columns (AB loaded once per lane), waves = slabs (twiddles wave-uniform).  Written over P.
+__global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
+  // One slab (bc, h) per wave: Z_h(col) = A_0 + sum_kh>=1 (A cos + i B sin), then the slab's
+  // V-product matrix M2T(v, k) written in MFMA A-fragment order [vt][ks][64 lanes], so that pass C'
+  // loads each k-step's fragment as one coalesced 256-B read:
+  //   rows v = 2 kd + (re, im): Vr = sum_kw (Ar cos - Bi sin), Vi = sum_kw (Ai cos + Br sin),
+  //     A/B = Z(kw) +/- Z(-kw), scaled by the C2R weight wt(kd) / N;
+  //   rows 2 (NDk + j) + (re, im): the out-of-box point j, ph_j = c_j e^{+2 pi i kh_j h / H} wt / N,
+  //     on its own k-step KW + 1 + j.
+  const BandMidArgs& a = kargs<BandMidArgs>();
+  __shared__ float2 zs[4][BAND_MAX_ZCOL];
+  __shared__ float2 phs[4][BAND_MAX_PTS];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.pl.H, D = a.pl.D, KH = a.g.KH, KW = a.g.KW, NDk = a.g.NDk, ncol = a.g.ncol;
+  const int npm = a.g.KS - NDk, KV = KW + 1 + npm, VT = band_vt(a.g);
+  const int u = (int)blockIdx.x * 4 + wv;
+  if (u >= H * a.nbc) return;
+  const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
+  const int s = (a.cofs + bcl) / a.C;
+  const float4* ABb = a.AB + (int64_t)bc * (KH + 1) * ncol;
+  for (int col = lane; col < ncol; col += 64) {
+    const float4 a0 = ABb[col];
+    float zx = a0.x, zy = a0.y;
+    int t = 0;
+    for (int k0 = 1; k0 <= KH; k0 += 4) {
+      float4 ab[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (k0 + q <= KH) ab[q] = ABb[(int64_t)(k0 + q) * ncol + col];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (k0 + q > KH) break;
+        t += h;
+        t = t >= H ? t - H : t;
+        const cf tw = a.pl.tw[0][t];  // (cos, -sin), wave-uniform
+        zx = fmaf(ab[q].x, tw.x, fmaf(ab[q].w, tw.y, zx));   // - B.y sin
+        zy = fmaf(ab[q].y, tw.x, fmaf(-ab[q].z, tw.y, zy));  // + B.x sin
+      }
+    }
+    zs[wv][col] = make_float2(zx, zy);
+  }
+  const BandSamplePts& sp = a.sp[s];
+  if (lane < BAND_MAX_PTS) {
+    float2 v = make_float2(0.f, 0.f);
+    if (lane < sp.n && lane < npm) {
+      const cf c = a.pts[(int64_t)bc * BAND_MAX_PTS + lane];
+      const cf tw = a.pl.tw[0][(int)(((int64_t)sp.p[lane].kh * h) % H)];
+      const float wt = ((sp.p[lane].kd == 0 || 2 * sp.p[lane].kd == D) ? 1.f : 2.f) * a.scale;
+      v = make_float2((c.x * tw.x + c.y * tw.y) * wt, (c.y * tw.x - c.x * tw.y) * wt);
+    }
+    phs[wv][lane] = v;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+  const float2* Zb = zs[wv];
+  const int nrv = 2 * (NDk + npm);
+  float* F = a.M2F + (int64_t)u * VT * KV * 64;
+  for (int vt = 0; vt < VT; ++vt)
+    for (int ks = 0; ks < KV; ++ks) {
+      const int r = 32 * vt + (lane & 31), sn = lane >> 5;
+      const int im = r & 1, kd = r >> 1;
+      float v = 0.f;
+      if (r < nrv) {
+        if (kd < NDk) {
+          if (ks <= KW) {
+            const float2 zp = Zb[(KW + ks) * NDk + kd];
+            const float2 zm = ks > 0 ? Zb[(KW - ks) * NDk + kd] : make_float2(0.f, 0.f);
+            const float ax = zp.x + zm.x, ay = zp.y + zm.y;
+            const float bx = ks > 0 ? zp.x - zm.x : 0.f, by = ks > 0 ? zp.y - zm.y : 0.f;
+            const float wt = ((kd == 0 || 2 * kd == D) ? 1.f : 2.f) * a.scale;
+            v = (im ? (sn ? bx : ay) : (sn ? -by : ax)) * wt;
+          }
+        } else if (ks == KW + 1 + (kd - NDk)) {
+          const float2 c = phs[wv][kd - NDk];
+          v = im ? (sn ? c.x : c.y) : (sn ? -c.y : c.x);
+        }
+      }
+      F[((int64_t)vt * KV + ks) * 64 + lane] = v;
+    }
+}
+
 // ----------------------------------------------------------------------------- pass C'
-// Per (bc, h) slab, all on the matrix cores after a small VALU prologue:
-//   Z_h(kw, kd)  = A_0 + sum_kh>=1 (A cos + i B sin)           (VALU; AB from pass B')
-//   V^T(v, w)    = M2T(v, k) . CS(k, w)                        (MFMA 32x32x2; v = 2 kd + re/im and
-//                  two rows per out-of-box point, k = (kw, cos/sin) terms; w on the lane)
-//   Y^T(n, w)    = B^T(n, v) . V^T(v, w)                       (MFMA, V^T straight from the
-//                  accumulators: the k order of each step is the accumulator's row pair
-//                  (rho(s), rho(s) + 4), the same permutation indexes the B table)
-// so each lane ends with 4 consecutive output columns of one image row: 16-B stores.
+// Per (bc, h) slab, on the matrix cores after a small prologue:
+//   V^T(v, w)  = M2T(v, k) . CS(k, w)       MFMA 32x32x2; v = 2 kd + (re, im) and two rows per
+//                out-of-box point; k = (kw, cos/sin) terms and one pair per point; w on the lane
+//   E(d, w)    = Bc^T(d, v_re) . V^T(v_re, w),   O(d, w) = Bs^T(d, v_im) . V^T(v_im, w)
+//                MFMA with V^T straight from the accumulators: accumulator register s holds the
+//                row pair (rho(s), rho(s) + 4) -- both real parts when s % 4 is even, both
+//                imaginary parts when odd -- so it is the B operand of one k-step as it stands
+//   y[w][d] = E - O,  y[w][D - d] = E + O   for d in [0, D/2]  (the C2R folded over d <-> D - d)
+// Each lane ends with 4 consecutive columns of one image row for both halves: 16-B stores.
 __device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
 
 template <int VT>  // 32-row tiles of V (2 (NDk + points) <= 32 VT)
 __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
+  // The workgroup takes its slabs in batches of BAND_SLOTS: the batch's inputs (V-product
+  // fragments from pass B2', the samples' point rows of the synthesis table) are loaded into LDS
+  // first, so that the (slab, 32-row tile) units the four waves then work through issue only
+  // stores -- no load waits behind the CU's queue of outgoing image rows.
   const BandInvArgs& a = kargs<BandInvArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float red[2 * BAND_NT / 64];
   const int tid = (int)threadIdx.x, lane = tid & 63, hl = lane >> 5, l31 = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
-  const int NDk = a.g.NDk, KW = a.g.KW, KH = a.g.KH, ncol = a.g.ncol, NCOL = a.g.NCOL;
+  const int NDk = a.g.NDk, KW = a.g.KW, NCOL = a.g.NCOL;
   const int npm = a.g.KS - NDk;        // point rows of the launch (max over its samples)
   const int KV = KW + 1 + npm;         // k-steps of the V product
-  const int MP = 2 * KV + 1;           // M2T pitch
-  const BandInvCarve cv = band_inv_carve(a.g, W);
-  float* Bimg = reinterpret_cast<float*>(smem + cv.bimg);  // [32 VT][NCOL]
-  float* M2T = reinterpret_cast<float*>(smem + cv.va);     // [32 VT][MP]
-  float2* Zb = reinterpret_cast<float2*>(smem + cv.zb);    // [ncol]
+  const int Dh = D / 2 + 1;            // folded output columns d in [0, D/2]
+  const int nrv = 2 * (NDk + npm);     // used rows of V / the synthesis table
+  const int fsz = VT * KV * 64;        // floats of one slab's fragments
+  const int psz = 2 * npm * NCOL;      // floats of one slab's point rows
+  const BandInvCarve cv = band_inv_carve(a.g, W, D);
+  float* Bimg = reinterpret_cast<float*>(smem + cv.bimg);  // [2 NDk][NCOL]: even rows cos, odd rows sin
   float2* twW = reinterpret_cast<float2*>(smem + cv.tww);  // (cos, -sin)(2 pi t / W)
-  const cf* twD = a.pl.tw[2];
+  float* Fs = reinterpret_cast<float*>(smem + cv.frag);    // [BAND_SLOTS][fsz]
+  float* Ps = reinterpret_cast<float*>(smem + cv.prow);    // [BAND_SLOTS][psz]
+  float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 32 * BAND_STG_P;  // this wave's 32 x 32 tile
   for (int t = tid; t < W; t += BAND_NT) twW[t] = ld2(a.pl.tw[1] + t);
-  // synthesis table rows v: 2k -> cos(2 pi kd_k n / D), 2k + 1 -> -sin; 0 for n >= D and unused rows
-  for (int e = tid; e < 32 * VT * NCOL; e += BAND_NT) {
-    const int r = e / NCOL, n = e - r * NCOL, k = r >> 1;
-    float v = 0.f;
-    if (k < NDk && n < D) {
-      const cf tw = twD[(int)(((int64_t)k * n) % D)];
-      v = (r & 1) ? tw.y : tw.x;
-    }
-    Bimg[e] = v;
-  }
-  const int units = H * a.nbc;
-  const int ntw = (W + 31) / 32;     // 32-row tiles of the slab
-  const int ntn = NCOL / 32;         // 32-column tiles of the output row
-  const int ycols = D + a.ypad;
+  for (int e = tid; e < 2 * NDk * NCOL; e += BAND_NT) Bimg[e] = a.tds[e];
+  const int ntw = (W + 31) / 32;     // 32-row tiles of a slab
+  const int nslab = H * a.nbc;
+  const int ntn = NCOL / 32;         // 32-column tiles of the folded row
+  const int ypad = a.ypad;
   const int diag = a.diag;
-  int cur_s = -1;
-  float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  for (int u = (int)blockIdx.x; u < units; u += (int)gridDim.x) {
-    const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
-    const int s = (a.cofs + bcl) / a.C;
-    const BandSamplePts& sp = a.sp[s];
-    __syncthreads();  // the previous unit is done with Zb / M2T / the point rows of Bimg
-    if (s != cur_s && npm > 0) {
-      for (int e = tid; e < 2 * npm * NCOL; e += BAND_NT) {
+  const bool mal = ((D - 3) & 3) == 0;  // mirrored 4-column groups start 16-B aligned
+  for (int k0 = 0;; k0 += BAND_SLOTS) {
+    const int u0 = (int)blockIdx.x + k0 * (int)gridDim.x;
+    if (u0 >= nslab) break;
+    int nb = 0;
+    while (nb < BAND_SLOTS && u0 + nb * (int)gridDim.x < nslab) ++nb;
+    __syncthreads();  // the previous batch is done with Fs / Ps
+    for (int i = 0; i < nb; ++i) {
+      const int slab = u0 + i * (int)gridDim.x;
+      const float* F = a.M2F + (int64_t)slab * fsz;
+      for (int e = tid; e < fsz; e += BAND_NT) Fs[i * fsz + e] = F[e];
+      const BandSamplePts& sp = a.sp[(a.cofs + slab / H) / a.C];
+      for (int e = tid; e < psz; e += BAND_NT) {
         const int r = e / NCOL, n = e - r * NCOL, j = r >> 1;
-        float v = 0.f;
-        if (j < sp.n && n < D) {
-          const cf tw = twD[(int)(((int64_t)sp.p[j].kd * n) % D)];
-          v = (r & 1) ? tw.y : tw.x;
-        }
-        Bimg[(2 * NDk + r) * NCOL + n] = v;
-      }
-    }
-    cur_s = s;
-    // Z_h(col) = A_0 + sum_kh>=1 (A cos + i B sin), theta = 2 pi kh h / H; loads issued 4 at a time
-    const float4* ABb = a.AB + (int64_t)bc * (KH + 1) * ncol;
-    for (int col = (diag & 1) ? ncol : tid; col < ncol; col += BAND_NT) {
-      const float4 a0 = ABb[col];
-      float zx = a0.x, zy = a0.y;
-      int t = 0;
-      for (int k0 = 1; k0 <= KH; k0 += 4) {
-        float4 ab[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (k0 + q <= KH) ab[q] = ABb[(int64_t)(k0 + q) * ncol + col];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (k0 + q > KH) break;
-          t += h;
-          t = t >= H ? t - H : t;
-          const cf tw = a.pl.tw[0][t];  // (cos, -sin)
-          zx = fmaf(ab[q].x, tw.x, fmaf(ab[q].w, tw.y, zx));   // - B.y sin
-          zy = fmaf(ab[q].y, tw.x, fmaf(-ab[q].z, tw.y, zy));  // + B.x sin
-        }
-      }
-      Zb[col] = make_float2(zx, zy);
-    }
-    // the sample's point coefficients rotated to this slab: ph_j = c_j e^{+2 pi i kh_j h / H} wt / N
-    float2 ph[BAND_MAX_PTS];
-#pragma unroll
-    for (int j = 0; j < BAND_MAX_PTS; ++j) {
-      ph[j] = make_float2(0.f, 0.f);
-      if (j < sp.n && j < npm) {
-        const cf c = a.pts[(int64_t)bc * BAND_MAX_PTS + j];
-        const cf tw = a.pl.tw[0][(int)(((int64_t)sp.p[j].kh * h) % H)];
-        const float wt = ((sp.p[j].kd == 0 || 2 * sp.p[j].kd == D) ? 1.f : 2.f) * a.scale;
-        ph[j] = make_float2((c.x * tw.x + c.y * tw.y) * wt, (c.y * tw.x - c.x * tw.y) * wt);
+        Ps[i * psz + e] = j < sp.n ? a.tds[(2 * sp.p[j].kd + (r & 1)) * NCOL + n] : 0.f;
       }
     }
     __syncthreads();
-    // M2T(v, k): Vr = sum (Ar cos - Bi sin), Vi = sum (Ai cos + Br sin) over kw; points: ph e^{+i phi}
-    for (int e = (diag & 2) ? 32 * VT * 2 * KV : tid; e < 32 * VT * 2 * KV; e += BAND_NT) {
-      const int r = e / (2 * KV), k = e - r * (2 * KV);
-      const int ks = k >> 1, sn = k & 1, im = r & 1, kd = r >> 1;
-      float v = 0.f;
-      if (kd < NDk) {
-        if (ks <= KW) {
-          const float2 zp = Zb[(KW + ks) * NDk + kd];
-          float2 A = zp, B = make_float2(0.f, 0.f);
-          if (ks > 0) {
-            const float2 zm = Zb[(KW - ks) * NDk + kd];
-            A = make_float2(zp.x + zm.x, zp.y + zm.y);
-            B = make_float2(zp.x - zm.x, zp.y - zm.y);
-          }
-          const float wt = ((kd == 0 || 2 * kd == D) ? 1.f : 2.f) * a.scale;
-          v = (im ? (sn ? B.x : A.y) : (sn ? -B.y : A.x)) * wt;
-        }
-      } else if (kd - NDk < npm) {
-        const int j = kd - NDk;
-        if (ks == KW + 1 + j) {
-          float2 c = make_float2(0.f, 0.f);
-#pragma unroll
-          for (int jj = 0; jj < BAND_MAX_PTS; ++jj)
-            if (jj == j) c = ph[jj];
-          v = im ? (sn ? c.x : c.y) : (sn ? -c.y : c.x);
-        }
-      }
-      M2T[r * MP + k] = v;
-    }
-    __syncthreads();
-    const float* afr = M2T + l31 * MP + hl;  // A fragment of k-step ks, tile vt: afr[32 vt MP + 2 ks]
-    float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
-    const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
-    for (int tw_ = wv; tw_ < ntw; tw_ += 4) {
+    for (int un = wv; un < nb * ntw; un += 4) {
+      const int slot = un / ntw, tw_ = un - slot * ntw;
+      const int slab = u0 + slot * (int)gridDim.x;
+      const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
+      const BandSamplePts& sp = a.sp[(a.cofs + bcl) / a.C];
+      const float* F = Fs + slot * fsz + lane;  // fragment of (vt, ks): F[(vt KV + ks) 64]
+      const float* Pr = Ps + slot * psz;
       const int w = 32 * tw_ + l31;
-      const bool wok = w < W;
       const int wm = w % W;
-      // V^T(:, w) for this lane's row w
       f32x16 vacc[VT];
 #pragma unroll
       for (int vt = 0; vt < VT; ++vt)
@@ -457,7 +499,7 @@ __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
         const float b = hl ? -c.y : c.x;
 #pragma unroll
         for (int vt = 0; vt < VT; ++vt)
-          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(afr[32 * vt * MP + 2 * ks], b, vacc[vt], 0, 0, 0);
+          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(F[(vt * KV + ks) * 64], b, vacc[vt], 0, 0, 0);
         t += wm;
         t = t >= W ? t - W : t;
       }
@@ -467,51 +509,149 @@ __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
         const float b = hl ? -c.y : c.x;
 #pragma unroll
         for (int vt = 0; vt < VT; ++vt)
-          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(afr[32 * vt * MP + 2 * (KW + 1 + j)], b, vacc[vt], 0, 0, 0);
+          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(F[(vt * KV + KW + 1 + j) * 64], b, vacc[vt], 0, 0, 0);
       }
-      float* yr = yb + (int64_t)w * a.sw;
+      float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
+      const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
+      float lo = 3.402823466e38f, hi = -3.402823466e38f;
       for (int nt = 0; nt < ntn; ++nt) {
-        f32x16 y;
+        f32x16 ye, yo;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) y[j] = 0.f;
-        const float* bb = Bimg + (4 * hl) * NCOL + nt * 32 + l31;
+        for (int j = 0; j < 16; ++j) ye[j] = yo[j] = 0.f;
+        const int col = nt * 32 + l31;
         if (!(diag & 8))
 #pragma unroll
           for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
-            for (int sI = 0; sI < 16; ++sI)
-              y = __builtin_amdgcn_mfma_f32_32x32x2f32(bb[(32 * vt + acc_row(sI)) * NCOL], vacc[vt][sI], y, 0, 0, 0);
-        if (!wok || (diag & 16)) continue;
+            for (int sI = 0; sI < 16; sI += 2) {  // even sI: real rows (E); sI + 1: imaginary rows (O)
+              if (32 * vt + acc_row(sI) >= nrv) break;  // both halves' rows past the used ones are zero
+              const int re = 32 * vt + acc_row(sI) + 4 * hl;  // this lane's (real) row of the step
+              float be = 0.f, bo = 0.f;
+              if (re < 2 * NDk) {
+                be = Bimg[re * NCOL + col];
+                bo = Bimg[(re + 1) * NCOL + col];
+              } else if (re < nrv) {
+                be = Pr[(re - 2 * NDk) * NCOL + col];
+                bo = Pr[(re - 2 * NDk + 1) * NCOL + col];
+              }
+              ye = __builtin_amdgcn_mfma_f32_32x32x2f32(be, vacc[vt][sI], ye, 0, 0, 0);
+              yo = __builtin_amdgcn_mfma_f32_32x32x2f32(bo, vacc[vt][sI + 1], yo, 0, 0, 0);
+            }
+        if (diag & 16) continue;
+        // y[w][d] = E - O (direct) and y[w][D - d] = E + O (mirror), staged [row][32 | 32] through
+        // LDS so that every store instruction writes whole 128-B row segments
+        const int c4 = lane & 7;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int n0 = nt * 32 + 8 * g + 4 * hl;
-          const float v0 = y[4 * g], v1 = y[4 * g + 1], v2 = y[4 * g + 2], v3 = y[4 * g + 3];
-          if (vec && n0 + 4 <= ycols) {
-            *reinterpret_cast<float4*>(yr + n0) = make_float4(v0, v1, v2, v3);
-          } else {
-            const float vv[4] = {v0, v1, v2, v3};
+          f32x4 dv, mv;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            dv[q] = ye[4 * g + q] - yo[4 * g + q];
+            mv[3 - q] = ye[4 * g + q] + yo[4 * g + q];
+          }
+          *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + 8 * g + 4 * hl) = dv;
+          *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + 32 + 28 - 8 * g - 4 * hl) = mv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int dbase = nt * 32 + 4 * c4, dmir = nt * 32 + 31 - 4 * c4;
+        // the mirror of d = 0 is column D: the first U-Net pad column, written as 0 in the same vector
+        const bool padlane = nt == 0 && c4 == 7 && ypad > 0;
+        int nd = 0, nm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          nd += dbase + q < Dh ? 1 : 0;
+          const int d = dmir - q;
+          nm += ((d >= 1 && 2 * d < D && d < Dh) || (padlane && d == 0)) ? 1 : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = (lane >> 3) + 8 * k;
+          const int wr = 32 * tw_ + r;
+          if (wr >= W) continue;
+          const f32x4 dv = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 4 * c4);
+          f32x4 mv = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 32 + 4 * c4);
+          if (padlane) mv[3] = 0.f;  // column D
+          float* yrr = yb + (int64_t)wr * a.sw;
+          if (vec && nd == 4) {
+            *reinterpret_cast<f32x4*>(yrr + dbase) = dv;
+            lo = fminf(lo, fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])));
+            hi = fmaxf(hi, fmaxf(fmaxf(dv[0], dv[1]), fmaxf(dv[2], dv[3])));
+          } else if (nd > 0) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-              if (n0 + q < ycols) yr[n0 + q] = vv[q];
+              if (q < nd) {
+                yrr[dbase + q] = dv[q];
+                lo = fminf(lo, dv[q]);
+                hi = fmaxf(hi, dv[q]);
+              }
           }
-          const float vv[4] = {v0, v1, v2, v3};
+          if (vec && mal && nm == 4) {
+            *reinterpret_cast<f32x4*>(yrr + D - dmir) = mv;
+            const float m3 = padlane ? mv[2] : mv[3];  // the pad zero is not an image value
+            lo = fminf(lo, fminf(fminf(mv[0], mv[1]), fminf(mv[2], m3)));
+            hi = fmaxf(hi, fmaxf(fmaxf(mv[0], mv[1]), fmaxf(mv[2], m3)));
+          } else if (nm > 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (n0 + q < D) {
-              lo = fminf(lo, vv[q]);
-              hi = fmaxf(hi, vv[q]);
+            for (int q = 0; q < 4; ++q) {
+              const int d = dmir - q;  // mv[q] is the value at column D - dmir + q = D - d
+              if (d >= 1 && 2 * d < D && d < Dh) {
+                yrr[D - d] = mv[q];
+                lo = fminf(lo, mv[q]);
+                hi = fmaxf(hi, mv[q]);
+              } else if (padlane && d == 0) {
+                yrr[D] = 0.f;
+              }
             }
+          }
+          if (padlane) {  // the rest of the zero D-padding: columns D + 1 .. D + ypad - 1
+            int p = 1;
+            for (; p < ypad && ((D + p) & 3); ++p) yrr[D + p] = 0.f;
+            if (vec)
+              for (; p + 4 <= ypad; p += 4) *reinterpret_cast<f32x4*>(yrr + D + p) = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (; p < ypad; ++p) yrr[D + p] = 0.f;
+          }
         }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (a.mm) {  // per-unit partial (reduced per sample by k_band_minmax)
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane == 0) a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
       }
     }
-    // flush the running min/max when the next unit belongs to another sample (or there is none)
-    const int un = u + (int)gridDim.x;
-    const int b = bc / a.C;
-    if (a.mm && (un >= units || (a.bc0 + un / H) / a.C != b)) {
-      block_minmax_atomic<BAND_NT>(lo, hi, red, a.mm + 2 * b);
-      lo = 3.402823466e38f;
-      hi = -3.402823466e38f;
+  }
+}
+
+// per-sample keys of the slab partials: one workgroup per sample
+__global__ __launch_bounds__(256) void k_band_minmax(const float2* __restrict__ mmp, uint32_t* __restrict__ mm, int bc0,
+                                                     int C, int H, int W) {
+  __shared__ float red[2 * 256 / 64];
+  const int b = (int)blockIdx.x;
+  const int ntw = (W + 31) / 32;
+  const int64_t n = (int64_t)C * H * ntw;  // one partial per (slab, 32-row tile)
+  const float2* p = mmp + (int64_t)b * C * H * ntw;
+  float lo = 3.402823466e38f, hi = -3.402823466e38f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const float2 v = p[i];
+    lo = fminf(lo, v.x);
+    hi = fmaxf(hi, v.y);
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wid] = lo;
+    red[4 + wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      lo = fminf(lo, red[w]);
+      hi = fmaxf(hi, red[4 + w]);
     }
+    const int sb = bc0 / C + b;
+    mm[2 * sb] = f2key(lo);
+    mm[2 * sb + 1] = f2key(hi);
   }
 }
 
@@ -556,9 +696,9 @@ int band_grid(int units, size_t lds, int ncu) {
   return units < g ? units : g;
 }
 
-template <int NT2, int NI>
+template <int NT2, int KWT>
 hipError_t launch_fwd_t(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
-  auto kern = k_band_fwd<NT2, NI>;
+  auto kern = k_band_fwd<NT2, KWT>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
   const int units = a.pl.H * a.nbc;
@@ -566,21 +706,13 @@ hipError_t launch_fwd_t(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t s
   return hipGetLastError();
 }
 
-template <int NT2>
-hipError_t launch_fwd_nt(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
-  const int items = (a.g.KW + 1) * a.g.NDk;
-  if (items <= BAND_NT) return launch_fwd_t<NT2, 1>(a, lds, ncu, st);
-  if (items <= 2 * BAND_NT) return launch_fwd_t<NT2, 2>(a, lds, ncu, st);
-  return launch_fwd_t<NT2, 4>(a, lds, ncu, st);
-}
-
 template <int VT>
 hipError_t launch_inv_t(const BandInvArgs& a, int ncu, hipStream_t st) {
-  const size_t lds = band_inv_carve(a.g, a.pl.W).total;
+  const size_t lds = band_inv_carve(a.g, a.pl.W, a.pl.D).total;
   auto kern = k_band_inv<VT>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
-  const int units = a.pl.H * a.nbc;
+  const int units = a.pl.H * a.nbc;  // slabs, taken in batches of BAND_SLOTS per workgroup
   hipLaunchKernelGGL(kern, dim3(band_grid(units, lds, ncu)), dim3(BAND_NT), lds, st, a);
   return hipGetLastError();
 }
@@ -589,18 +721,26 @@ hipError_t launch_inv_t(const BandInvArgs& a, int ncu, hipStream_t st) {
 
 hipError_t launch_band_fwd(const BandFwdArgs& a, int ncu, hipStream_t st) {
   const size_t lds = band_lds_fwd(a.g, a.pl.W, a.pl.D);
-  return a.g.NDk <= 16 ? launch_fwd_nt<1>(a, lds, ncu, st) : launch_fwd_nt<2>(a, lds, ncu, st);
+  const bool n1 = a.g.NDk <= 16, k1 = a.g.KW < 16;
+  if (n1) return k1 ? launch_fwd_t<1, 1>(a, lds, ncu, st) : launch_fwd_t<1, 2>(a, lds, ncu, st);
+  return k1 ? launch_fwd_t<2, 1>(a, lds, ncu, st) : launch_fwd_t<2, 2>(a, lds, ncu, st);
 }
 
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_band_mid, dim3((a.g.ncol + 63) / 64, a.g.KH + 1, a.nbc), dim3(BAND_NT), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4), dim3(BAND_NT), 0, st, a);
   return hipGetLastError();
 }
 
 
 
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
-  return 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
+  const hipError_t e = 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
+  if (e != hipSuccess || !a.mm) return e;
+  hipLaunchKernelGGL(k_band_minmax, dim3(a.nbc / a.C), dim3(256), 0, st, a.mmp, a.mm, a.bc0, a.C, a.pl.H, a.pl.W);
+  return hipGetLastError();
 }
 
 hipError_t launch_copy_pad(const CopyArgs& a, hipStream_t st) {

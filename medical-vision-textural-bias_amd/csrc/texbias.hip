@@ -209,6 +209,8 @@ struct tb_plan {
   bool ct_tile = false;  // H has a compile-time pass-B plan (kspace_ct.h)
   float2* tdf = nullptr; // band pass A': [D/2 + 1][NKP] (cos, sin)(2 pi kd d / D)
   int NKP = 0;
+  float* tds = nullptr;  // band pass C': [D/2 + 1][2][NCOLS] cos / sin(2 pi kd d / D), d < D/2 + 1, else 0
+  float* tbt = nullptr;  // band pass A': [2][KSd][2][64] B fragments of the folded D product
 };
 
 namespace {
@@ -328,6 +330,32 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
     }
     p->NKP = nkp;
   }
+  {  // folded synthesis table (pass C') and the D-product B fragments (pass A'), double precision
+    const int Dh = D / 2 + 1, ncols = 32 * ((Dh + 31) / 32), KSd = (Dh + 3) / 4;
+    std::vector<float> ts((size_t)Dh * 2 * ncols, 0.f), tb((size_t)2 * KSd * 2 * 64, 0.f);
+    for (int k = 0; k < Dh; ++k)
+      for (int d = 0; d < Dh; ++d) {
+        const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)k * d) % D) / (double)D;
+        ts[((size_t)k * 2) * ncols + d] = (float)std::cos(ang);
+        ts[((size_t)k * 2 + 1) * ncols + d] = (float)std::sin(ang);
+      }
+    for (int nt = 0; nt < 2; ++nt)
+      for (int ks = 0; ks < KSd; ++ks)
+        for (int part = 0; part < 2; ++part)
+          for (int ln = 0; ln < 64; ++ln) {
+            const int d = 4 * ks + (ln >> 4), kd = 16 * nt + (ln & 15);
+            if (d >= Dh || kd >= Dh) continue;
+            const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)kd * d) % D) / (double)D;
+            tb[(((size_t)nt * KSd + ks) * 2 + part) * 64 + ln] = (float)(part ? std::sin(ang) : std::cos(ang));
+          }
+    if (hipMalloc(reinterpret_cast<void**>(&p->tds), ts.size() * 4) != hipSuccess ||
+        hipMemcpy(p->tds, ts.data(), ts.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&p->tbt), tb.size() * 4) != hipSuccess ||
+        hipMemcpy(p->tbt, tb.data(), tb.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      tb_plan_destroy(p);
+      return hip_fail(hipGetLastError());
+    }
+  }
   p->rset_h = needs_all(p->host.ax[0]) ? RS_ALL : RS_SMALL;
   p->rset_wd = (needs_all(p->host.ax[1]) || needs_all(p->host.ax[2])) ? RS_ALL : RS_SMALL;
   *out = p;
@@ -338,13 +366,25 @@ int tb_plan_destroy(tb_plan* plan) {
   if (!plan) return TB_OK;
   if (plan->dmem) (void)hipFree(plan->dmem);
   if (plan->tdf) (void)hipFree(plan->tdf);
+  if (plan->tds) (void)hipFree(plan->tds);
+  if (plan->tbt) (void)hipFree(plan->tbt);
   delete plan;
   return TB_OK;
 }
 
 size_t tb_workspace_bytes(const tb_plan* plan, int bc) {
   if (!plan || bc < 0) return 0;
-  return (size_t)bc * plan->dev.H * plan->dev.W * (plan->dev.D / 2 + 1) * sizeof(cf);
+  const size_t spec = (size_t)bc * plan->dev.H * plan->dev.W * (plan->dev.D / 2 + 1) * sizeof(cf);
+  // the band passes' largest layout (band_plan() refuses boxes past these limits)
+  BandGeo g{};
+  g.KH = BAND_MAX_KH;
+  g.KW = 31;
+  g.NDk = BAND_MAX_NDK;
+  g.ncol = BAND_MAX_ZCOL;
+  g.KS = 32;
+  g.NCOL = 32 * ((plan->dev.D / 2 + 1 + 31) / 32);
+  const size_t band = band_ws(g, plan->dev.H, bc).total;
+  return spec > band ? spec : band;
 }
 
 int tb_plan_radices(const tb_plan* plan, int axis, int* radices) {
@@ -489,12 +529,13 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   g.NW = 2 * KW + 1;
   g.ncol = g.NW * g.NDk;
   g.KS = g.NDk + npt;
-  g.NCOL = 32 * ((D + y_pad + 31) / 32);
-  if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || (KW + 1) * g.NDk > 4 * BAND_NT) return false;
-  if (2 * g.KS > 64) return false;  // pass C' holds V in at most two 32-row MFMA tiles
+  g.NCOL = 32 * ((D / 2 + 1 + 31) / 32);
+  if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || KW >= 32 || KH > BAND_MAX_KH) return false;
+  if (g.ncol > BAND_MAX_ZCOL || W > 1024) return false;
+  if (2 * g.KS > 64 || g.KS > 32) return false;  // pass C' holds V in at most two 32-row MFMA tiles
   // worth it only when the box is a small part of the half spectrum
   if ((double)(2 * KH + 1) * g.ncol * 4.0 > (double)H * W * (D / 2 + 1)) return false;
-  if (band_lds_fwd(g, W, D) > 160000 || band_inv_carve(g, W).total > 160000) return false;
+  if (band_lds_fwd(g, W, D) > 160000 || band_inv_carve(g, W, D).total > 160000) return false;
   if (band_ws(g, H, bcn).total > ws_bytes) return false;
   return true;
 }
@@ -562,7 +603,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
   const double pbytes = (double)nbc * H * g.ncol * 8.0, abytes = (double)nbc * (g.KH + 1) * g.ncol * 16.0;
   {
     Timer t(0, st, (double)nbc * H * W * D * 4.0 + pbytes, "k_band_fwd");
-    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g, g_band_diag & 0xff};
+    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g, g_band_diag & 0xff, p->tbt};
     TB_HIP(tb::launch_band_fwd(fa, p->ncu, st));
   }
   {
@@ -573,6 +614,8 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ma.P = P;
     ma.AB = AB;
     ma.pts = pts;
+    ma.M2F = reinterpret_cast<float*>(ws + wl.off_m2f);
+    ma.scale = (float)(1.0 / ((double)H * (double)W * (double)D));
     ma.bc0 = bc0;
     ma.C = C;
     ma.cofs = 0;
@@ -589,6 +632,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     BandInvArgs ia;
     std::memset(&ia, 0, sizeof(ia));
     ia.pl = p->dev;
+    ia.M2F = reinterpret_cast<float*>(ws + wl.off_m2f);
     ia.AB = AB;
     ia.pts = pts;
     ia.y = y;
@@ -602,6 +646,8 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.nbc = nbc;
     ia.scale = (float)(1.0 / ((double)H * (double)W * (double)D));
     ia.mm = minmax;
+    ia.mmp = reinterpret_cast<float2*>(ws + wl.off_mmp);
+    ia.tds = p->tds;
     ia.g = g;
     ia.diag = (g_band_diag >> 8) & 0xff;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];

@@ -8,8 +8,9 @@ behaviour as the reference; the arithmetic runs in the texbias HIP kernels
 Tensors on the CPU are moved to the current HIP device for the filter and the
 result is returned on the caller's device; there is no CPU implementation --
 without a HIP device the filters raise.  For throughput use the batched
-device-side stage ``texbias.pipeline.BatchedKSpaceAugment`` after collation
-instead of per-sample calls inside DataLoader workers.
+device-side stage ``texbias.pipeline.FusedChain`` after collation instead of
+per-sample calls inside DataLoader workers.  The arithmetic goes through the
+``torch.ops.texbias.*`` custom operators (``texbias/ops.py``).
 
 Reference line numbers are cited per class (``filters_and_operators.py:N``).
 """
@@ -23,6 +24,7 @@ import numpy as np
 import torch
 
 from texbias import kprog as _K
+from texbias import ops as _ops  # registers torch.ops.texbias.*
 from texbias import runtime as _rt
 from texbias.shell import shell_coords as _shell_coords
 from texbias.transform_base import (MapTransform, Randomizable, RandomizableTransform, Transform,
@@ -62,7 +64,7 @@ def _kspace(img: torch.Tensor, n_dims: int, program: Sequence, pad: int = 0) -> 
     lead = x.shape[: x.dim() - n_dims]
     chans = int(np.prod(lead)) if len(lead) else 1
     xb = x.reshape((1, chans) + tuple(x.shape[x.dim() - n_dims:]))
-    y = _rt.kspace_filter(xb, n_dims, [list(program)], chans)
+    y, _ = torch.ops.texbias.kspace_filter(xb, n_dims, _ops.pack_programs([list(program)]), chans, 0)
     y = y.reshape(tuple(x.shape))
     return y if img.device == dev else y.to(img.device)
 

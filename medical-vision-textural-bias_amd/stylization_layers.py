@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from filters_and_operators import Fourier as _Fourier
 from filters_and_operators import RandKSpaceSpikeNoise
-from texbias import kprog as _K
+from texbias import ops as _ops  # noqa: F401 - registers torch.ops.texbias.*
 from texbias import runtime as _rt
 from texbias.unet import UNet
 
@@ -31,33 +31,6 @@ __all__ = ["Fourier", "GibbsNoiseLayer", "Gibbs_UNet", "spike_layer", "Spikes_UN
 
 class Fourier(_Fourier):
     """Full-spectrum helpers (:16-52), shared with filters_and_operators."""
-
-
-class _LayerFilter(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, img: torch.Tensor, alpha: torch.Tensor, spatial):
-        ctx.spatial = spatial
-        ctx.save_for_backward(alpha)
-        return _layer_apply(img, alpha, spatial)
-
-    @staticmethod
-    def backward(ctx, gy):
-        (alpha,) = ctx.saved_tensors
-        gx = _layer_apply(gy.contiguous(), alpha, ctx.spatial) if ctx.needs_input_grad[0] else None
-        ga = torch.zeros_like(alpha) if ctx.needs_input_grad[1] else None
-        return gx, ga, None
-
-
-def _layer_apply(img: torch.Tensor, alpha: torch.Tensor, spatial) -> torch.Tensor:
-    B = img.shape[0]
-    n_dims = img.dim() - 1
-    a = alpha.detach().reshape(-1)[:1].to(device=img.device, dtype=torch.float32).contiguous()
-    prog = [_K.layer_op(0.0, spatial, alpha_ptr=a.data_ptr())]
-    x = img if img.dtype == torch.float32 else img.float()
-    # `a` aliases the alpha buffer (or is a stream-ordered temporary): the caching allocator only
-    # hands its memory to work queued after this launch, so the kernel's read is safe.
-    y = _rt.kspace_filter(x.reshape((B, 1) + tuple(img.shape[1:])), n_dims, [prog] * B, 1)
-    return y.reshape(img.shape)
 
 
 class GibbsNoiseLayer(nn.Module, Fourier):
@@ -80,7 +53,7 @@ class GibbsNoiseLayer(nn.Module, Fourier):
     def forward(self, img: torch.Tensor) -> torch.Tensor:
         if img.device.type != "cuda":
             raise _rt.TexbiasError("GibbsNoiseLayer runs on a HIP device; move the model and input to cuda")
-        return _LayerFilter.apply(img, self.alpha, tuple(img.shape[1:]))
+        return torch.ops.texbias.gibbs_layer(img, self.alpha)
 
 
 class Gibbs_UNet(nn.Module):

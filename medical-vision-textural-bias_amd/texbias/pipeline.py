@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from . import kprog as K
+from . import ops as tbops
 from . import runtime as rt
 
 
@@ -58,12 +59,13 @@ class FusedChain:
         self.key = key
         self._mm: Optional[torch.Tensor] = None
         self._mm_b = 0
+        self._last_mm: Optional[torch.Tensor] = None
 
     @property
     def last_minmax(self) -> Optional[np.ndarray]:
         """float32 [B, 2] (min, max) per sample that the last call's salt-and-pepper stage used
         (decoded on demand: reading it synchronises), or None when no such stage ran."""
-        return rt.keys_to_float(self._mm[: self._mm_b]) if self._mm_b else None
+        return rt.keys_to_float(self._last_mm) if self._mm_b else None
 
     # --- host side: one sample's draws, in Compose order --------------------------------
     def _sample_plan(self, spatial, phase: Optional[Sequence[float]] = None) -> List:
@@ -117,7 +119,10 @@ class FusedChain:
     # --- device side --------------------------------------------------------------------
     def __call__(self, x: torch.Tensor, pad: int = 0, plans: Optional[List[List]] = None,
                  phases: Optional[Sequence[Sequence[float]]] = None, u: Optional[torch.Tensor] = None,
-                 cls: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 cls: Optional[torch.Tensor] = None, seed: Optional[int] = None) -> torch.Tensor:
+        """``seed``: Philox key of the salt-and-pepper field (default: drawn from torch's global
+        generator, which synchronises with the host; pass it explicitly to capture the chain in a
+        HIP graph)."""
         rt.require_hip(x, "FusedChain")
         if x.dim() != 5:
             raise ValueError("FusedChain expects [B, C, H, W, D]")
@@ -134,6 +139,7 @@ class FusedChain:
             self._mm = torch.empty((max(B, 8), 2), dtype=torch.int32, device=x.device)
         mm = self._mm[:B]
         self._mm_b = 0
+        self._last_mm = None
         cur = x
         padded = False
         mm_valid = False
@@ -147,8 +153,8 @@ class FusedChain:
                 if padded:   # filter the padded buffer in place (pass A reads all before C writes)
                     view = cur[..., : spatial[-1]]
                     rt.kspace_filter(view, 3, progs, C, out=view, minmax=mm)
-                else:
-                    cur = rt.kspace_filter(cur, 3, progs, C, pad=out_pad, minmax=mm)
+                else:   # the functional custom op (torch.compile / graph-capture friendly)
+                    cur, mm = torch.ops.texbias.kspace_filter(cur, 3, tbops.pack_programs(progs), C, out_pad)
                     padded = out_pad > 0
                 mm_valid = True
             else:
@@ -163,8 +169,8 @@ class FusedChain:
                     rt.minmax_keys(view, 4, out=mm)
                 thr = [((np.float32(p / 2), np.float32(p)) if p is not None else (-1.0, -1.0)) for p in ps]
                 if u is None and cls is None:
-                    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
-                    rt.salt_and_pepper(view, 4, thr, mm, out=view, seed=seed)
+                    sd = seed if seed is not None else int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+                    torch.ops.texbias.salt_and_pepper_(view, mm, torch.tensor(thr, dtype=torch.float32), sd, 0, 4)
                 else:
                     # parity mode: the explicit field / class map share the (padded) view's strides
                     def like_view(t, dtype):
@@ -177,11 +183,13 @@ class FusedChain:
                         return full[..., : spatial[-1]]
                     uv = like_view(u, torch.float32)
                     cv = like_view(cls, torch.int8) if cls is not None else None
-                    seed = 0 if u is not None else int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
-                    rt.salt_and_pepper(view, 4, thr, mm, out=view, u=uv, cls=cv, seed=seed)
+                    sd = 0 if u is not None else (
+                        seed if seed is not None else int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item()))
+                    rt.salt_and_pepper(view, 4, thr, mm, out=view, u=uv, cls=cv, seed=sd)
                     if cls is not None:
                         cls.copy_(cv)
                 self._mm_b = B
+                self._last_mm = mm
                 mm_valid = False
         if cur is x:
             cur = x.clone() if not pad else torch.nn.functional.pad(x, (0, pad))

@@ -52,7 +52,9 @@ class TrainStep:
     """model / loss / optimizer of the reference, optionally wrapped in DDP."""
 
     def __init__(self, model: torch.nn.Module, device: torch.device, distributed: bool = False,
-                 bucket_cap_mb: float = 4.0, channels_last: bool = False):
+                 bucket_cap_mb: float = 4.0, channels_last: bool = False, capturable: bool = False):
+        """``capturable``: the optimizer keeps its step counters on the device so the whole step can be
+        captured in a HIP graph (torch.cuda.graph)."""
         self.device = device
         self.channels_last = channels_last
         model = model.to(device)
@@ -70,6 +72,8 @@ class TrainStep:
         opt_kw = dict(lr=1e-4, weight_decay=1e-5, amsgrad=True)
         if device.type == "cuda":
             opt_kw["fused"] = True
+            if capturable:
+                opt_kw["capturable"] = True
         try:
             self.opt = torch.optim.Adam(self.model.parameters(), **opt_kw)
         except (RuntimeError, TypeError):
