@@ -101,11 +101,16 @@ int tb_kspace_filter_f32(const tb_plan* plan, const float* x, const int64_t* xs,
 
 /*
  * Salt and pepper over B samples of `rows` rows of `len` floats (row pitch `ld`, sample pitch `sb`):
- *   u = u_in[...] if u_in else Philox4x32-10(seed; counter = offset + b*rows*len + row*len + d)
  *   cls = u <= thr[b][0] ? 1 (MIN) : u <= thr[b][1] ? 2 (MAX) : 0 (keep)
  *   y = cls==1 ? min_b/2 : cls==2 ? max_b/2 : x     (min_b/max_b from minmax keys)
- * When x == y only the changed voxels are stored.  cls (int8, same indexing as x) may be NULL.
- * thr is a HOST float[B][2].
+ * u_in != NULL (parity mode): u is the caller's field, one value per voxel (the reference's
+ *   torch.rand), classified exactly as above.
+ * u_in == NULL: the device stream -- per segment of 1024 voxels, Philox4x32-10 (key seed, counter
+ *   from sample / segment / draw, stream `offset`) drives a geometric-gap walk over the changed
+ *   voxels (gap = floor(log u / log(1 - thr[b][1]))) and each changed voxel's class (MIN with
+ *   probability thr[b][0] / thr[b][1]): the same Bernoulli field at ~p of the RNG work.
+ *   In place (x == y) only the changed voxels are stored; out of place y is a copy plus them.
+ * cls (int8, same indexing as x) may be NULL.  thr is a HOST float[B][2].
  */
 int tb_salt_pepper_f32(const float* x, float* y, int8_t* cls, const float* u_in, uint64_t seed, uint64_t offset,
                        const float* thr, const uint32_t* minmax, int B, int64_t rows, int len, int64_t ld,
@@ -142,6 +147,15 @@ int tb_kspace_logabs_sum_f32(const tb_plan* plan, const float* x, const int64_t*
  */
 int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
                         int Hi, int Wi, int stride, int pad, void* stream);
+
+/*
+ * The tiling tb_conv3d_wgrad_f32 chooses for these sizes, without launching anything (host only):
+ * cfg[0] = SEG (64-column row segments staged per wave, 1..4), cfg[1] = TX (1: 16 input channels x
+ * 27 tap accumulators; 3: (channel, tx) columns for <= 5 channels), cfg[2] = YB (output rows per
+ * chunk), cfg[3] = chunks (work units), cfg[4] = LDS bytes per workgroup.  Same error codes.
+ */
+int tb_conv3d_wgrad_config(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride, int pad,
+                           int64_t* cfg);
 
 /*
  * Dice statistics of DiceLoss(sigmoid, squared_pred) (MONAI 0.5 formula, used by the reference's

@@ -96,14 +96,17 @@ struct BandInvArgs {
   const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
 };
 
+// floats of pass A's X region: the 64-row chunk (+8 slack), reused at slab end for the four
+// waves' O partials [wave][cos/sin][re/im][KWT][NT2][64 lanes][4] -- whichever is larger
+TB_HD int band_fwd_xn(int P, int NT2, int KWT) {
+  const int xn = BAND_ROWS_A * P + 8, ob = 4 * 2 * 2 * KWT * NT2 * 64 * 4;
+  return xn > ob ? xn : ob;
+}
 // LDS bytes of the two slab kernels
 TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
   const int P = (D & 1) ? D : D + 1;
   const int KSd = (D / 2 + 1 + 3) / 4, NT2 = g.NDk <= 16 ? 1 : 2, KWT = g.KW < 16 ? 1 : 2;
-  int xn = BAND_ROWS_A * P + 8;                     // the chunk, and the waves' O partials at slab end
-  const int ob = 4 * 2 * 2 * KWT * NT2 * 64 * 4;
-  xn = xn > ob ? xn : ob;
-  return (size_t)xn * 4 + (size_t)W * 8 + (size_t)NT2 * KSd * 128 * 4;
+  return (size_t)band_fwd_xn(P, NT2, KWT) * 4 + (size_t)W * 8 + (size_t)NT2 * KSd * 128 * 4;
 }
 constexpr int BAND_STG_P = 68;  // pitch (floats) of a wave's staged 32 x (32 + 32) output tile
 constexpr int BAND_SLOTS = 4;   // slabs whose pass-C' inputs a workgroup holds in LDS at once

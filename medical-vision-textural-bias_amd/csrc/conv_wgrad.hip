@@ -218,26 +218,20 @@ int launch_seg(const WgArgs& a, int seg, int by, size_t lds, hipStream_t st) {
   }
 }
 
-}  // namespace
-
-// dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2, padding 1 (file header).
-int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
-                        int Hi, int Wi, int stride, int pad, void* stream) {
-  if (!G || !X || !dW || N < 1 || M < 1 || Cc < 1 || Do < 1 || Ho < 1 || Wo < 1 || Di < 1 || Hi < 1 || Wi < 1)
-    return TB_ERR_INVALID_ARG;
+// Tiling of one weight-gradient call: TX (taps vs (c, tx) columns), SEG (64-wide row segments a
+// wave stages) and YB (output rows per chunk, the largest that fits the LDS budget).
+int wg_setup(WgArgs& a, int& seg, int& TX, int& by, size_t& lds, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
+             int Hi, int Wi, int stride, int pad) {
+  if (N < 1 || M < 1 || Cc < 1 || Do < 1 || Ho < 1 || Wo < 1 || Di < 1 || Hi < 1 || Wi < 1) return TB_ERR_INVALID_ARG;
   if ((stride != 1 && stride != 2) || pad != 1) return TB_ERR_INVALID_ARG;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st) != hipSuccess) return TB_ERR_HIP;
-  WgArgs a{};
-  a.G = G; a.X = X; a.dW = dW;
   a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
-  const int TX = Cc <= 5 ? 3 : 1;
+  TX = Cc <= 5 ? 3 : 1;
   a.ncc = TX == 3 ? 5 : 16;
   a.Wo4 = (Wo + 3) / 4 * 4;
   const int xw = stride * (a.Wo4 - 1) + 3;            // staged columns incl. the left halo
   a.XP = xw | 1;
   a.xcols = Wi < a.XP - 1 ? Wi : a.XP - 1;             // input columns that can be touched
-  const int seg = (((Wo > a.xcols ? Wo : a.xcols) + 63) / 64);
+  seg = (((Wo > a.xcols ? Wo : a.xcols) + 63) / 64);
   if (seg > 4) return TB_ERR_UNSUPPORTED_SIZE;
   const int prem = TX == 3 ? 3 : 2;                     // plane pitch mod 32 (bank spread of B reads)
   a.YB = 0;
@@ -260,8 +254,38 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
   a.nchunks = (int64_t)N * Do * a.nyb;
   const int mtiles = (M + 15) / 16;
   a.ctiles = (Cc + a.ncc - 1) / a.ncc;
-  const size_t lds = sizeof(float) * (size_t)((M < 16 ? M : 16) * a.PG + (Cc < a.ncc ? Cc : a.ncc) * a.PC + kSlack);
-  const int by = mtiles * a.ctiles;
+  lds = sizeof(float) * (size_t)((M < 16 ? M : 16) * a.PG + (Cc < a.ncc ? Cc : a.ncc) * a.PC + kSlack);
+  by = mtiles * a.ctiles;
+  return TB_OK;
+}
+
+}  // namespace
+
+// dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2, padding 1 (file header).
+int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
+                        int Hi, int Wi, int stride, int pad, void* stream) {
+  if (!G || !X || !dW) return TB_ERR_INVALID_ARG;
+  WgArgs a{};
+  int seg = 0, TX = 0, by = 0;
+  size_t lds = 0;
+  const int rc = wg_setup(a, seg, TX, by, lds, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad);
+  if (rc != TB_OK) return rc;
+  a.G = G; a.X = X; a.dW = dW;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st) != hipSuccess) return TB_ERR_HIP;
   if (stride == 1) return TX == 1 ? launch_seg<1, 1>(a, seg, by, lds, st) : launch_seg<1, 3>(a, seg, by, lds, st);
   return TX == 1 ? launch_seg<2, 1>(a, seg, by, lds, st) : launch_seg<2, 3>(a, seg, by, lds, st);
+}
+
+// The tiling tb_conv3d_wgrad_f32 would choose (no launch): cfg = {SEG, TX, YB, chunks, LDS bytes}.
+int tb_conv3d_wgrad_config(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride, int pad,
+                           int64_t* cfg) {
+  if (!cfg) return TB_ERR_INVALID_ARG;
+  WgArgs a{};
+  int seg = 0, TX = 0, by = 0;
+  size_t lds = 0;
+  const int rc = wg_setup(a, seg, TX, by, lds, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad);
+  if (rc != TB_OK) return rc;
+  cfg[0] = seg; cfg[1] = TX; cfg[2] = a.YB; cfg[3] = a.nchunks; cfg[4] = (int64_t)lds;
+  return TB_OK;
 }

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   const int P = (D & 1) ? D : D + 1;
   const int Ld = D / 2 + 1;                 // folded d in [0, D/2]
   const int KSd = (Ld + 3) / 4;             // 16x16x4 k-steps of the D product
-  const int XN = BAND_ROWS_A * P + 8;
+  const int XN = band_fwd_xn(P, NT2, KWT);  // twW / Bt start past the O partials too
   float* X = reinterpret_cast<float*>(smem);                     // [64][P] (+8 slack); O partials at slab end
   float2* twW = reinterpret_cast<float2*>(X + XN);               // (cos, -sin)(2 pi t / W)
   float* Bt = reinterpret_cast<float*>(twW + W);                 // [NT2][KSd][2][64]

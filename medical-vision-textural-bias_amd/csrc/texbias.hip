@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <math.h>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -172,6 +173,53 @@ __global__ __launch_bounds__(NT) void k_salt_pepper(const float* __restrict__ x,
           y[off] = c == 0 ? x[off] : (c == 1 ? vmin : vmax);
         }
       }
+    }
+  }
+}
+
+// Salt-and-pepper from the device stream: instead of one uniform per voxel, each lane walks a
+// segment of SAP_SEG voxels jumping straight to the next changed voxel -- the gap to it is
+// geometric, floor(log(u) / log(1 - p)) -- and draws its class (MIN with probability lo / hi).
+// The changed voxels form the same Bernoulli(p) field with P(MIN) = p_lo, P(MAX) = p_hi - p_lo
+// as u <= lo / lo < u <= hi of the reference (:478-479), at ~p of the RNG work.
+constexpr int SAP_SEG = 1024;
+struct SapGeomArgs {
+  float* y;
+  int8_t* cls;
+  uint64_t seed, offset;
+  float lo[TB_MAX_BATCH], hi[TB_MAX_BATCH];
+  const uint32_t* mm;
+  int b0;
+  int64_t rows;
+  int len;
+  int64_t ld, sb;
+};
+__global__ __launch_bounds__(256) void k_sap_geom(SapGeomArgs a) {
+  const int bl = blockIdx.y, b = a.b0 + bl;
+  const int64_t n = a.rows * a.len;
+  const int64_t start = ((int64_t)blockIdx.x * 256 + threadIdx.x) * SAP_SEG;
+  const float p = a.hi[bl];
+  if (start >= n || !(p > 0.f)) return;
+  const int64_t end = start + SAP_SEG < n ? start + SAP_SEG : n;
+  const float vmin = key2f(a.mm[2 * b]) * 0.5f, vmax = key2f(a.mm[2 * b + 1]) * 0.5f;
+  const float pmin = a.lo[bl] > 0.f ? a.lo[bl] / p : 0.f;  // P(MIN | changed)
+  const float lq = p >= 1.f ? -INFINITY : log1pf(-p);
+  const uint64_t ctr0 = ((uint64_t)b << 44) ^ ((uint64_t)(start / SAP_SEG) << 20);
+  int64_t pos = start - 1;
+  uint32_t j = 0;
+  for (;;) {
+    const u32x4 r = philox(ctr0 | j++, a.offset, a.seed);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float u1 = ((float)(r.v[2 * h] >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+      const float g = lq == -INFINITY ? 0.f : floorf(logf(u1) / lq);
+      pos += 1 + (g < (float)SAP_SEG ? (int64_t)g : (int64_t)SAP_SEG);
+      if (pos >= end) return;
+      const int c = u01(r.v[2 * h + 1]) < pmin ? 1 : 2;
+      const int64_t row = n < 0x7fffffff ? (int64_t)((uint32_t)pos / (uint32_t)a.len) : pos / a.len;
+      const int64_t off = b * a.sb + row * a.ld + (pos - row * a.len);
+      a.y[off] = c == 1 ? vmin : vmax;
+      if (a.cls) a.cls[off] = (int8_t)c;
     }
   }
 }
@@ -774,21 +822,54 @@ int tb_salt_pepper_f32(const float* x, float* y, int8_t* cls, const float* u_in,
                        void* stream) {
   if (!x || !y || !thr || !mm || B < 1 || rows < 1 || len < 1 || ld < len) return TB_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int sparse = (x == y && !cls && !u_in) ? 1 : 0;
   const int64_t n = rows * len;
-  int64_t blocks = ((n + 3) / 4 + NT_SAP - 1) / NT_SAP;
-  if (blocks > 2048) blocks = 2048;
-  // sparse in-place: only ~p of the voxels are stored (no algorithmic byte count is claimed)
-  Timer t(3, st, sparse ? 0.0 : (double)B * n * (8.0 + (u_in ? 4.0 : 0.0) + (cls ? 1.0 : 0.0)), "k_salt_pepper");
+  if (u_in) {  // parity mode: the caller's uniform field, one class per voxel
+    int64_t blocks = ((n + 3) / 4 + NT_SAP - 1) / NT_SAP;
+    if (blocks > 2048) blocks = 2048;
+    Timer t(3, st, (double)B * n * (12.0 + (cls ? 1.0 : 0.0)), "k_salt_pepper");
+    for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
+      const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
+      SapThr th;
+      for (int i = 0; i < TB_MAX_BATCH; ++i) {
+        th.lo[i] = i < nb ? thr[2 * (b0 + i)] : 0.f;
+        th.hi[i] = i < nb ? thr[2 * (b0 + i) + 1] : 0.f;
+      }
+      hipLaunchKernelGGL(k_salt_pepper<NT_SAP>, dim3((unsigned)blocks, nb), dim3(NT_SAP), 0, st, x, y, cls, u_in, seed,
+                         offset, th, mm, b0, rows, len, ld, sb, 0);
+      TB_HIP(hipGetLastError());
+    }
+    return TB_OK;
+  }
+  // device stream: out of place = copy, then the sparse scatter of the changed voxels (the class
+  // map, when asked for, is zeroed first); in place only the changed voxels are written
+  for (int b = 0; b < B; ++b) {
+    if (x != y)
+      TB_HIP(hipMemcpy2DAsync(y + b * sb, ld * 4, x + b * sb, ld * 4, (size_t)len * 4, rows, hipMemcpyDeviceToDevice, st));
+    if (cls) TB_HIP(hipMemset2DAsync(cls + b * sb, ld, 0, (size_t)len, rows, st));
+  }
+  // algorithmic bytes: one 4-B store per changed voxel (~p n), no reads
+  double changed = 0.0;
+  for (int b = 0; b < B; ++b) changed += (double)n * (thr[2 * b + 1] > 0.f ? (thr[2 * b + 1] < 1.f ? thr[2 * b + 1] : 1.f) : 0.f);
+  Timer t(3, st, changed * (4.0 + (cls ? 1.0 : 0.0)), "k_sap_geom");
+  const int64_t segs = (n + SAP_SEG - 1) / SAP_SEG;
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
-    SapThr th;
+    SapGeomArgs ga;
+    ga.y = y;
+    ga.cls = cls;
+    ga.seed = seed;
+    ga.offset = offset;
     for (int i = 0; i < TB_MAX_BATCH; ++i) {
-      th.lo[i] = i < nb ? thr[2 * (b0 + i)] : 0.f;
-      th.hi[i] = i < nb ? thr[2 * (b0 + i) + 1] : 0.f;
+      ga.lo[i] = i < nb ? thr[2 * (b0 + i)] : 0.f;
+      ga.hi[i] = i < nb ? thr[2 * (b0 + i) + 1] : 0.f;
     }
-    hipLaunchKernelGGL(k_salt_pepper<NT_SAP>, dim3((unsigned)blocks, nb), dim3(NT_SAP), 0, st, x, y, cls, u_in, seed,
-                       offset, th, mm, b0, rows, len, ld, sb, sparse);
+    ga.mm = mm;
+    ga.b0 = b0;
+    ga.rows = rows;
+    ga.len = len;
+    ga.ld = ld;
+    ga.sb = sb;
+    hipLaunchKernelGGL(k_sap_geom, dim3((unsigned)((segs + 255) / 256), nb), dim3(256), 0, st, ga);
     TB_HIP(hipGetLastError());
   }
   return TB_OK;

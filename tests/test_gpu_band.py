@@ -108,6 +108,24 @@ def test_band_program_variants(rt, prog_kind):
     assert torch.all(yb[..., sp[-1]:] == 0)
 
 
+@pytest.mark.parametrize("radius", [9.0, 15.5, 18.0, 20.0])
+def test_band_tile_variants_unpadded(rt, radius):
+    """All four pass-A' instantiations (NDk <= 16 or 32 kd columns, KW < 16 or 32 kw rows), whose
+    slab-end O partials outgrow the 64-row chunk in LDS at the larger ones; odd D, no padding (the
+    scalar-store path of pass C')."""
+    torch.manual_seed(5)
+    shape = (2, 2, 96, 112, 77)
+    x = torch.randn(shape, device="cuda")
+    geo = K.geometry(shape[2:])
+    prog = [K.disk_op(radius, False), K.spike_op((60, 90, 30), geo, 9.0, phase=0.2), K.wrap_op(0.25)]
+    yb, yf, names, mmb, mmf = both(rt, x, [prog, prog], shape[1])
+    assert names[0] == "k_band_fwd", names
+    assert torch.isfinite(yb).all()
+    assert (yb - yf).abs().max().item() / yf.abs().max().item() < 2e-6
+    mmf_ = rt.keys_to_float(mmb)
+    np.testing.assert_array_equal(mmf_[:, 1], yb.reshape(2, -1).max(1).values.cpu().numpy())
+
+
 def test_band_2d_and_1d_geometry(rt):
     """Size-1 leading axes (the reference's 2-D slices: [C, 1, H, W] / [C, 256, 256])."""
     torch.manual_seed(3)

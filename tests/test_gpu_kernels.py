@@ -244,3 +244,41 @@ def test_chain_chunking_is_bit_identical(rt, shape):
     for y, mm in outs[1:]:
         assert torch.equal(y, outs[0][0])
         assert torch.equal(mm, outs[0][1])
+
+
+@pytest.mark.parametrize("p", [0.05, 0.35, 1.0])
+def test_sap_geometric_stream_statistics(rt, p):
+    """The device stream walks geometric gaps between changed voxels: the changed set must be a
+    Bernoulli(p) field -- rate p, flat over the position inside the 1024-voxel segments, classes
+    MIN / MAX with probability 1/2 each given a change (thresholds p/2, p)."""
+    n_rows, ln = 4096, 512
+    x = torch.zeros((2, n_rows, ln), device="cuda")
+    x[:, 0, 0] = -4.0
+    x[:, 0, 1] = 6.0
+    mm = rt.minmax_keys(x, 2)
+    cls = torch.empty(x.shape, dtype=torch.int8, device="cuda")
+    thr = [(np.float32(p / 2), np.float32(p))] * 2
+    rt.salt_and_pepper(x, 2, thr, mm, cls=cls, seed=99, offset=3)
+    c = cls.reshape(2, -1).cpu().numpy()
+    n = c.shape[1]
+    hit = c > 0
+    rate = hit.mean()
+    sd = np.sqrt(p * (1 - p) / hit.size) + 1e-12
+    assert abs(rate - p) < 6 * sd + 1e-9
+    if p < 1.0:
+        pmin = (c == 1).sum() / max(hit.sum(), 1)
+        assert abs(pmin - 0.5) < 6 * np.sqrt(0.25 / hit.sum())
+        pos = np.arange(n) % 1024
+        bins = np.array([hit[:, (pos >= 128 * k) & (pos < 128 * (k + 1))].mean() for k in range(8)])
+        sdb = np.sqrt(p * (1 - p) / (hit.size / 8))
+        assert np.all(np.abs(bins - p) < 6 * sdb)
+    # in place writes only the changed voxels and agrees with the out-of-place result
+    y = x.clone()
+    rt.salt_and_pepper(y, 2, thr, mm, out=y, seed=99, offset=3)
+    z = rt.salt_and_pepper(x, 2, thr, mm, seed=99, offset=3)
+    torch.testing.assert_close(y, z, rtol=0, atol=0)
+    mmf = rt.keys_to_float(mm)
+    zc = z.cpu().numpy().reshape(2, -1)
+    for b in range(2):
+        np.testing.assert_array_equal(zc[b][c[b] == 1], np.float32(mmf[b, 0]) / 2)
+        np.testing.assert_array_equal(zc[b][c[b] == 2], np.float32(mmf[b, 1]) / 2)
