@@ -44,6 +44,17 @@ def wgrad(G: torch.Tensor, X: torch.Tensor, w_shape, stride: int, pad: int) -> t
     return dW.view(w_shape)
 
 
+def wgrad_config(g_shape, x_shape, stride: int, pad: int = 1) -> dict:
+    """The tiling ``wgrad`` picks for G [N, M, Do, Ho, Wo] / X [N, Cc, Di, Hi, Wi] (host only,
+    tb_conv3d_wgrad_config): SEG, TX, YB, chunks, lds_bytes."""
+    import ctypes
+    cfg = (ctypes.c_int64 * 5)()
+    N, M, Do, Ho, Wo = g_shape
+    Cc, Di, Hi, Wi = x_shape[1:]
+    check(lib().tb_conv3d_wgrad_config(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad, cfg), "tb_conv3d_wgrad_config")
+    return dict(zip(("SEG", "TX", "YB", "chunks", "lds_bytes"), list(cfg)))
+
+
 def channel_sum(g: torch.Tensor) -> torch.Tensor:
     """g [N, C, *spatial] -> [C]: sum over N and the spatial axes (tb_channel_sum_f32)."""
     g = g.contiguous()

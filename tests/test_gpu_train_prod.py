@@ -1,0 +1,197 @@
+"""The train step's HIP kernels at the shapes bench.py runs (U-Net input 2 x 4 x 240 x 240 x 160),
+against float64 restatements computed on the GPU:
+
+* split-K MFMA weight gradient (tb_conv3d_wgrad_f32) with its production tilings, gate left at
+  its default (no MIN_K_PER_OUTPUT override): the first down conv 4->16 stride 2 (SEG 3, TX 3,
+  YB 2), the half-resolution 16->16 stride-1 convs (SEG 2, TX 1) and the top ConvTranspose3d
+  32->3 stride 2 (SEG 3, TX 3, YB 4) -- each first at full row width on a short volume, then at
+  the full volume;
+* the direct few-channel conv (tb_conv3d_small_f32): forward, input and weight gradients of the
+  3->3 full-resolution conv;
+* fused InstanceNorm3d + PReLU forward/backward at the full- and half-resolution shapes;
+* fused DiceLoss(sigmoid, squared_pred) value and input gradient on the 3 x 240 x 240 x 160 logits.
+
+Reference: dW[m][c][t] = sum_{n,z,y,x} G[n][m][z,y,x] X[n][c][s z + tz - 1][..][..] as 27 float64
+einsums over strided views of the zero-padded input (the defining sum, independent of MIOpen); the
+convolution itself as the same 27-tap sum.  Tolerances (float32 arithmetic against float64, errors
+normalised by the largest reference magnitude): weight gradients 1e-4 (reductions of 2.3-18 M
+products), conv outputs / input gradients 1e-5, norm 2e-5, Dice value 1e-5 abs, gradient 1e-4.
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def conv(gpu):
+    from texbias import conv as C
+    return C
+
+
+def _taps(X64, stride, out_sp):
+    """(t, strided view of the padded input) for the 27 taps."""
+    Xp = F.pad(X64, (1, 1, 1, 1, 1, 1))
+    Do, Ho, Wo = out_sp
+    for tz in range(3):
+        for ty in range(3):
+            for tx in range(3):
+                yield (tz, ty, tx), Xp[:, :, tz:tz + stride * (Do - 1) + 1:stride,
+                                       ty:ty + stride * (Ho - 1) + 1:stride, tx:tx + stride * (Wo - 1) + 1:stride]
+
+
+def wgrad_ref64(G, X, stride):
+    Gd = G.double()
+    M, Cc = G.shape[1], X.shape[1]
+    out = torch.zeros((M, Cc, 3, 3, 3), dtype=torch.float64, device=G.device)
+    for (tz, ty, tx), Xs in _taps(X.double(), stride, G.shape[2:]):
+        out[:, :, tz, ty, tx] = torch.einsum("nmzyx,nczyx->mc", Gd, Xs)
+    return out
+
+
+def conv_ref64(x, w, b, stride=1):
+    sp = [(n + 2 - 3) // stride + 1 for n in x.shape[2:]]
+    w = w.double()
+    y = torch.zeros((x.shape[0], w.shape[0], *sp), dtype=torch.float64, device=x.device)
+    for (tz, ty, tx), Xs in _taps(x.double(), stride, sp):
+        y += torch.einsum("oc,nczyx->nozyx", w[:, :, tz, ty, tx], Xs)
+    if b is not None:
+        y += b.double().view(1, -1, 1, 1, 1)
+    return y
+
+
+def relmax(a, ref):
+    return (a.double() - ref).abs().max().item() / ref.abs().max().item()
+
+
+def _conv_case(conv, cin, cout, stride, x_shape, transposed, expect):
+    torch.manual_seed(0)
+    if transposed:
+        m = conv.ConvTranspose3d(cin, cout, 3, stride=stride, padding=1, output_padding=stride - 1).cuda()
+    else:
+        m = conv.Conv3d(cin, cout, 3, stride=stride, padding=1).cuda()
+    x = torch.randn(x_shape, device="cuda", requires_grad=True)
+    y = m(x)
+    # the gate at its default: the production layer takes the MFMA weight gradient
+    out_sp = None if transposed else list(y.shape[2:])
+    assert conv.fast_wgrad_applies(x, m.weight, out_sp, m.stride, m.padding, transposed)
+    G_shape, X_shape = (tuple(x.shape), tuple(y.shape)) if transposed else (tuple(y.shape), tuple(x.shape))
+    cfg = conv.wgrad_config(G_shape, X_shape, stride)
+    for k, v in expect.items():
+        assert cfg[k] == v, cfg
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    G, X = (x.detach(), g) if transposed else (g, x.detach())
+    ref = wgrad_ref64(G, X, stride)
+    assert relmax(m.weight.grad, ref) < 1e-4
+    bref = g.double().sum(dim=(0, 2, 3, 4))
+    assert relmax(m.bias.grad, bref) < 1e-5
+    return cfg
+
+
+def test_wgrad_row_width_conv_stride2(conv):
+    """First down conv 4->16 stride 2 at full row width (160 -> 80): SEG 3, TX 3, YB 2."""
+    _conv_case(conv, 4, 16, 2, (2, 4, 24, 24, 160), False, {"SEG": 3, "TX": 3, "YB": 2})
+
+
+def test_wgrad_row_width_convtranspose_32_3(conv):
+    """Top ConvTranspose3d 32->3 stride 2, output_padding 1, producing (2, 3, 24, 24, 160)."""
+    _conv_case(conv, 32, 3, 2, (2, 32, 12, 12, 80), True, {"SEG": 3, "TX": 3, "YB": 4})
+
+
+def test_wgrad_full_volume_first_down_conv(conv):
+    cfg = _conv_case(conv, 4, 16, 2, (2, 4, 240, 240, 160), False, {"SEG": 3, "TX": 3, "YB": 2})
+    assert cfg["chunks"] == 2 * 120 * 60
+
+
+def test_wgrad_full_volume_half_res_16_16(conv):
+    _conv_case(conv, 16, 16, 1, (2, 16, 120, 120, 80), False, {"SEG": 2, "TX": 1})
+
+
+def test_wgrad_full_volume_top_convtranspose(conv):
+    _conv_case(conv, 32, 3, 2, (2, 32, 120, 120, 80), True, {"SEG": 3, "TX": 3, "YB": 4})
+
+
+def test_small_conv_full_volume_3_3(conv):
+    """The top ResidualUnit's 3->3 conv at 2 x 3 x 240 x 240 x 160: forward, dx, dW, db."""
+    torch.manual_seed(1)
+    m = conv.Conv3d(3, 3, 3, padding=1).cuda()
+    x = torch.randn((2, 3, 240, 240, 160), device="cuda", requires_grad=True)
+    assert conv.small_conv_applies(x, m.weight, m.stride, m.padding)
+    y = m(x)
+    assert "SmallConv" in type(y.grad_fn).__name__
+    yr = conv_ref64(x.detach(), m.weight.detach(), m.bias.detach())
+    assert relmax(y, yr) < 1e-5
+    del yr
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    # dx = the stride-1 conv of g with the flipped, channel-transposed kernel
+    wt = m.weight.detach().flip(2, 3, 4).transpose(0, 1)
+    assert relmax(x.grad, conv_ref64(g, wt, None)) < 1e-5
+    assert relmax(m.weight.grad, wgrad_ref64(g, x.detach(), 1)) < 1e-4
+    assert relmax(m.bias.grad, g.double().sum(dim=(0, 2, 3, 4))) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 240, 240, 160), (2, 16, 120, 120, 80)])
+def test_instnorm_prelu_full_volume(gpu, shape):
+    from texbias.norm import instnorm_prelu
+    torch.manual_seed(2)
+    x = (torch.randn(shape, device="cuda") * 1.7 + 0.4).requires_grad_(True)
+    w = torch.tensor([0.25], device="cuda", requires_grad=True)
+    y = instnorm_prelu(x, w, 1e-5)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    xr = x.detach().double().requires_grad_(True)
+    wr = w.detach().double().requires_grad_(True)
+    yr = F.prelu(F.instance_norm(xr, eps=1e-5), wr)
+    (yr * g.double()).sum().backward()
+    assert relmax(y, yr.detach()) < 2e-5
+    assert relmax(x.grad, xr.grad) < 2e-5
+    assert relmax(w.grad, wr.grad) < 2e-5
+
+
+def test_dice_full_volume(gpu):
+    from texbias.losses import DiceLoss
+    torch.manual_seed(3)
+    shape = (2, 3, 240, 240, 160)
+    x = torch.randn(shape, device="cuda", requires_grad=True)
+    t = (torch.rand(shape, device="cuda") > 0.8).float()
+    loss = DiceLoss(sigmoid=True, squared_pred=True)
+    lf = loss(x, t)
+    gf, = torch.autograd.grad(lf, x)
+    xd = x.detach().double().requires_grad_(True)
+    lr = loss(xd, t.double())  # float64 on the GPU: the plain formula (fused path is float32-only)
+    gr, = torch.autograd.grad(lr, xd)
+    assert abs(lf.item() - lr.item()) < 1e-5
+    assert relmax(gf, gr) < 1e-4
+
+
+def test_train_step_full_volume_finite_and_fast_paths(gpu):
+    """One bench-shaped train step: every 3x3x3 layer whose gate opens takes the MFMA weight
+    gradient, and the step's loss and gradients are finite."""
+    from texbias import conv as C
+    from texbias.train import TrainStep, reference_model
+    torch.manual_seed(4)
+    model = reference_model(4, 3)
+    fast = []
+
+    def hook(mod, inp, out):
+        x = inp[0]
+        if isinstance(mod, C.ConvTranspose3d):
+            fast.append(C.fast_wgrad_applies(x, mod.weight, None, mod.stride, mod.padding, True))
+        elif mod.weight.shape[2:] == (3, 3, 3):
+            fast.append(C.fast_wgrad_applies(x, mod.weight, list(out.shape[2:]), mod.stride, mod.padding, False)
+                        or C.small_conv_applies(x, mod.weight, mod.stride, mod.padding))
+    hs = [m.register_forward_hook(hook) for m in model.modules() if isinstance(m, (C.Conv3d, C.ConvTranspose3d))]
+    step = TrainStep(model, torch.device("cuda"))
+    x = torch.randn((2, 4, 240, 240, 160), device="cuda")
+    lab = (torch.rand((2, 3, 240, 240, 160), device="cuda") > 0.85).float()
+    loss = step(x, lab)
+    for h in hs:
+        h.remove()
+    assert torch.isfinite(loss).item()
+    assert all(torch.isfinite(p).all().item() for p in model.parameters())
+    # the full- and half-resolution layers (the expensive ones) are all on the texbias kernels
+    assert sum(fast) >= 10, fast
