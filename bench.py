@@ -42,29 +42,43 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=2, help="volumes per GPU per step")
-    ap.add_argument("--shape", type=str, default="240,240,155")
-    ap.add_argument("--pad-to", type=int, default=160, help="U-Net D extent (G10: 155 is not /16)")
+    ap.add_argument("--config", choices=("c3", "c2"), default="c3",
+                    help="c3: full filter chain + U-Net train step on 4x240x240x155 (the headline); "
+                         "c2: Gibbs truncation (disk low-pass r=12.5) alone on 4x128x128x128 (BASELINE config 2)")
+    ap.add_argument("--batch", type=int, default=None, help="volumes per GPU per step (c3: 2, c2: 16)")
+    ap.add_argument("--shape", type=str, default=None, help="c3: 240,240,155; c2: 128,128,128")
+    ap.add_argument("--pad-to", type=int, default=None, help="U-Net D extent (c3: 160, G10: 155 is not /16)")
     ap.add_argument("--random-filters", action="store_true")
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--no-cudnn-benchmark", action="store_true",
                     help="skip MIOpen Find (its exhaustive solver search makes the first step slow, the rest fast)")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-vols", type=int, default=1)
+    ap.add_argument("--cpu-sample-vols", type=int, default=None,
+                    help="volumes per process in the CPU baseline's multi-process modes (c3: 1, c2: 8)")
+    ap.add_argument("--cpu-cores", type=int, default=None, help="CPU baseline core count (default: the job's share)")
     ap.add_argument("--filter-only", action="store_true", help="diagnostic: time the filter chain alone")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c2 = a.config == "c2"
+    a.batch = a.batch or (16 if c2 else 2)
+    a.shape = a.shape or ("128,128,128" if c2 else "240,240,155")
+    if a.pad_to is None:
+        a.pad_to = 0 if c2 else 160
+    a.cpu_sample_vols = a.cpu_sample_vols or (8 if c2 else 1)
+    if c2:
+        a.filter_only = True  # config 2 is the filter kernel alone
+    return a
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2", "traffic.json")
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r2")  # traffic_<config>.json (scripts/make_traffic.py)
 
 
-def pmc_traffic(kernel: str, launch_bytes: int):
+def pmc_traffic(kernel: str, launch_bytes: int, config: str = "c3"):
     """HBM bytes per launch of a filter kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
     WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), or None when not measured for launches of
     this size (the record carries the kernel name and the algorithmic bytes of the launches it measured)."""
     try:
-        with open(TRAFFIC_FILE) as f:
+        with open(os.path.join(TRAFFIC_DIR, f"traffic_{config}.json")) as f:
             rec = json.load(f)["kernels"].get(kernel)
         if not rec or abs(int(rec.get("algorithmic_bytes_per_launch", -1)) - int(launch_bytes)) > 0.001 * launch_bytes:
             return None
@@ -90,32 +104,39 @@ def maybe_launch_ranks(args) -> None:
     sys.exit(subprocess.call(cmd))
 
 
-def cpu_baseline(x0: np.ndarray, args) -> dict:
-    """The reference's CPU filter path restated op for op (oracle/, numpy complex64, 1 thread)."""
-    from oracle import filters_oracle as O
-    n = max(1, args.cpu_sample_vols)
-    rs = np.random.RandomState(0)
-    coords = O.ellipsoid_shell(x0.shape[1:], 55.0, 55.0, 30.0)
-    t0 = time.perf_counter()
-    for _ in range(n):
-        idx = O.ellipsoid_sample(coords, rs)
-        u = rs.random_sample(x0.shape).astype(np.float32)
-        O.chain(x0, 12.5, idx, 15.0, 0.5, 0.05, u)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "vols/s", "cores": 1, "kind": "port",
-            "sample": f"{n} volume(s) 4x{'x'.join(map(str, x0.shape[1:]))} through the oracle's op-for-op restatement of "
-                      "the reference chain disk(12.5)->planes(55,55,30,I=15)->wrap(0.5)->S&P(0.05) (numpy complex64 "
-                      f"FFTs, single thread); filter only, {dt:.1f} s"}
+def cpu_baseline(args, shape) -> dict:
+    """The reference's CPU filter path on this host's cores (oracle/cpu_bench.py, test/baseline
+    infrastructure): the torch-CPU restatement in the three BASELINE.md modes plus the numpy oracle.
+    ``value`` is the best mode (the strongest CPU baseline); every mode is listed."""
+    from oracle import cpu_bench
+    n = args.cpu_sample_vols
+    rep = cpu_bench.three_modes(args.config, shape, vols_single=2 * n, vols_multi=n, cores=args.cpu_cores,
+                                numpy_vols=n)
+    torch_modes = [m for m in rep["modes"] if m["kind"] == "torch"]
+    best = max(torch_modes, key=lambda m: m["vols_per_s"])
+    chain = ("disk(12.5)->planes(55,55,30,I=15)->wrap(0.5)->S&P(0.05)" if args.config == "c3"
+             else "disk low-pass r=12.5 (RandFourierDiskMaskd)")
+    return {"value": best["vols_per_s"], "unit": "vols/s", "cores": best["cores"], "kind": "port",
+            "sample": f"{best['volumes']} volume(s) 4x{'x'.join(map(str, shape))} in mode '{best['mode']}' through the "
+                      f"torch-CPU restatement of the reference's {chain} (oracle/torch_chain.py), {best['seconds']} s; "
+                      f"filter only; best of the modes listed",
+            "cpu_model": rep["cpu_model"], "job_cores": rep["job_cores"], "modes": rep["modes"]}
 
 
 def main():
     args = parse()
     maybe_launch_ranks(args)
+    H, W, D = (int(v) for v in args.shape.split(","))
+    cpu_line = None
+    if args.gpus == 1 and "WORLD_SIZE" not in os.environ and not args.no_cpu_baseline:
+        # before anything touches the GPU: the CPU workers are fresh interpreters and the host is idle
+        t_c = time.perf_counter()
+        cpu_line = cpu_baseline(args, (4, H, W, D))
+        print(f"[bench] cpu baseline {time.perf_counter() - t_c:.1f} s", file=sys.stderr, flush=True)
     from texbias import runtime as rt
-    from texbias.pipeline import FusedChain
+    from texbias.pipeline import FusedChain, reference_c3_chain
     from texbias.synth import brats_labels, brats_like
     from texbias.train import TrainStep, init_distributed, reference_model
-    import filters_and_operators as F
 
     rank, world, local = init_distributed()
     if world != args.gpus:
@@ -124,23 +145,19 @@ def main():
         print(f"[bench] world size {world} (backend {dist.get_backend() if world > 1 else 'none'})",
               file=sys.stderr, flush=True)
     dev = torch.device("cuda", local)
-    H, W, D = (int(v) for v in args.shape.split(","))
     B, C = args.batch, 4
     pad = max(0, args.pad_to - D)
     torch.manual_seed(1000 + rank)
 
     # resident synthetic data: two distinct batches per rank, labels pre-padded
     pool = [brats_like(B, C, (H, W, D), seed=rank * 97 + i, device=dev) for i in range(2)]
-    labels = [brats_labels(B, (H, W, D), seed=rank * 97 + i, device=dev, pad_to=D + pad) for i in range(2)]
+    labels = [] if args.filter_only else \
+        [brats_labels(B, (H, W, D), seed=rank * 97 + i, device=dev, pad_to=D + pad) for i in range(2)]
 
-    disk = F.RandFourierDiskMaskd(keys="image", r=12.5, inside_off=False, prob=1.0)
-    planes = F.RandPlaneWaves_ellipsoid("image", 55.0, 55.0, 30.0, intensity_value=15.0, prob=1.0)
-    wrap = F.WrapArtifactd("image", 0.5)
-    sap = F.SaltAndPepper(0.05)
-    for j, t in enumerate((disk, planes, sap)):
-        t.set_random_state(10 * rank + j)
-    planes.ellipsoid.set_random_state(10 * rank + 7)
-    chain = FusedChain([disk, planes, wrap, sap])
+    chain, tr = reference_c3_chain(rank)  # per-rank seeded transform streams
+    disk, planes, wrap, sap = tr["disk"], tr["planes"], tr["wrap"], tr["sap"]
+    if args.config == "c2":
+        chain = FusedChain([disk])
     prs = np.random.RandomState(12345 + rank)
 
     def randomize_filters():
@@ -221,10 +238,12 @@ def main():
             "dtype": "f32",
             "data": "synthetic BraTS-like z-scored 4-ch volumes resident in HBM; random-init U-Net",
             "config": {
-                "workload": ("C3 full filter chain (disk 12.5 -> plane wave (55,55,30) I=15 -> wrap 0.5 -> S&P 0.05) "
-                             "+ 3D U-Net(4->3, 16..256, 2 res units) fwd/bwd/Adam(amsgrad), DiceLoss")
-                            + (" [random per-batch filter params, config 4]" if args.random_filters else "")
-                            + (" [FILTER ONLY diagnostic]" if args.filter_only else ""),
+                "workload": (("C3 full filter chain (disk 12.5 -> plane wave (55,55,30) I=15 -> wrap 0.5 -> S&P 0.05) "
+                              "+ 3D U-Net(4->3, 16..256, 2 res units) fwd/bwd/Adam(amsgrad), DiceLoss")
+                             + (" [random per-batch filter params, config 4]" if args.random_filters else "")
+                             + (" [FILTER ONLY diagnostic]" if args.filter_only else ""))
+                            if args.config == "c3" else
+                            "C2 Gibbs truncation: RandFourierDiskMaskd(r=12.5) low-pass alone, batched 4x128^3 volumes",
                 "volume": [C, H, W, D],
                 "unet_input": [B, C, H, W, D + pad],
                 "per_gpu_batch": B,
@@ -233,14 +252,14 @@ def main():
             },
             "roofline": {"kernel": passes[dom]["kernel"], "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(passes[dom]["kernel"], dom_bytes),
-                         "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/r2/traffic.json)",
+                         "traffic": pmc_traffic(passes[dom]["kernel"], dom_bytes, args.config),
+                         "traffic_unit": f"bytes per launch (rocprofv3 PMC, profiles/r2/traffic_{args.config}.json)",
                          "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(pool[0][0].cpu().numpy(), args)
+        if cpu_line is not None:
+            line["cpu_baseline"] = cpu_line
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

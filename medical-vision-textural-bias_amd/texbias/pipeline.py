@@ -196,3 +196,21 @@ class FusedChain:
         elif pad and not padded:
             cur = torch.nn.functional.pad(cur, (0, pad))
         return cur
+
+
+def reference_c3_chain(rank: int = 0, seed_base: int = 10):
+    """The C3 chain (10_scripts/127_gibbs_spikes_wraparound_sap_OneChannel/
+    stylized_gibbs12p5_spikes15_wrap0p5_sap0p05_3modalities.py:171-174): disk r=12.5 -> plane wave on
+    the (55, 55, 30) ellipsoid shell, I=15 -> wrap 0.5 -> salt-and-pepper 0.05, with every random
+    transform seeded per data-parallel rank (``seed_base * rank + j``; the ellipsoid's own stream
+    ``seed_base * rank + 7``), so ranks draw distinct, reproducible streams -- the DataLoader
+    workers' independent streams in the reference.  Returns (FusedChain, {name: transform})."""
+    import filters_and_operators as F
+    disk = F.RandFourierDiskMaskd(keys="image", r=12.5, inside_off=False, prob=1.0)
+    planes = F.RandPlaneWaves_ellipsoid("image", 55.0, 55.0, 30.0, intensity_value=15.0, prob=1.0)
+    wrap = F.WrapArtifactd("image", 0.5)
+    sap = F.SaltAndPepper(0.05)
+    for j, t in enumerate((disk, planes, sap)):
+        t.set_random_state(seed_base * rank + j)
+    planes.ellipsoid.set_random_state(seed_base * rank + 7)
+    return FusedChain([disk, planes, wrap, sap]), dict(disk=disk, planes=planes, wrap=wrap, sap=sap)

@@ -89,3 +89,30 @@ class TrainStep:
         loss.backward()
         self.opt.step()
         return loss.detach()
+
+
+@torch.no_grad()
+def gibbs_gd(inputs: torch.Tensor, labels: torch.Tensor, model: torch.nn.Module, loss_fn, layer=None,
+             h: float = 0.01, learning_rate: float = 0.02) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Finite-difference update of a Gibbs layer's alpha (Gibbs_GD,
+    10_scripts/300_instutional_distribution/350_stylized_layers/gibbs0p7_layer_domain_GD.py:252-269):
+    loss at alpha and at alpha + h on the same batch, delta = (L_h - L_0) / h,
+    alpha <- alpha - learning_rate * delta.
+
+    ``layer`` defaults to ``model.gibbs`` (through a DDP wrapper).  Data-parallel form (the
+    reference trains on one GPU): every rank sees a different batch, so the per-rank slopes differ;
+    one 2-element all-reduce averages (delta, L_0) over the ranks before the update, and every
+    replica's alpha moves identically.  Returns (L_0, alpha) as device tensors -- no host sync (the
+    reference's ``.item()`` calls are left to the caller)."""
+    if layer is None:
+        layer = getattr(model, "module", model).gibbs
+    old = layer.alpha.clone()
+    l0 = loss_fn(model(inputs), labels)
+    layer.alpha = old + h
+    lh = loss_fn(model(inputs), labels)
+    buf = torch.stack([(lh - l0) / h, l0]).to(torch.float32)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        buf /= dist.get_world_size()
+    layer.alpha = old - learning_rate * buf[0].to(old.dtype)
+    return buf[1], layer.alpha

@@ -28,8 +28,8 @@ fetch = read(sys.argv[1], "FETCH_SIZE")
 write = read(sys.argv[2], "WRITE_SIZE")
 bench = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
 alg = {p["kernel"]: p.get("algorithmic_bytes") for p in bench["filter_passes"].values()}
-out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, python3 bench.py --filter-only "
-                 "(B=2 x 4 x 240x240x155, output padded to 160); per-launch averages",
+out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, python3 bench.py "
+                 + (sys.argv[5] if len(sys.argv) > 5 else "--filter-only") + " ; per-launch averages",
        "correction": "FETCH_SIZE (KiB) x 1024 x 2 per MI355X_MICROARCH.md HBM section (gfx950 tallies 128-B "
                      "requests at 64 B; calibrated there for 16-B/lane reads), WRITE_SIZE (KiB) x 1024 as is",
        "kernels": {}}

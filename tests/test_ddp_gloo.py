@@ -58,3 +58,93 @@ def test_ddp_two_ranks_stay_in_sync():
     diff, moved = q.get(timeout=5), q.get(timeout=5)
     assert diff == 0.0          # replicas bit-identical
     assert moved > 0.0          # and they actually trained
+
+
+def _plan_bytes(plans):
+    out = []
+    for stages in plans:
+        for kind, v in stages:
+            out.append((kind, [bytes(op) for op in v] if kind == "k" else v))
+    return out
+
+
+def _worker_chain_gd(rank, world, port, out):
+    """Host side of the data-parallel filter stage and the Gibbs-layer update, 2 gloo ranks."""
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "medical-vision-textural-bias_amd"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    import torch.nn as nn
+    from texbias.pipeline import reference_c3_chain
+    from texbias.train import gibbs_gd, init_distributed
+    torch.set_num_threads(1)
+    init_distributed("gloo")
+    # (1) per-rank seeded chain: bench.py's draws, two steps of a batch of 2
+    chain, _ = reference_c3_chain(rank)
+    plans = [_plan_bytes(chain.plan(2, (240, 240, 155))) for _ in range(2)]
+    again, _ = reference_c3_chain(rank)
+    replay = [_plan_bytes(again.plan(2, (240, 240, 155))) for _ in range(2)]
+    got = [None] * world
+    dist.all_gather_object(got, plans)
+
+    # (2) Gibbs_GD across ranks: a CPU stand-in for the Gibbs U-Net whose loss depends smoothly on
+    # alpha; every rank has its own batch, so its own finite-difference slope
+    class Layer(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.register_buffer("alpha", torch.tensor([0.5]))
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.gibbs = Layer()
+
+        def forward(self, x):
+            return x * self.gibbs.alpha + x * x * self.gibbs.alpha ** 2
+
+    net = Net()
+    g = torch.Generator().manual_seed(7 + rank)
+    x = torch.randn((2, 1, 8, 8, 8), generator=g)
+    lab = torch.randn((2, 1, 8, 8, 8), generator=g)
+    loss_fn = lambda y, t: ((y - t) ** 2).mean()  # noqa: E731
+    a0 = net.gibbs.alpha.clone()
+    with torch.no_grad():
+        own = (loss_fn(net.__class__.forward(_with_alpha(net, a0 + 0.01), x), lab)
+               - loss_fn(net.__class__.forward(_with_alpha(net, a0), x), lab)) / 0.01
+    l0, alpha = gibbs_gd(x, lab, net, loss_fn)
+    slopes = [None] * world
+    dist.all_gather_object(slopes, float(own))
+    alphas = [None] * world
+    dist.all_gather_object(alphas, float(alpha))
+    if rank == 0:
+        out.put((got, plans == replay, slopes, alphas, float(a0)))
+    dist.destroy_process_group()
+
+
+def _with_alpha(net, a):
+    import copy
+    m = copy.deepcopy(net)
+    m.gibbs.alpha = a.clone()
+    return m
+
+
+@pytest.mark.timeout(300)
+def test_ddp_filter_seeding_and_gibbs_gd():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_chain_gd, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs)
+    got, reproducible, slopes, alphas, a0 = q.get(timeout=5)
+    assert reproducible                  # a rank's draws are a function of its seed
+    assert got[0] != got[1]              # and the ranks' streams differ (distinct spike points)
+    assert [k for k, _ in got[0][0]] == ["k", "sap", "k", "sap"]  # per sample: one fused k pass, then S&P
+    assert slopes[0] != slopes[1]        # different batches, different finite-difference slopes
+    # every replica applied the rank-averaged slope: alpha identical everywhere
+    assert alphas[0] == alphas[1]
+    assert abs(alphas[0] - (a0 - 0.02 * (slopes[0] + slopes[1]) / 2)) < 1e-6
