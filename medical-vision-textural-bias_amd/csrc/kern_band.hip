@@ -431,7 +431,7 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
 __device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
 
 template <int VT>  // 32-row tiles of V (2 (NDk + points) <= 32 VT)
-__global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
+__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1 ? 3 : 2, 4))) void k_band_inv(BandInvArgs) {
   // The workgroup takes its slabs in batches of BAND_SLOTS: the batch's inputs (V-product
   // fragments from pass B2', the samples' point rows of the synthesis table) are loaded into LDS
   // first, so that the (slab, 32-row tile) units the four waves then work through issue only
@@ -538,21 +538,9 @@ __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
               yo = __builtin_amdgcn_mfma_f32_32x32x2f32(bo, vacc[vt][sI + 1], yo, 0, 0, 0);
             }
         if (diag & 16) continue;
-        // y[w][d] = E - O (direct) and y[w][D - d] = E + O (mirror), staged [row][32 | 32] through
-        // LDS so that every store instruction writes whole 128-B row segments
+        // y[w][d] = E - O (direct half), then y[w][D - d] = E + O (mirror half), each staged
+        // [row][32] through LDS so that every store instruction writes whole 128-B row segments
         const int c4 = lane & 7;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 dv, mv;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            dv[q] = ye[4 * g + q] - yo[4 * g + q];
-            mv[3 - q] = ye[4 * g + q] + yo[4 * g + q];
-          }
-          *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + 8 * g + 4 * hl) = dv;
-          *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + 32 + 28 - 8 * g - 4 * hl) = mv;
-        }
-        __builtin_amdgcn_wave_barrier();
         const int dbase = nt * 32 + 4 * c4, dmir = nt * 32 + 31 - 4 * c4;
         // the mirror of d = 0 is column D: the first U-Net pad column, written as 0 in the same vector
         const bool padlane = nt == 0 && c4 == 7 && ypad > 0;
@@ -564,54 +552,73 @@ __global__ __launch_bounds__(BAND_NT) void k_band_inv(BandInvArgs) {
           nm += ((d >= 1 && 2 * d < D && d < Dh) || (padlane && d == 0)) ? 1 : 0;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int r = (lane >> 3) + 8 * k;
-          const int wr = 32 * tw_ + r;
-          if (wr >= W) continue;
-          const f32x4 dv = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 4 * c4);
-          f32x4 mv = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 32 + 4 * c4);
-          if (padlane) mv[3] = 0.f;  // column D
-          float* yrr = yb + (int64_t)wr * a.sw;
-          if (vec && nd == 4) {
-            *reinterpret_cast<f32x4*>(yrr + dbase) = dv;
-            lo = fminf(lo, fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])));
-            hi = fmaxf(hi, fmaxf(fmaxf(dv[0], dv[1]), fmaxf(dv[2], dv[3])));
-          } else if (nd > 0) {
+        for (int half = 0; half < 2; ++half) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (q < nd) {
-                yrr[dbase + q] = dv[q];
-                lo = fminf(lo, dv[q]);
-                hi = fmaxf(hi, dv[q]);
-              }
-          }
-          if (vec && mal && nm == 4) {
-            *reinterpret_cast<f32x4*>(yrr + D - dmir) = mv;
-            const float m3 = padlane ? mv[2] : mv[3];  // the pad zero is not an image value
-            lo = fminf(lo, fminf(fminf(mv[0], mv[1]), fminf(mv[2], m3)));
-            hi = fmaxf(hi, fmaxf(fmaxf(mv[0], mv[1]), fmaxf(mv[2], m3)));
-          } else if (nm > 0) {
+          for (int g = 0; g < 4; ++g) {
+            f32x4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const int d = dmir - q;  // mv[q] is the value at column D - dmir + q = D - d
-              if (d >= 1 && 2 * d < D && d < Dh) {
-                yrr[D - d] = mv[q];
-                lo = fminf(lo, mv[q]);
-                hi = fmaxf(hi, mv[q]);
-              } else if (padlane && d == 0) {
-                yrr[D] = 0.f;
+              if (half == 0)
+                v[q] = ye[4 * g + q] - yo[4 * g + q];
+              else
+                v[3 - q] = ye[4 * g + q] + yo[4 * g + q];
+            }
+            const int col = half == 0 ? 8 * g + 4 * hl : 28 - 8 * g - 4 * hl;
+            *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + col) = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int r = (lane >> 3) + 8 * k;
+            const int wr = 32 * tw_ + r;
+            if (wr >= W) continue;
+            f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 4 * c4);
+            float* yrr = yb + (int64_t)wr * a.sw;
+            if (half == 0) {
+              if (vec && nd == 4) {
+                *reinterpret_cast<f32x4*>(yrr + dbase) = v;
+                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], v[3])));
+                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+              } else if (nd > 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (q < nd) {
+                    yrr[dbase + q] = v[q];
+                    lo = fminf(lo, v[q]);
+                    hi = fmaxf(hi, v[q]);
+                  }
+              }
+            } else {
+              if (padlane) v[3] = 0.f;  // column D
+              if (vec && mal && nm == 4) {
+                *reinterpret_cast<f32x4*>(yrr + D - dmir) = v;
+                const float m3 = padlane ? v[2] : v[3];  // the pad zero is not an image value
+                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], m3)));
+                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], m3)));
+              } else if (nm > 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const int d = dmir - q;  // v[q] is the value at column D - dmir + q = D - d
+                  if (d >= 1 && 2 * d < D && d < Dh) {
+                    yrr[D - d] = v[q];
+                    lo = fminf(lo, v[q]);
+                    hi = fmaxf(hi, v[q]);
+                  } else if (padlane && d == 0) {
+                    yrr[D] = 0.f;
+                  }
+                }
+              }
+              if (padlane) {  // the rest of the zero D-padding: columns D + 1 .. D + ypad - 1
+                int p = 1;
+                for (; p < ypad && ((D + p) & 3); ++p) yrr[D + p] = 0.f;
+                if (vec)
+                  for (; p + 4 <= ypad; p += 4) *reinterpret_cast<f32x4*>(yrr + D + p) = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (; p < ypad; ++p) yrr[D + p] = 0.f;
               }
             }
           }
-          if (padlane) {  // the rest of the zero D-padding: columns D + 1 .. D + ypad - 1
-            int p = 1;
-            for (; p < ypad && ((D + p) & 3); ++p) yrr[D + p] = 0.f;
-            if (vec)
-              for (; p + 4 <= ypad; p += 4) *reinterpret_cast<f32x4*>(yrr + D + p) = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (; p < ypad; ++p) yrr[D + p] = 0.f;
-          }
+          __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
       }
       if (a.mm) {  // per-unit partial (reduced per sample by k_band_minmax)
         lo = wave_min(lo);
@@ -689,9 +696,20 @@ __global__ __launch_bounds__(256) void k_copy_pad(CopyArgs a) {
   }
 }
 
-int band_grid(int units, size_t lds, int ncu) {
-  int per_cu = (int)(163840 / (lds ? lds : 1));
-  per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+// Persistent grid: the workgroups that are resident at once (LDS and register occupancy, at most
+// 4 per CU), never more than there are units -- no second, partial round of workgroups.
+template <class K>
+int band_grid(K kern, int units, size_t lds, int ncu) {
+  static size_t last_lds = ~(size_t)0;
+  static int last_occ = 1;
+  if (lds != last_lds) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BAND_NT, lds) != hipSuccess || occ < 1)
+      occ = (int)(163840 / (lds ? lds : 1));
+    last_occ = occ;
+    last_lds = lds;
+  }
+  const int per_cu = last_occ < 1 ? 1 : (last_occ > 4 ? 4 : last_occ);
   const int g = ncu * per_cu;
   return units < g ? units : g;
 }
@@ -702,7 +720,7 @@ hipError_t launch_fwd_t(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t s
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
   const int units = a.pl.H * a.nbc;
-  hipLaunchKernelGGL(kern, dim3(band_grid(units, lds, ncu)), dim3(BAND_NT), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(band_grid(kern, units, lds, ncu)), dim3(BAND_NT), lds, st, a);
   return hipGetLastError();
 }
 
@@ -713,7 +731,7 @@ hipError_t launch_inv_t(const BandInvArgs& a, int ncu, hipStream_t st) {
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
   const int units = a.pl.H * a.nbc;  // slabs, taken in batches of BAND_SLOTS per workgroup
-  hipLaunchKernelGGL(kern, dim3(band_grid(units, lds, ncu)), dim3(BAND_NT), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(band_grid(kern, units, lds, ncu)), dim3(BAND_NT), lds, st, a);
   return hipGetLastError();
 }
 
