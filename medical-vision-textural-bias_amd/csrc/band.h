@@ -123,8 +123,8 @@ TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
   c.bimg = 0;                                         // [2 NDk][NCOL] band rows of the synthesis table
   c.tww = band_al16(c.bimg + 2 * g.NDk * g.NCOL * 4); // [W] twiddles
   c.frag = band_al16(c.tww + W * 8);                  // [SLOTS][VT KV 64] V-product fragments
-  c.prow = band_al16(c.frag + BAND_SLOTS * band_vt(g) * band_kv(g) * 64 * 4);  // [SLOTS][2 npm][NCOL]
-  c.stg = band_al16(c.prow + BAND_SLOTS * 2 * npm * g.NCOL * 4);  // [4 waves][32][BAND_STG_P] staging
+  c.prow = band_al16(c.frag + BAND_SLOTS * band_vt(g) * band_kv(g) * 64 * 4);  // [SLOTS][2 npm + 4][NCOL]
+  c.stg = band_al16(c.prow + BAND_SLOTS * (2 * npm + 4) * g.NCOL * 4);  // [4 waves][32][BAND_STG_P] staging
   c.total = band_al16(c.stg + 4 * 32 * BAND_STG_P * 4);
   return c;
 }

@@ -99,6 +99,26 @@ __device__ __forceinline__ void chunk_copy_strided(float* xs, int P, const Chunk
   }
 }
 
+// Global -> LDS copy of n elements of T by the whole workgroup with U loads in flight per thread
+// (a plain loop would wait for every load before its LDS store: one memory round trip per
+// iteration, ~20 of them in a kernel prologue before the first output is written).
+template <int U, class T>
+__device__ __forceinline__ void lds_fill(T* dst, const T* __restrict__ src, int n, int tid) {
+  for (int base = 0; base < n; base += U * BAND_NT) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * BAND_NT + tid;
+      if (i < n) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * BAND_NT + tid;
+      if (i < n) dst[i] = v[u];
+    }
+  }
+}
+
 // NT2: 16-wide kd tiles (NDk <= 16 NT2); KWT: 16-wide kw tiles (KW < 16 KWT).
 // Per 64-row chunk each wave owns 16 rows:
 //   D product  R(row, kd) = sum_d s_d cos + i sum_d t_d sin      16x16x4 MFMA, folded over (d, D-d)
@@ -120,9 +140,10 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
   float* X = reinterpret_cast<float*>(smem);                     // [64][P] (+8 slack); O partials at slab end
   float2* twW = reinterpret_cast<float2*>(X + XN);               // (cos, -sin)(2 pi t / W)
   float* Bt = reinterpret_cast<float*>(twW + W);                 // [NT2][KSd][2][64]
-  for (int t = tid; t < W; t += BAND_NT) twW[t] = ld2(a.pl.tw[1] + t);
+  lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  // plan table (host double precision); 8-B pieces: Bt follows W float2 twiddles
+  lds_fill<8>(reinterpret_cast<float2*>(Bt), reinterpret_cast<const float2*>(a.tbt), NT2 * KSd * 64, tid);
   for (int t = tid; t < XN; t += BAND_NT) X[t] = 0.f;   // rows past W in a short last chunk stay finite
-  for (int e = tid; e < NT2 * KSd * 128; e += BAND_NT) Bt[e] = a.tbt[e];  // plan table (host double precision)
   const FastDiv fd = FastDiv::make(D);
   const int units = H * a.nbc;
   const int nch = (W + BAND_ROWS_A - 1) / BAND_ROWS_A;
@@ -447,15 +468,15 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int Dh = D / 2 + 1;            // folded output columns d in [0, D/2]
   const int nrv = 2 * (NDk + npm);     // used rows of V / the synthesis table
   const int fsz = VT * KV * 64;        // floats of one slab's fragments
-  const int psz = 2 * npm * NCOL;      // floats of one slab's point rows
+  const int psz = (2 * npm + 4) * NCOL;  // floats of one slab's point rows (+4 zero rows: see E/O)
   const BandInvCarve cv = band_inv_carve(a.g, W, D);
   float* Bimg = reinterpret_cast<float*>(smem + cv.bimg);  // [2 NDk][NCOL]: even rows cos, odd rows sin
   float2* twW = reinterpret_cast<float2*>(smem + cv.tww);  // (cos, -sin)(2 pi t / W)
   float* Fs = reinterpret_cast<float*>(smem + cv.frag);    // [BAND_SLOTS][fsz]
   float* Ps = reinterpret_cast<float*>(smem + cv.prow);    // [BAND_SLOTS][psz]
   float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 32 * BAND_STG_P;  // this wave's 32 x 32 tile
-  for (int t = tid; t < W; t += BAND_NT) twW[t] = ld2(a.pl.tw[1] + t);
-  for (int e = tid; e < 2 * NDk * NCOL; e += BAND_NT) Bimg[e] = a.tds[e];
+  lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  lds_fill<4>(reinterpret_cast<float4*>(Bimg), reinterpret_cast<const float4*>(a.tds), 2 * NDk * NCOL / 4, tid);
   const int ntw = (W + 31) / 32;     // 32-row tiles of a slab
   const int nslab = H * a.nbc;
   const int ntn = NCOL / 32;         // 32-column tiles of the folded row
@@ -470,12 +491,27 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
     __syncthreads();  // the previous batch is done with Fs / Ps
     for (int i = 0; i < nb; ++i) {
       const int slab = u0 + i * (int)gridDim.x;
-      const float* F = a.M2F + (int64_t)slab * fsz;
-      for (int e = tid; e < fsz; e += BAND_NT) Fs[i * fsz + e] = F[e];
+      lds_fill<2>(reinterpret_cast<float4*>(Fs + i * fsz), reinterpret_cast<const float4*>(a.M2F + (int64_t)slab * fsz),
+                  fsz / 4, tid);
       const BandSamplePts& sp = a.sp[(a.cofs + slab / H) / a.C];
-      for (int e = tid; e < psz; e += BAND_NT) {
-        const int r = e / NCOL, n = e - r * NCOL, j = r >> 1;
-        Ps[i * psz + e] = j < sp.n ? a.tds[(2 * sp.p[j].kd + (r & 1)) * NCOL + n] : 0.f;
+      const int nc4 = NCOL / 4;
+      float4 v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // psz / 4 <= 2 BAND_NT for the launches band_plan admits
+        const int e = u * BAND_NT + tid;
+        const int r = e / nc4, n = e - r * nc4, j = r >> 1;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < psz / 4 && j < sp.n)
+          v[u] = reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (u * BAND_NT + tid < psz / 4) reinterpret_cast<float4*>(Ps + i * psz)[u * BAND_NT + tid] = v[u];
+      for (int e = 2 * BAND_NT + tid; e < psz / 4; e += BAND_NT) {  // larger point sets: plain loop
+        const int r = e / nc4, n = e - r * nc4, j = r >> 1;
+        reinterpret_cast<float4*>(Ps + i * psz)[e] =
+            j < sp.n ? reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n]
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     __syncthreads();
@@ -514,11 +550,14 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
       float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
       const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
       float lo = 3.402823466e38f, hi = -3.402823466e38f;
+      // synthesis-table rows: < 2 NDk the band rows (Bimg), above them the slab's point rows and
+      // four zero rows (the upper lane half reads up to 4 rows past nrv): B operands without branches
+      const float* Tb = Bimg + l31;
+      const float* Tp = Pr + l31 - 2 * NDk * NCOL;
       for (int nt = 0; nt < ntn; ++nt) {
         f32x16 ye, yo;
 #pragma unroll
         for (int j = 0; j < 16; ++j) ye[j] = yo[j] = 0.f;
-        const int col = nt * 32 + l31;
         if (!(diag & 8))
 #pragma unroll
           for (int vt = 0; vt < VT; ++vt)
@@ -526,16 +565,9 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
             for (int sI = 0; sI < 16; sI += 2) {  // even sI: real rows (E); sI + 1: imaginary rows (O)
               if (32 * vt + acc_row(sI) >= nrv) break;  // both halves' rows past the used ones are zero
               const int re = 32 * vt + acc_row(sI) + 4 * hl;  // this lane's (real) row of the step
-              float be = 0.f, bo = 0.f;
-              if (re < 2 * NDk) {
-                be = Bimg[re * NCOL + col];
-                bo = Bimg[(re + 1) * NCOL + col];
-              } else if (re < nrv) {
-                be = Pr[(re - 2 * NDk) * NCOL + col];
-                bo = Pr[(re - 2 * NDk + 1) * NCOL + col];
-              }
-              ye = __builtin_amdgcn_mfma_f32_32x32x2f32(be, vacc[vt][sI], ye, 0, 0, 0);
-              yo = __builtin_amdgcn_mfma_f32_32x32x2f32(bo, vacc[vt][sI + 1], yo, 0, 0, 0);
+              const float* tr = (re < 2 * NDk ? Tb : Tp) + re * NCOL + nt * 32;
+              ye = __builtin_amdgcn_mfma_f32_32x32x2f32(tr[0], vacc[vt][sI], ye, 0, 0, 0);
+              yo = __builtin_amdgcn_mfma_f32_32x32x2f32(tr[NCOL], vacc[vt][sI + 1], yo, 0, 0, 0);
             }
         if (diag & 16) continue;
         // y[w][d] = E - O (direct half), then y[w][D - d] = E + O (mirror half), each staged
@@ -638,7 +670,24 @@ __global__ __launch_bounds__(256) void k_band_minmax(const float2* __restrict__ 
   const int64_t n = (int64_t)C * H * ntw;  // one partial per (slab, 32-row tile)
   const float2* p = mmp + (int64_t)b * C * H * ntw;
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  for (int64_t i = threadIdx.x; i < n; i += 256) {
+  int64_t i0 = 0;
+  if (((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {  // two partials per 16-B load, 4 loads in flight
+    const float4* p4 = reinterpret_cast<const float4*>(p);
+    const int64_t n4 = n / 2;
+    for (int64_t j = threadIdx.x; j < n4; j += 4 * 256) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = j + u * 256 < n4 ? p4[j + u * 256] : make_float4(lo, hi, lo, hi);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        lo = fminf(lo, fminf(v[u].x, v[u].z));
+        hi = fmaxf(hi, fmaxf(v[u].y, v[u].w));
+      }
+    }
+    i0 = 2 * n4;
+  }
+  for (int64_t i = i0 + threadIdx.x; i < n; i += 256) {
     const float2 v = p[i];
     lo = fminf(lo, v.x);
     hi = fmaxf(hi, v.y);
