@@ -182,7 +182,10 @@ __global__ __launch_bounds__(NT) void k_salt_pepper(const float* __restrict__ x,
 // geometric, floor(log(u) / log(1 - p)) -- and draws its class (MIN with probability lo / hi).
 // The changed voxels form the same Bernoulli(p) field with P(MIN) = p_lo, P(MAX) = p_hi - p_lo
 // as u <= lo / lo < u <= hi of the reference (:478-479), at ~p of the RNG work.
-constexpr int SAP_SEG = 1024;
+#ifndef TB_SAP_SEG
+#define TB_SAP_SEG 256  // voxels per thread: 4 waves per SIMD on a C3 launch (1024: 61 us, 256: 51.5 us)
+#endif
+constexpr int SAP_SEG = TB_SAP_SEG;
 struct SapGeomArgs {
   float* y;
   int8_t* cls;

@@ -249,7 +249,7 @@ def test_chain_chunking_is_bit_identical(rt, shape):
 @pytest.mark.parametrize("p", [0.05, 0.35, 1.0])
 def test_sap_geometric_stream_statistics(rt, p):
     """The device stream walks geometric gaps between changed voxels: the changed set must be a
-    Bernoulli(p) field -- rate p, flat over the position inside the 1024-voxel segments, classes
+    Bernoulli(p) field -- rate p, flat over the position inside the per-thread segments, classes
     MIN / MAX with probability 1/2 each given a change (thresholds p/2, p)."""
     n_rows, ln = 4096, 512
     x = torch.zeros((2, n_rows, ln), device="cuda")
