@@ -204,6 +204,34 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
                               size_t ws_bytes, void* stream);
 
 /*
+ * GPU-side BraTS preprocessing of B resident raw volumes img [B][C][H0][W0][D0] and
+ * label maps lab [B][H0][W0][D0] (float class ids, as LoadImaged gives them; may be NULL when
+ * out_lab is NULL), per sample b with params[b] drawn on the host:
+ *   crop      out[.][i][j][k] = in[h0 + i][w0 + j][d0 + k]          RandSpatialCropd (MONAI 0.5)
+ *   flip      bit 0/1/2 of `flip` mirrors spatial axis 0/1/2 inside the window   RandFlipd
+ *   normalize (x - mean) / std over the window's nonzero voxels, per channel, std 0 -> 1
+ *             (when `normalize`)                                   NormalizeIntensityd(nonzero, channel_wise)
+ *   scale     x * scale  (scale = 1 + factor, or 1)                RandScaleIntensityd
+ *   shift     x + shift on every voxel (or 0)                      RandShiftIntensityd
+ * out [B][C][h][w][d]; out_lab [B][3][h][w][d] = (TC: 2|3, WT: 1|2|3, ET: 2) as 0/1 floats --
+ * ConvertToMultiChannelBasedOnBratsClassesd, source_code/filters_and_operators.py:61-87.
+ * Driver call site: 10_scripts/127_gibbs_spikes_wraparound_sap_OneChannel/
+ * stylized_gibbs12p5_spikes15_wrap0p5_sap0p05_3modalities.py:151-170.  ws >= tb_brats_prep_workspace_bytes.
+ */
+typedef struct tb_prep_params {
+  int h0, w0, d0; /* crop corner */
+  int flip;       /* bit a: mirror spatial axis a */
+  float scale;    /* 1 + factor, or 1 */
+  float shift;    /* offset, or 0 */
+  int normalize;  /* 1: NormalizeIntensity(nonzero=True, channel_wise=True) */
+  int reserved;
+} tb_prep_params;
+size_t tb_brats_prep_workspace_bytes(int B, int C);
+int tb_brats_prep_f32(const float* img, const float* lab, int B, int C, int H0, int W0, int D0,
+                      const tb_prep_params* params, int h, int w, int d, float* out, float* out_lab, void* ws,
+                      size_t ws_bytes, void* stream);
+
+/*
  * Compiled plans: slab shapes with a compile-time FFT plan (W x D = 240 x 155, 128 x 128) run passes
  * A and C on dedicated persistent kernels; enable = 0 forces the generic run-time-planned passes
  * (same results to rounding).  Default on; TEXBIAS_COMPILED_PLANS=0 in the environment turns it off.

@@ -56,3 +56,9 @@ def programs_array(programs):
         for j, op in enumerate(prog):
             arr[b].op[j] = op
     return arr
+
+
+class TbPrepParams(C.Structure):
+    """tb_prep_params (include/texbias.h): one sample's preprocessing draws."""
+    _fields_ = [("h0", C.c_int), ("w0", C.c_int), ("d0", C.c_int), ("flip", C.c_int),
+                ("scale", C.c_float), ("shift", C.c_float), ("normalize", C.c_int), ("reserved", C.c_int)]

@@ -77,6 +77,20 @@ def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     return ws
 
 
+_ws_prep = {}
+
+
+def workspace_prep(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Small per-device workspace of the preprocessing statistics (kept apart from the spectrum
+    workspace so neither reallocates the other)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    ws = _ws_prep.get(idx)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", idx))
+        _ws_prep[idx] = ws
+    return ws
+
+
 def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 

@@ -296,9 +296,27 @@ def gen_chain():
             absk=k1[:, idx[0], idx[1], idx[2]].abs().numpy())
 
 
+def gen_labels():
+    """ConvertToMultiChannelBasedOnBratsClassesd (filters_and_operators.py:61-87) on BraTS-style
+    label maps (values 0..4; 4 is not a class of this dataset and maps to nothing)."""
+    rng = np.random.default_rng(41)
+    for i, shape in enumerate([(24, 20, 12), (1, 33, 17, 9)]):
+        lab = rng.integers(0, 5, size=shape).astype(np.float32)
+        t = fo.ConvertToMultiChannelBasedOnBratsClassesd(keys="label")
+        out = t({"label": lab})["label"]
+        put(f"labels_{i}", {"shape": list(shape)}, label=lab, out=out)
+
+
+GENERATORS = {"disk": "gen_disk", "planes": "gen_planes", "wrap": "gen_wrap", "sap": "gen_sap",
+              "gibbs": "gen_gibbs", "spikes": "gen_spikes", "layers": "gen_layers", "chain": "gen_chain",
+              "labels": "gen_labels"}
+
+
 def main():
-    for g in (gen_disk, gen_planes, gen_wrap, gen_sap, gen_gibbs, gen_spikes, gen_layers, gen_chain):
-        g()
+    """All generators, or only those named on the command line (e.g. ``make_golden.py labels``)."""
+    names = sys.argv[1:] or list(GENERATORS)
+    for n in names:
+        globals()[GENERATORS[n]]()
     groups = {}
     for name, (meta, arrays) in CASES.items():
         groups.setdefault(name.split("_")[0], {})[name] = (meta, arrays)
