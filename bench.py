@@ -42,10 +42,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=("c3", "c2"), default="c3",
+    ap.add_argument("--config", choices=("c3", "c2", "c5"), default="c3",
                     help="c3: full filter chain + U-Net train step on 4x240x240x155 (the headline); "
-                         "c2: Gibbs truncation (disk low-pass r=12.5) alone on 4x128x128x128 (BASELINE config 2)")
-    ap.add_argument("--batch", type=int, default=None, help="volumes per GPU per step (c3: 2, c2: 16)")
+                         "c2: Gibbs truncation (disk low-pass r=12.5) alone on 4x128x128x128 (BASELINE config 2); "
+                         "c5: DCGAN step on filtered 1x128x128 BraTS slices, bf16 (BASELINE config 5)")
+    ap.add_argument("--batch", type=int, default=None, help="volumes (c5: slices) per GPU per step (c3: 2, c2: 16, c5: 64)")
+    ap.add_argument("--fp32", action="store_true", help="c5: run the networks in fp32 instead of bf16 autocast")
     ap.add_argument("--shape", type=str, default=None, help="c3: 240,240,155; c2: 128,128,128")
     ap.add_argument("--pad-to", type=int, default=None, help="U-Net D extent (c3: 160, G10: 155 is not /16)")
     ap.add_argument("--random-filters", action="store_true")
@@ -59,11 +61,13 @@ def parse():
     ap.add_argument("--cpu-cores", type=int, default=None, help="CPU baseline core count (default: the job's share)")
     ap.add_argument("--filter-only", action="store_true", help="diagnostic: time the filter chain alone")
     a = ap.parse_args()
-    c2 = a.config == "c2"
-    a.batch = a.batch or (16 if c2 else 2)
-    a.shape = a.shape or ("128,128,128" if c2 else "240,240,155")
+    c2, c5 = a.config == "c2", a.config == "c5"
+    a.batch = a.batch or (16 if c2 else 64 if c5 else 2)
+    a.shape = a.shape or ("128,128,128" if c2 else "1,128,128" if c5 else "240,240,155")
     if a.pad_to is None:
-        a.pad_to = 0 if c2 else 160
+        a.pad_to = 0 if (c2 or c5) else 160
+    if c5:
+        a.no_cpu_baseline = True  # the reference trains its DCGAN on the GPU; no CPU path to time
     a.cpu_sample_vols = a.cpu_sample_vols or (8 if c2 else 1)
     if c2:
         a.filter_only = True  # config 2 is the filter kernel alone
@@ -145,7 +149,7 @@ def main():
         print(f"[bench] world size {world} (backend {dist.get_backend() if world > 1 else 'none'})",
               file=sys.stderr, flush=True)
     dev = torch.device("cuda", local)
-    B, C = args.batch, 4
+    B, C = args.batch, (1 if args.config == "c5" else 4)
     pad = max(0, args.pad_to - D)
     torch.manual_seed(1000 + rank)
 
@@ -158,6 +162,8 @@ def main():
     disk, planes, wrap, sap = tr["disk"], tr["planes"], tr["wrap"], tr["sap"]
     if args.config == "c2":
         chain = FusedChain([disk])
+    elif args.config == "c5":  # 2-D slices [B, 1, 1, 128, 128]: the plane-wave shell does not fit
+        chain = FusedChain([disk, wrap, sap])
     prs = np.random.RandomState(12345 + rank)
 
     def randomize_filters():
@@ -167,7 +173,13 @@ def main():
         sap.p = float(prs.uniform(0.05, 0.35))
 
     step_fn = None
-    if not args.filter_only:
+    if args.config == "c5":
+        from texbias.dcgan import DCGANStep
+        torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
+        torch.manual_seed(0)  # identical network init on every rank
+        step_fn = DCGANStep(dev, distributed=world > 1, bf16=not args.fp32)
+        torch.manual_seed(1000 + rank)
+    elif not args.filter_only:
         torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
         step_fn = TrainStep(reference_model(C, 3), dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb,
                             channels_last=args.channels_last)
@@ -176,6 +188,8 @@ def main():
         if args.random_filters:
             randomize_filters()
         y = chain(pool[i % 2], pad=pad)
+        if args.config == "c5":
+            return step_fn(y.view(B, 1, W, D))
         if step_fn is not None:
             return step_fn(y, labels[i % 2])
         return y
@@ -258,6 +272,25 @@ def main():
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),
         }
+        if args.config == "c5":
+            from texbias.dcgan import step_flops
+            fl = step_flops() * B  # per rank and step (analytic: 3x forward per backward pass)
+            tfs = fl / (elapsed / args.steps) / 1e12
+            line.update({
+                "unit": "slices/s", "dtype": "f32" if args.fp32 else "bf16",
+                "data": "synthetic BraTS-like 1x128x128 slices resident in HBM, filtered on the GPU each step; "
+                        "random-init DCGAN (N(0, 0.02) init)",
+            })
+            line["config"] = {
+                "workload": "C5 DCGAN (50_reconstruction/networks.py, nz=100, ngf=ndf=128) step: D on real + D on G(z) "
+                            "+ Adam(2e-4, 0.5), G through the updated D + Adam; input slices filtered by disk 12.5 -> "
+                            "wrap 0.5 -> S&P 0.05 on the GPU" + (" [fp32]" if args.fp32 else " [bf16 autocast]"),
+                "slice": [1, W, D], "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"}
+            line["roofline"] = {"kernel": "DCGAN step (MIOpen/hipBLASLt convolutions)", "bound": "mfma",
+                                "achieved": round(tfs, 2), "peak": 2500.0 if not args.fp32 else 157.3,
+                                "unit": "TFLOP/s", "frac": round(tfs / (2500.0 if not args.fp32 else 157.3), 4),
+                                "traffic": None, "algorithmic_flops_per_step": fl,
+                                "note": "analytic conv flops / measured step time (whole step, not one kernel)"}
         if cpu_line is not None:
             line["cpu_baseline"] = cpu_line
         print(json.dumps(line), flush=True)

@@ -15,7 +15,8 @@ import torch.nn.functional as F
 
 
 def _brain_mask(spatial: Sequence[int], device) -> torch.Tensor:
-    axes = [torch.linspace(-1, 1, n, device=device) for n in spatial]
+    # a size-1 axis (2-D slices as [1, H, W]) sits at the centre
+    axes = [torch.linspace(-1, 1, n, device=device) if n > 1 else torch.zeros(1, device=device) for n in spatial]
     g = torch.meshgrid(*axes, indexing="ij")
     r2 = sum((a / s) ** 2 for a, s in zip(g, (0.85, 0.8, 0.9)))
     return r2 < 1.0
