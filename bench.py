@@ -177,7 +177,7 @@ def main():
         from texbias.dcgan import DCGANStep
         torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
         torch.manual_seed(0)  # identical network init on every rank
-        step_fn = DCGANStep(dev, distributed=world > 1, bf16=not args.fp32)
+        step_fn = DCGANStep(dev, distributed=world > 1, bf16=not args.fp32, channels_last=args.channels_last)
         torch.manual_seed(1000 + rank)
     elif not args.filter_only:
         torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
@@ -284,7 +284,8 @@ def main():
             line["config"] = {
                 "workload": "C5 DCGAN (50_reconstruction/networks.py, nz=100, ngf=ndf=128) step: D on real + D on G(z) "
                             "+ Adam(2e-4, 0.5), G through the updated D + Adam; input slices filtered by disk 12.5 -> "
-                            "wrap 0.5 -> S&P 0.05 on the GPU" + (" [fp32]" if args.fp32 else " [bf16 autocast]"),
+                            "wrap 0.5 -> S&P 0.05 on the GPU" + (" [fp32]" if args.fp32 else " [bf16 autocast]")
+                            + (" [channels_last]" if args.channels_last else ""),
                 "slice": [1, W, D], "per_gpu_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"}
             line["roofline"] = {"kernel": "DCGAN step (MIOpen/hipBLASLt convolutions)", "bound": "mfma",
                                 "achieved": round(tfs, 2), "peak": 2500.0 if not args.fp32 else 157.3,

@@ -75,11 +75,14 @@ class DCGANStep:
     and after the D step) as device tensors."""
 
     def __init__(self, device: torch.device, nz: int = 100, ngf: int = 128, ndf: int = 128, nc: int = 1,
-                 lr: float = 2e-4, beta1: float = 0.5, distributed: bool = False, bf16: bool = True):
-        self.device, self.nz, self.bf16 = device, nz, bf16
+                 lr: float = 2e-4, beta1: float = 0.5, distributed: bool = False, bf16: bool = True,
+                 channels_last: bool = False):
+        self.device, self.nz, self.bf16, self.channels_last = device, nz, bf16, channels_last
         G, D = Generator(nz, ngf, nc).to(device), Discriminator(nc, ndf).to(device)
         G.apply(weights_init)
         D.apply(weights_init)
+        if channels_last:  # NHWC activations and weights (MIOpen's preferred layout for bf16)
+            G, D = G.to(memory_format=torch.channels_last), D.to(memory_format=torch.channels_last)
         self.G_module, self.D_module = G, D
         if distributed:
             kw = dict(broadcast_buffers=False)  # BatchNorm running stats stay per rank (training uses batch stats)
@@ -106,6 +109,8 @@ class DCGANStep:
 
     def __call__(self, real: torch.Tensor, noise: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
         b = real.size(0)
+        if self.channels_last:
+            real = real.contiguous(memory_format=torch.channels_last)
         ones = torch.ones((b,), dtype=torch.float32, device=real.device)
         zeros = torch.zeros((b,), dtype=torch.float32, device=real.device)
         if noise is None:
