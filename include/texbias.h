@@ -166,6 +166,12 @@ int tb_conv3d_wgrad_config(int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
  */
 int tb_dice_sums_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, int sigmoid, int squared,
                      void* stream);
+/*
+ * Dice METRIC statistics of the reference's evaluation loop (source_code/utils.py:313-411:
+ * Activations(sigmoid=True) + AsDiscrete(threshold 0.5) then DiceMetric(include_background)):
+ * sums[nc] = {sum t p, sum t, sum p} over S voxels with p = (sigmoid(x) >= 0.5) in {0, 1}.
+ */
+int tb_dice_metric_sums_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, void* stream);
 int tb_dice_sums_bwd_f32(const float* x, const float* t, const float* g, float* dx, int64_t NC, int64_t S, int sigmoid,
                          int squared, void* stream);
 

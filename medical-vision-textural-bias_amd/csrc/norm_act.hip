@@ -147,7 +147,8 @@ __global__ __launch_bounds__(NT) void k_dice_sums(const float* __restrict__ x, c
   const Chunk c = chunk_of(S);
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
   auto add1 = [&](float xv, float tv) {
-    const float p = (flags & 1) ? sigm(xv) : xv;
+    float p = (flags & 1) ? sigm(xv) : xv;
+    if (flags & 4) p = p >= 0.5f ? 1.f : 0.f;  // the metric's AsDiscrete(threshold 0.5)
     a0 += tv * p;
     if (flags & 2) {
       a1 += tv * tv;
@@ -409,6 +410,18 @@ int tb_dice_sums_f32(const float* x, const float* t, double* sums, int64_t NC, i
   const int vec = (S % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(t) & 15) == 0);
   const dim3 grid((unsigned)((S + CHUNK - 1) / CHUNK), (unsigned)NC);
   hipLaunchKernelGGL(k_dice_sums, grid, dim3(NT), 0, st, x, t, sums, S, (sigmoid ? 1 : 0) | (squared ? 2 : 0), vec);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+// Dice metric statistics of the reference's evaluation (utils.py:313-411: Activations(sigmoid) +
+// AsDiscrete(threshold 0.5), then DiceMetric): per instance {sum t p, sum t, sum p}, p in {0, 1}.
+int tb_dice_metric_sums_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, void* stream) {
+  if (!x || !t || !sums || NC < 1 || S < 1 || NC > 65535) return TB_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(sums, 0, sizeof(double) * 3 * (size_t)NC, st) != hipSuccess) return TB_ERR_HIP;
+  const int vec = (S % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  const dim3 grid((unsigned)((S + CHUNK - 1) / CHUNK), (unsigned)NC);
+  hipLaunchKernelGGL(k_dice_sums, grid, dim3(NT), 0, st, x, t, sums, S, 1 | 4, vec);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
