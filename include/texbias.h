@@ -51,6 +51,10 @@ extern "C" {
                          f[1] = phase override or NaN (keep own phase); f[2],f[3] = cos,sin(f[1]);
                          reserved = 1: same KSpaceSpikeNoise call as the previous SPIKE op (all
                          spikes of one call read the spectrum from before the call)          */
+#define TB_OP_ZF 6    /* random k-space undersampling (RandZF, 50_reconstruction/reconGan/utils2.py:34-74):
+                         coefficient (c, kh, kw, kd) (UNSHIFTED) is kept iff u > f[0] = p, with
+                         u = (splitmix64(idx ^ l) >> 40) / 2^24, idx = ((c H + kh) i[1] + kw) i[2] + kd,
+                         i[1] = W, i[2] = D, l = splitmix64(seed) (host); applied as (m(f) + m(-f)) / 2 */
 
 #define TB_MAX_OPS 6
 #define TB_MAX_BATCH 8 /* samples per launch group; larger batches are split by the library */

@@ -591,6 +591,18 @@ TB_HD cf spike_target(const tb_op& op, cf kf) {
   return mk(op.f[0] * op.f[2], op.f[0] * op.f[3]);  // host passes cos/sin of the override
 }
 
+// RandZF draw of one unshifted coefficient: kept iff u > p (utils2.py:70-72 zeroes u <= p)
+TB_HD uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+TB_HD float zf_keep(const tb_op& op, uint64_t idx) {
+  const float u = (float)(splitmix64(idx ^ (uint64_t)op.l) >> 40) * (1.0f / 16777216.0f);
+  return u > op.f[0] ? 1.f : 0.f;
+}
+
 // Apply a sample's op program to one stored half-spectrum coefficient.
 // Every op is followed by the reference's `.real` (G4: Hermitian symmetrisation);
 // on a half spectrum that is exact for symmetric masks, needs (M(f)+M(-f))/2 for
@@ -644,6 +656,12 @@ TB_HD cf apply_ops(const SO& so, int chan, cf v, const FreqCol& fc, int kh, int 
           const cf d = sub(spike_target(op, kf), kf);
           v = add(v, scl(conj(d), 0.5f));
         }
+      } break;
+      case TB_OP_ZF: {  // independent draws at f and -f: the .real symmetrises them
+        const uint64_t Wz = (uint64_t)op.i[1], Dz = (uint64_t)op.i[2], ch = (uint64_t)chan * (uint64_t)H;
+        const float m = 0.5f * (zf_keep(op, ((ch + (uint64_t)kh) * Wz + (uint64_t)fc.kw) * Dz + (uint64_t)fc.kd) +
+                                zf_keep(op, ((ch + (uint64_t)h.nk) * Wz + (uint64_t)fc.nkw) * Dz + (uint64_t)fc.nkd));
+        v = scl(v, m);
       } break;
       default: break;
     }

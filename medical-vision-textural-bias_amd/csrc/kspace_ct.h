@@ -100,6 +100,17 @@ TB_HD void ops_bfly(const SO& so, int chan, v2* v, const FreqCol& fc, int kh0, i
           }
         }
       } break;
+      case TB_OP_ZF: {
+        const uint64_t Wz = (uint64_t)op.i[1], Dz = (uint64_t)op.i[2], ch = (uint64_t)chan * (uint64_t)H;
+        TB_UNROLL
+        for (int q = 0; q < R; ++q) {
+          const int kh = kh0 + kst * q;
+          const float m = 0.5f * (zf_keep(op, ((ch + (uint64_t)kh) * Wz + (uint64_t)fc.kw) * Dz + (uint64_t)fc.kd) +
+                                  zf_keep(op, ((ch + (uint64_t)negk(kh, H)) * Wz + (uint64_t)fc.nkw) * Dz +
+                                              (uint64_t)fc.nkd));
+          v[q] = m * v[q];
+        }
+      } break;
       default: break;
     }
   }

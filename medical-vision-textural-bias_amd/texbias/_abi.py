@@ -18,6 +18,7 @@ TB_OP_DISK = 1
 TB_OP_GIBBS = 2
 TB_OP_LAYER = 3
 TB_OP_WRAP = 4
+TB_OP_ZF = 6
 TB_OP_SPIKE = 5
 
 TB_MAX_OPS = 6

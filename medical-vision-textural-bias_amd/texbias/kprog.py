@@ -22,7 +22,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from ._abi import (TB_OP_DISK, TB_OP_GIBBS, TB_OP_LAYER, TB_OP_SPIKE, TB_OP_WRAP, TbOp)
+from ._abi import (TB_OP_DISK, TB_OP_GIBBS, TB_OP_LAYER, TB_OP_SPIKE, TB_OP_WRAP, TB_OP_ZF, TbOp)
 
 
 @dataclass(frozen=True)
@@ -151,6 +151,29 @@ def wrap_op(alpha: float) -> TbOp:
     """WrapArtifact (filters_and_operators.py:509-511)."""
     op = _op(TB_OP_WRAP)
     op.f[0] = np.float32(alpha)
+    return op
+
+
+# ---------------------------------------------------------------------- ZF
+_M64 = (1 << 64) - 1
+
+
+def splitmix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def zf_op(p: float, seed: int, spatial3: Sequence[int]) -> TbOp:
+    """RandZF (50_reconstruction/reconGan/utils2.py:34-74): each k-space coefficient zeroed with
+    probability p (u <= p), u from a counter-based hash of (seed, channel, frequency) -- see
+    TB_OP_ZF in include/texbias.h.  ``spatial3`` = the (H, W, D) geometry of the transform."""
+    op = _op(TB_OP_ZF)
+    op.f[0] = np.float32(min(max(0.0, float(p)), 1.0))
+    op.i[1], op.i[2] = int(spatial3[1]), int(spatial3[2])
+    k = splitmix64(int(seed) & _M64)
+    op.l = k - (1 << 64) if k >= (1 << 63) else k   # int64 field, same bits
     return op
 
 

@@ -219,3 +219,30 @@ def chain(x: np.ndarray, r, idx, intensity: float, alpha: float, p: float, u: np
     y3 = wrap_artifact(y2, alpha)
     y, cls = salt_and_pepper(y3, p, u)
     return y1, y2, y3, y, cls
+
+
+# 50_reconstruction/reconGan/utils2.py:34-74 (RandZF): full spectrum, k[u <= p] = 0, inverse .real.
+# The mask is given (``keep`` in the fftshift-ed layout of k); ``zf_keep_mask`` replays the device
+# stream of TB_OP_ZF (include/texbias.h) for the parity tests.
+def rand_zf(x: np.ndarray, keep: np.ndarray) -> np.ndarray:
+    n = x.ndim - 1
+    k = shift_fourier(x, n)
+    k = np.where(keep, k, np.complex64(0)).astype(np.complex64)
+    return inv_shift_fourier(k, n)
+
+
+def _splitmix64(z: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def zf_keep_mask(shape: Sequence[int], p: float, seed: int) -> np.ndarray:
+    """bool [C, *spatial] in the fftshift-ed layout: coefficient kept iff u > p."""
+    key = _splitmix64(np.array([seed], dtype=np.uint64))[0]
+    idx = np.arange(int(np.prod(shape)), dtype=np.uint64).reshape(tuple(shape))  # unshifted frequencies
+    u = (_splitmix64(idx ^ key) >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    keep = u > np.float32(min(max(0.0, p), 1.0))
+    return np.fft.fftshift(keep, axes=tuple(range(1, len(shape))))

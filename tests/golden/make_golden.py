@@ -307,9 +307,23 @@ def gen_labels():
         put(f"labels_{i}", {"shape": list(shape)}, label=lab, out=out)
 
 
+def gen_zf():
+    """RandZF (50_reconstruction/reconGan/utils2.py:34-74) on 2-D slices and a 3-D volume, with
+    the uniform field it drew (replayed from the same torch seed) so the oracle can be pinned."""
+    sys.path.insert(0, os.path.join(os.path.dirname(REF), "50_reconstruction", "reconGan"))
+    import utils2  # noqa: E402
+    for i, (shape, p) in enumerate([((1, 32, 28), 0.3), ((2, 16, 12, 10), 0.6)]):
+        x = brats_like(shape, 50 + i)
+        torch.manual_seed(1234 + i)
+        y = utils2.RandZF(p)(torch.from_numpy(x))
+        torch.manual_seed(1234 + i)
+        u = torch.rand(shape)  # the draw inside rand_mask (k has the image's shape)
+        put(f"zf_{i}", {"p": p}, x=x, u=u.numpy(), y=y.numpy())
+
+
 GENERATORS = {"disk": "gen_disk", "planes": "gen_planes", "wrap": "gen_wrap", "sap": "gen_sap",
               "gibbs": "gen_gibbs", "spikes": "gen_spikes", "layers": "gen_layers", "chain": "gen_chain",
-              "labels": "gen_labels"}
+              "labels": "gen_labels", "zf": "gen_zf"}
 
 
 def main():
