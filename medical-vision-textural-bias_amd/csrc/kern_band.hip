@@ -107,9 +107,9 @@ __device__ __forceinline__ void lds_fill(T* dst, const T* __restrict__ src, int 
   for (int base = 0; base < n; base += U * BAND_NT) {
     T v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) {  // clamped index: every lane loads, no divergent partial array
       const int i = base + u * BAND_NT + tid;
-      if (i < n) v[u] = src[i];
+      v[u] = src[i < n ? i : n - 1];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {

@@ -47,6 +47,29 @@ __global__ void p_lanerow(float* y) {
   }
 }
 
+// P3: MFMA-layout values staged through LDS per half-tile (as pass C'), then row-segment stores
+__global__ __launch_bounds__(256) void p_staged(float* y, int nhalf) {
+  __shared__ __attribute__((aligned(16))) float stg_all[4][32 * 36];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l31 = lane & 31, hl = lane >> 5, c4 = lane & 7;
+  float* stg = stg_all[wv];
+  for (long u = blockIdx.x * 4L + wv; u < UNITS; u += gridDim.x * 4L) {
+    float* t = y + u * TR * ROWP;
+    for (int h = 0; h < nhalf; ++h) {
+      const int ch = h % 5;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(stg + l31 * 36 + 8 * g + 4 * hl) = f32x4{(float)g, 1.f, 2.f, (float)h};
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = (lane >> 3) + 8 * k;
+        *reinterpret_cast<f32x4*>(t + r * ROWP + ch * 32 + 4 * c4) = *reinterpret_cast<const f32x4*>(stg + r * 36 + 4 * c4);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
 int main() {
   const long n = UNITS * TR * ROWP;
   float* y;
@@ -68,7 +91,10 @@ int main() {
   };
   run("linear fill 4096x256", [&] { p_linear<<<4096, 256>>>((f32x4*)y, n / 4); });
   run("linear fill 1024x256", [&] { p_linear<<<1024, 256>>>((f32x4*)y, n / 4); });
-  for (int g : {768, 1024, 2048}) {
+  run("staged 5 halves G=768", [&] { p_staged<<<768, 256>>>(y, 5); });
+  run("staged 6 halves G=768", [&] { p_staged<<<768, 256>>>(y, 6); });
+  run("staged 5 halves G=1024", [&] { p_staged<<<1024, 256>>>(y, 5); });
+  for (int g : {768, 1024}) {
     char b[64];
     snprintf(b, 64, "rowseg chunk-major G=%d", g);
     run(b, [&] { p_rowseg<<<g, 256>>>(y, 0); });
