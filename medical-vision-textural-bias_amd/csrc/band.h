@@ -109,7 +109,7 @@ TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
   return (size_t)band_fwd_xn(P, NT2, KWT) * 4 + (size_t)W * 8 + (size_t)NT2 * KSd * 128 * 4;
 }
 constexpr int BAND_STG_P = 36;  // pitch (floats) of a wave's staged 32 x 32 output half-tile
-constexpr int BAND_SLOTS = 2;   // slabs whose pass-C' inputs a workgroup holds in LDS at once
+constexpr int BAND_SLOTS = 3;   // slabs whose pass-C' inputs a workgroup holds in LDS at once
 struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
   int bimg, tww, frag, prow, stg, total;
 };

@@ -483,14 +483,22 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int ypad = a.ypad;
   const int diag = a.diag;
   const bool mal = ((D - 3) & 3) == 0;  // mirrored 4-column groups start 16-B aligned
-  for (int k0 = 0;; k0 += BAND_SLOTS) {
-    const int u0 = (int)blockIdx.x + k0 * (int)gridDim.x;
-    if (u0 >= nslab) break;
-    int nb = 0;
-    while (nb < BAND_SLOTS && u0 + nb * (int)gridDim.x < nslab) ++nb;
+  // Each workgroup owns a contiguous range of (slab, row tile) units, dealt round-robin to its
+  // waves, so every wave of the grid gets the same number of units (a slab-granular split left
+  // half the workgroups with 3 slabs and half with 2); the range's slabs are loaded in batches of
+  // up to BAND_SLOTS.
+  const int nunit = nslab * ntw;
+  const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int ub = (int)blockIdx.x * per, ue = ub + per < nunit ? ub + per : nunit;
+  for (int c0 = ub; c0 < ue;) {
+    const int s0 = c0 / ntw;
+    const int slast = (ue - 1) / ntw;
+    const int s1 = slast < s0 + BAND_SLOTS - 1 ? slast : s0 + BAND_SLOTS - 1;
+    const int c1 = (s1 + 1) * ntw < ue ? (s1 + 1) * ntw : ue;  // units [c0, c1) of this batch
+    const int nb = s1 - s0 + 1;
     __syncthreads();  // the previous batch is done with Fs / Ps
     for (int i = 0; i < nb; ++i) {
-      const int slab = u0 + i * (int)gridDim.x;
+      const int slab = s0 + i;
       lds_fill<2>(reinterpret_cast<float4*>(Fs + i * fsz), reinterpret_cast<const float4*>(a.M2F + (int64_t)slab * fsz),
                   fsz / 4, tid);
       const BandSamplePts& sp = a.sp[(a.cofs + slab / H) / a.C];
@@ -515,9 +523,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
       }
     }
     __syncthreads();
-    for (int un = wv; un < nb * ntw; un += 4) {
-      const int slot = un / ntw, tw_ = un - slot * ntw;
-      const int slab = u0 + slot * (int)gridDim.x;
+    for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {  // (un - ub) % 4 == wave
+      const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
       const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
       const BandSamplePts& sp = a.sp[(a.cofs + bcl) / a.C];
       const float* F = Fs + slot * fsz + lane;  // fragment of (vt, ks): F[(vt KV + ks) 64]
@@ -658,6 +665,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
         if (lane == 0) a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
       }
     }
+    c0 = c1;
   }
 }
 
