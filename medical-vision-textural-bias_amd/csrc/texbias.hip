@@ -726,36 +726,51 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
   for (int b = 0; b < B; ++b)
     if (ops[b].n < 0 || ops[b].n > TB_MAX_OPS) return TB_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (minmax) {
-    hipLaunchKernelGGL(k_minmax_init, dim3((B + 255) / 256), dim3(256), 0, st, minmax, B);
-    TB_HIP(hipGetLastError());
-  }
   // Runs of consecutive samples with the same route, in launch groups of <= TB_MAX_BATCH samples
   // (the op programs travel in the kernel arguments): empty programs are copied through (the
   // reference returns the input untouched), low-pass programs take the band passes A'/B'/C',
-  // the rest the full-spectrum passes A/B/C.
+  // the rest the full-spectrum passes A/B/C.  Routes are planned first: the band passes write
+  // their samples' min/max keys outright, the others accumulate them atomically from a reset.
+  struct Run {
+    int s0, s1, route;
+    BandGeo g;
+    BandSamplePts sp[TB_MAX_BATCH];
+  };
+  std::vector<Run> runs;
+  bool atomic_keys = false;
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
     int i = 0;
     while (i < nb) {
       auto route = [&](int s) { return ops[s].n == 0 ? RUN_COPY : RUN_FULL; };
-      const int r = route(b0 + i);
+      Run run;
+      run.route = route(b0 + i);
       int j = i + 1;
-      while (j < nb && route(b0 + j) == r) ++j;
-      int rc = TB_OK;
-      if (r == RUN_COPY) {
-        rc = run_copy(p, x, xs, y, ys, y_pad, b0 + i, j - i, C, minmax, st);
-      } else {
-        BandGeo g;
-        BandSamplePts sp[TB_MAX_BATCH];
-        if (g_band && band_plan(p, ops, b0 + i, b0 + j, y_pad, ws_bytes, B * C, g, sp))
-          rc = run_band(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, b0 + i, j - i, C, ops, g, sp, minmax, st);
-        else
-          rc = run_full<RA, RB>(p, x, xs, y, ys, y_pad, static_cast<cf*>(ws), b0 + i, j - i, C, ops, minmax, st);
-      }
-      if (rc) return rc;
+      while (j < nb && route(b0 + j) == run.route) ++j;
+      run.s0 = b0 + i;
+      run.s1 = b0 + j;
+      if (run.route == RUN_FULL && g_band && band_plan(p, ops, run.s0, run.s1, y_pad, ws_bytes, B * C, run.g, run.sp))
+        run.route = RUN_BAND;
+      atomic_keys |= run.route != RUN_BAND;
+      runs.push_back(run);
       i = j;
     }
+  }
+  if (minmax && atomic_keys) {
+    hipLaunchKernelGGL(k_minmax_init, dim3((B + 255) / 256), dim3(256), 0, st, minmax, B);
+    TB_HIP(hipGetLastError());
+  }
+  for (const Run& run : runs) {
+    const int nb = run.s1 - run.s0;
+    int rc = TB_OK;
+    if (run.route == RUN_COPY)
+      rc = run_copy(p, x, xs, y, ys, y_pad, run.s0, nb, C, minmax, st);
+    else if (run.route == RUN_BAND)
+      rc = run_band(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, run.s0, nb, C, ops, run.g, run.sp, minmax,
+                    st);
+    else
+      rc = run_full<RA, RB>(p, x, xs, y, ys, y_pad, static_cast<cf*>(ws), run.s0, nb, C, ops, minmax, st);
+    if (rc) return rc;
   }
   return TB_OK;
 }
