@@ -150,6 +150,7 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
 hipError_t launch_band_fwd(const BandFwdArgs& a, int ncu, hipStream_t st);
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st);
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);
+hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st);
 
 // identity samples (empty program): strided copy + zero D-padding + min/max
 struct CopyArgs {

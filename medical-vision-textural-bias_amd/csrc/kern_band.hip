@@ -497,29 +497,31 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
     const int c1 = (s1 + 1) * ntw < ue ? (s1 + 1) * ntw : ue;  // units [c0, c1) of this batch
     const int nb = s1 - s0 + 1;
     __syncthreads();  // the previous batch is done with Fs / Ps
-    for (int i = 0; i < nb; ++i) {
-      const int slab = s0 + i;
-      lds_fill<2>(reinterpret_cast<float4*>(Fs + i * fsz), reinterpret_cast<const float4*>(a.M2F + (int64_t)slab * fsz),
-                  fsz / 4, tid);
-      const BandSamplePts& sp = a.sp[(a.cofs + slab / H) / a.C];
-      const int nc4 = NCOL / 4;
-      float4 v[2];
+    {  // the batch's fragments (contiguous slabs) and point rows in one round of loads in flight
+      const int nf4 = nb * fsz / 4, np4 = nb * psz / 4, ntot = nf4 + np4, nc4 = NCOL / 4, pp4 = psz / 4;
+      const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
+      for (int base = 0; base < ntot; base += 6 * BAND_NT) {
+        float4 v[6];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {  // psz / 4 <= 2 BAND_NT for the launches band_plan admits
-        const int e = u * BAND_NT + tid;
-        const int r = e / nc4, n = e - r * nc4, j = r >> 1;
-        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e < psz / 4 && j < sp.n)
-          v[u] = reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n];
-      }
+        for (int u = 0; u < 6; ++u) {
+          const int e = base + u * BAND_NT + tid;
+          if (e < nf4 || e >= ntot) {
+            v[u] = F4[e < nf4 ? e : 0];
+          } else {
+            const int q = e - nf4, i = q / pp4, rem = q - i * pp4, r = rem / nc4, n = rem - r * nc4, j = r >> 1;
+            const BandSamplePts& sp = a.sp[(a.cofs + (s0 + i) / H) / a.C];
+            v[u] = j < sp.n ? reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n]
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (u * BAND_NT + tid < psz / 4) reinterpret_cast<float4*>(Ps + i * psz)[u * BAND_NT + tid] = v[u];
-      for (int e = 2 * BAND_NT + tid; e < psz / 4; e += BAND_NT) {  // larger point sets: plain loop
-        const int r = e / nc4, n = e - r * nc4, j = r >> 1;
-        reinterpret_cast<float4*>(Ps + i * psz)[e] =
-            j < sp.n ? reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n]
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 0; u < 6; ++u) {
+          const int e = base + u * BAND_NT + tid;
+          if (e < nf4)
+            reinterpret_cast<float4*>(Fs)[e] = v[u];
+          else if (e < ntot)
+            reinterpret_cast<float4*>(Ps)[e - nf4] = v[u];
+        }
       }
     }
     __syncthreads();
@@ -812,9 +814,11 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
 
 
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
-  const hipError_t e = 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
-  if (e != hipSuccess || !a.mm) return e;
-  hipLaunchKernelGGL(k_band_minmax, dim3(a.nbc / a.C), dim3(256), 0, st, a.mmp, a.mm, a.bc0, a.C, a.pl.H, a.pl.W);
+  return 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
+}
+
+hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(k_band_minmax, dim3(nbc / C), dim3(256), 0, st, mmp, mm, bc0, C, H, W);
   return hipGetLastError();
 }
 
