@@ -8,10 +8,12 @@
 // output spectrum lives in a small box around DC plus a handful of spike points, and the full
 // mixed-radix FFT round trip (passes A/B/C, 32 B/voxel of HBM traffic) is replaced by:
 //
-//   A' k_band_fwd   per (bc, h) slab, 64-row chunks staged in LDS: pruned real DFT along D
-//                   (kd in [0, NDk), d-symmetric, twiddles from scalar loads), then pruned DFT
-//                   along W (kw in [-KW, KW]) accumulated in registers over the chunks;
-//                   writes P[bc][h][NW][NDk].  Reads the image once.
+//   A' k_band_fwd   per 16-row strip of a (bc, h) slab, each wave streaming its own contiguous,
+//                   balanced range of strips (next strip prefetched into registers, staged in the
+//                   wave's own LDS region, no workgroup barriers): pruned real DFT along D (kd in
+//                   [0, NDk), d-symmetric, MFMA) then pruned DFT along W (kw in [-KW, KW]) accumulated
+//                   in registers; a slab shared by several waves gets one partial sum per wave
+//                   (P[bc][h][seg][NW][NDk], seg < BAND_FWD_SEGS) that pass B' adds.  Reads the image once.
 //   B' k_band_mid   per (bc, kh, 64 columns): pruned DFT along H (kh and -kh at once), the
 //                   sample's op program (apply_ops, the same code as pass B) on every box
 //                   coefficient, stored as the kh/-kh sum and difference AB[bc][kh][col]; the
@@ -53,17 +55,34 @@ struct BandGeo {
   int NCOL;         // folded output columns of the MFMA n-tiles: 32 * ceil((D/2 + 1) / 32)
 };
 
+// Pass A''s division of the launch's T = slabs x nst 16-row strips among G waves: wave w takes
+// strips [w T / G, (w + 1) T / G).  G <= T / ceil(nst / 2), so a slab spans at most 3 waves.
+// (T + 1) G < 2^32 (host-checked): 32-bit arithmetic.
+constexpr int BAND_FWD_SEGS = 3;
+constexpr int BAND_FWD_ROWS = 16;  // rows per strip (one per lane of a 16x16x4 MFMA row)
+struct FwdSplit {
+  uint32_t T, G, nst;
+};
+TB_HD uint32_t fwd_start(const FwdSplit& s, uint32_t w) { return w * s.T / s.G; }
+TB_HD uint32_t fwd_wave_of(const FwdSplit& s, uint32_t t) { return ((t + 1) * s.G - 1) / s.T; }
+// partial sums of a slab = waves that hold one of its strips
+TB_HD int fwd_nseg(const FwdSplit& s, uint32_t slab) {
+  return (int)(fwd_wave_of(s, slab * s.nst + s.nst - 1) - fwd_wave_of(s, slab * s.nst)) + 1;
+}
+
 struct BandFwdArgs {
   tb_plan_dev pl;
   const float* x;
   int64_t sbc, sh, sw;
-  cf* P;            // [bc][H][ncol]  (bc absolute)
+  cf* P;            // [bc][H][BAND_FWD_SEGS][ncol] partial sums (bc absolute)
   const float2* tdf;  // [d][NKP] = (cos, sin)(2 pi kd d / D), d in [0, D/2]
   int NKP;
   int bc0, nbc;
   BandGeo g;
   int diag;         // measurement only (TEXBIAS_BAND_DIAG): skip stages, results invalid
   const float* tbt; // [2][KSd][2][64] B fragments of the folded D product (plan table)
+  FwdSplit split;   // set by launch_band_fwd
+  int vec;          // contiguous 16-B aligned rows (sw == D, 16-B aligned base and slab strides)
 };
 
 struct BandMidArgs {
@@ -75,6 +94,7 @@ struct BandMidArgs {
   float scale;      // 1 / (H W D)
   int bc0, C, cofs, nbc;
   BandGeo g;
+  FwdSplit split;   // pass A''s strip division (how many partial sums each slab has)
   BandSamplePts sp[TB_MAX_BATCH];
   BatchOps ops;
 };
@@ -96,20 +116,27 @@ struct BandInvArgs {
   const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
 };
 
-// floats of pass A's X region: the 64-row chunk (+8 slack), reused at slab end for the four
-// waves' O partials [wave][cos/sin][re/im][KWT][NT2][64 lanes][4] -- whichever is larger
-TB_HD int band_fwd_xn(int P, int NT2, int KWT) {
-  const int xn = BAND_ROWS_A * P + 8, ob = 4 * 2 * 2 * KWT * NT2 * 64 * 4;
+// Pass A': LDS row pitch of a staged strip.  Odd D: D (the strip is one contiguous run, 16-B
+// vectors land aligned); compiled D with D % 4 == 0: D + 4 (16-B rows, conflict-free folded reads);
+// otherwise D + 1 (element-wise staging).
+TB_HD int band_fwd_pitch(int D, bool ct) { return (D & 1) ? D : (ct && (D & 3) == 0) ? D + 4 : D + 1; }
+// compiled pass-A' kernels (D known at compile time, D-product table in registers)
+TB_HD bool band_fwd_ct(int D, int NT2) { return NT2 == 1 && (D == 155 || D == 128); }
+// floats of one wave's region: the staged strip (+8 slack) or, at a segment end, its O partials
+// [cos/sin][re/im][KWT][NT2][64 lanes][4] -- whichever is larger
+TB_HD int band_fwd_xw(int P, int NT2, int KWT) {
+  const int xn = BAND_FWD_ROWS * P + 8, ob = 2 * 2 * KWT * NT2 * 64 * 4;
   return xn > ob ? xn : ob;
 }
-// LDS bytes of the two slab kernels
-TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D) {
-  const int P = (D & 1) ? D : D + 1;
-  const int KSd = (D / 2 + 1 + 3) / 4, NT2 = g.NDk <= 16 ? 1 : 2, KWT = g.KW < 16 ? 1 : 2;
-  return (size_t)band_fwd_xn(P, NT2, KWT) * 4 + (size_t)W * 8 + (size_t)NT2 * KSd * 128 * 4;
+// LDS bytes of pass A': [W twiddles][D-product table (runtime D only)][4 wave regions]
+TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D, bool ct) {
+  const int NT2 = g.NDk <= 16 ? 1 : 2, KWT = g.KW < 16 ? 1 : 2, KSd = (D / 2 + 1 + 3) / 4;
+  const size_t tw = ((size_t)W * 8 + 15) & ~(size_t)15;
+  const size_t bt = ct ? 0 : (size_t)NT2 * KSd * 128 * 4;
+  return tw + bt + (size_t)4 * band_fwd_xw(band_fwd_pitch(D, ct), NT2, KWT) * 4;
 }
-constexpr int BAND_STG_P = 36;  // pitch (floats) of a wave's staged 32 x 32 output half-tile
 constexpr int BAND_SLOTS = 3;   // slabs whose pass-C' inputs a workgroup holds in LDS at once
+constexpr int BAND_STG_P = 36;  // pitch (floats) of a wave's staged 32 x 32 output half-tile
 struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
   int bimg, tww, frag, prow, stg, total;
 };
@@ -136,7 +163,7 @@ struct BandWs {
 TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   BandWs w;
   w.off_P = 0;
-  w.off_AB = (size_t)bcn * H * g.ncol * 8;
+  w.off_AB = (size_t)bcn * H * BAND_FWD_SEGS * g.ncol * 8;
   w.off_AB = (w.off_AB + 255) & ~(size_t)255;
   w.off_pts = w.off_AB + (size_t)bcn * (g.KH + 1) * g.ncol * 16;
   w.off_mmp = w.off_pts + (size_t)bcn * BAND_MAX_PTS * 8;
@@ -147,7 +174,8 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
 }
 
 // Launchers (kern_band.hip).  ncu = compute units (persistent slab grids).
-hipError_t launch_band_fwd(const BandFwdArgs& a, int ncu, hipStream_t st);
+hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st);  // sets a.split
+bool band_fwd_use_ct(int D, int NT2);  // the compiled-D pass-A' kernel runs for this D
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st);
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);
 hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st);

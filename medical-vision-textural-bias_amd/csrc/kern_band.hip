@@ -8,6 +8,9 @@
 // The op program is applied by apply_ops (fft_core.h), shared with the full-spectrum pass B.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "band.h"
 
 namespace tb {
@@ -23,81 +26,6 @@ __device__ __forceinline__ float2 ld2(const cf* p) {
 
 // ----------------------------------------------------------------------------- pass A'
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int BAND_PF = 10;  // 16-B (or 4-B) prefetch registers per lane: 64 rows x D <= 2560 floats
-
-// One 64-row chunk of a slab: where its rows start and how they are laid out in memory.
-struct ChunkSrc {
-  const float* src;  // first element of the chunk's first row
-  int total;         // rows * D
-  int off;           // contiguous rows: src - (16-B aligned start), in floats
-  int nq;            // contiguous rows: 16-B vectors covering the chunk
-};
-__device__ __forceinline__ ChunkSrc chunk_src(const float* xb, int64_t sw, int w0, int nr, int D) {
-  ChunkSrc c;
-  c.src = xb + (int64_t)w0 * sw;
-  c.total = nr * D;
-  c.off = (int)((reinterpret_cast<uintptr_t>(c.src) >> 2) & 3);
-  c.nq = (c.total + c.off + 3) >> 2;
-  return c;
-}
-// Issue the chunk's global loads into registers (no LDS traffic): every lane keeps up to
-// BAND_PF independent 16-B loads in flight while the current chunk is computed (contiguous rows).
-__device__ __forceinline__ void chunk_load(f32x4 (&v)[BAND_PF], const ChunkSrc& c, int tid) {
-  const f32x4* s4 = reinterpret_cast<const f32x4*>(c.src - c.off);
-#pragma unroll
-  for (int u = 0; u < BAND_PF; ++u) {
-    const int q = tid + u * BAND_NT;
-    if (q < c.nq) v[u] = __builtin_nontemporal_load(s4 + q);
-  }
-}
-// Odd D (LDS pitch = D): the chunk is one contiguous run in LDS too, laid out so that element e
-// sits at X[off + e] -- every 16-B global vector lands 16-B aligned in LDS (one ds_write_b128,
-// no per-element index math); the chunk's base pointer is then X + off.  Even D (pitch D + 1 for
-// conflict-free row reads) inserts one pad float per row.
-__device__ __forceinline__ const float* chunk_store(float* X, const f32x4 (&v)[BAND_PF], const ChunkSrc& c, int D,
-                                                    const FastDiv& fd, int tid) {
-  if (D & 1) {
-#pragma unroll
-    for (int u = 0; u < BAND_PF; ++u) {
-      const int q = tid + u * BAND_NT;
-      if (q < c.nq) *reinterpret_cast<f32x4*>(X + 4 * q) = v[u];
-    }
-    return X + c.off;
-  }
-#pragma unroll
-  for (int u = 0; u < BAND_PF; ++u) {
-    const int e0 = 4 * (tid + u * BAND_NT) - c.off;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = e0 + k;
-      if (e >= 0 && e < c.total) X[e + fd.div(e)] = v[u][k];
-    }
-  }
-  return X;
-}
-// strided rows (e.g. the padded U-Net buffer filtered in place): plain copy, no prefetch
-__device__ __forceinline__ void chunk_copy_strided(float* xs, int P, const ChunkSrc& c, int64_t sw, int D,
-                                                   const FastDiv& fd, int tid) {
-  for (int e0 = tid; e0 < c.total; e0 += 8 * BAND_NT) {
-    float v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int e = e0 + k * BAND_NT;
-      if (e < c.total) {
-        const int r = fd.div(e);
-        v[k] = c.src[(int64_t)r * sw + (e - r * D)];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int e = e0 + k * BAND_NT;
-      if (e < c.total) {
-        const int r = fd.div(e);
-        xs[r * P + (e - r * D)] = v[k];
-      }
-    }
-  }
-}
 
 // Global -> LDS copy of n elements of T by the whole workgroup with U loads in flight per thread
 // (a plain loop would wait for every load before its LDS store: one memory round trip per
@@ -119,45 +47,159 @@ __device__ __forceinline__ void lds_fill(T* dst, const T* __restrict__ src, int 
   }
 }
 
-// NT2: 16-wide kd tiles (NDk <= 16 NT2); KWT: 16-wide kw tiles (KW < 16 KWT).
-// Per 64-row chunk each wave owns 16 rows:
+constexpr int FWD_PF = 10;  // 16-B prefetch registers per lane: a 16-row strip of D <= 159
+
+// One strip (<= 16 rows of a slab): where it starts and how it sits in memory.
+struct StripSrc {
+  const float* src;  // first element of the strip's first row
+  int nr;            // rows
+  int total;         // rows * D
+  int off;           // src - (16-B aligned start), in floats
+  int nq;            // 16-B vectors covering the strip (contiguous rows)
+};
+
+// Wave-private strip staging.  The wave's 64 lanes issue the strip's 16-B loads into registers
+// (FWD_PF per lane) one strip ahead, then store them to the wave's LDS region:
+//   odd D   -- pitch D, the strip is one contiguous run in LDS as in memory; element e sits at
+//              Xw[off + e], so every 16-B vector lands 16-B aligned (ds_write_b128);
+//   D % 4 == 0, compiled D, aligned rows -- pitch D + 4: a vector never straddles a row, one
+//              ds_write_b128 at e + 4 (e / D);
+//   other even D -- pitch D + 1, element-wise.
+template <int DC>
+struct Strip {
+  __device__ __forceinline__ static void load(f32x4 (&v)[FWD_PF], const StripSrc& s, int lane) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(s.src - s.off);
+#pragma unroll
+    for (int u = 0; u < FWD_PF; ++u) {
+      const int q = lane + 64 * u;
+      if (q < s.nq) v[u] = __builtin_nontemporal_load(s4 + q);
+    }
+  }
+  // returns the strip's row-0 pointer in LDS
+  __device__ __forceinline__ static const float* store(float* Xw, const f32x4 (&v)[FWD_PF], const StripSrc& s, int D,
+                                                      int P, const FastDiv& fd, int lane) {
+    if (D & 1) {
+#pragma unroll
+      for (int u = 0; u < FWD_PF; ++u) {
+        const int q = lane + 64 * u;
+        if (q < s.nq) *reinterpret_cast<f32x4*>(Xw + 4 * q) = v[u];
+      }
+      return Xw + s.off;
+    }
+    if (DC > 0 && P == D + 4) {  // off == 0 (host-checked alignment)
+#pragma unroll
+      for (int u = 0; u < FWD_PF; ++u) {
+        const int q = lane + 64 * u;
+        if (q < s.nq) *reinterpret_cast<f32x4*>(Xw + 4 * q + 4 * ((4 * q) / D)) = v[u];
+      }
+      return Xw;
+    }
+#pragma unroll
+    for (int u = 0; u < FWD_PF; ++u) {
+      const int e0 = 4 * (lane + 64 * u) - s.off;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = e0 + k;
+        if (e >= 0 && e < s.total) Xw[e + fd.div(e)] = v[u][k];
+      }
+    }
+    return Xw;
+  }
+};
+// strided rows or a long D (e.g. the padded U-Net buffer filtered in place): plain copy by the wave
+__device__ __forceinline__ void strip_copy(float* Xw, int P, const StripSrc& s, int64_t sw, int D, const FastDiv& fd,
+                                           int lane) {
+  for (int e0 = lane; e0 < s.total; e0 += 8 * 64) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = e0 + k * 64;
+      if (e < s.total) {
+        const int r = fd.div(e);
+        v[k] = s.src[(int64_t)r * sw + (e - r * D)];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = e0 + k * 64;
+      if (e < s.total) {
+        const int r = fd.div(e);
+        Xw[r * P + (e - r * D)] = v[k];
+      }
+    }
+  }
+}
+
+// NT2: 16-wide kd tiles (NDk <= 16 NT2); KWT: 16-wide kw tiles (KW < 16 KWT); DC: compiled D
+// (0: runtime D, D-product table read from LDS).  Per 16-row strip, on the wave alone:
 //   D product  R(row, kd) = sum_d s_d cos + i sum_d t_d sin      16x16x4 MFMA, folded over (d, D-d)
 //   W product  O(kw, kd) += sum_rows {cos, sin}(2 pi kw w / W) R  16x16x4 MFMA; the B operand is the
 //              D product's accumulator register j (its rows 4 (l/16) + j are the k index), so R never
-//              leaves the registers.  The four waves' O are summed once per slab through LDS.
-template <int NT2, int KWT>
-__global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
+//              leaves the registers.
+// At the end of the wave's part of a slab, O goes through the wave's LDS region into the slab's
+// partial-sum slot P[bc][h][seg] (seg = this wave's rank among the slab's waves).
+template <int NT2, int KWT, int DC>
+__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * KWT == 1 ? 3 : NT2 * KWT == 2 ? 2 : 1, 4))) void k_band_fwd(BandFwdArgs) {
   const BandFwdArgs& a = kargs<BandFwdArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
+  const int H = a.pl.H, W = a.pl.W;
+  const int D = DC > 0 ? DC : a.pl.D;
   const int NDk = a.g.NDk, KW = a.g.KW, ncol = a.g.ncol;
-  const int P = (D & 1) ? D : D + 1;
+  const int P = band_fwd_pitch(D, DC > 0);
   const int Ld = D / 2 + 1;                 // folded d in [0, D/2]
   const int KSd = (Ld + 3) / 4;             // 16x16x4 k-steps of the D product
-  const int XN = band_fwd_xn(P, NT2, KWT);  // twW / Bt start past the O partials too
-  float* X = reinterpret_cast<float*>(smem);                     // [64][P] (+8 slack); O partials at slab end
-  float2* twW = reinterpret_cast<float2*>(X + XN);               // (cos, -sin)(2 pi t / W)
-  float* Bt = reinterpret_cast<float*>(twW + W);                 // [NT2][KSd][2][64]
-  lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
-  // plan table (host double precision); 8-B pieces: Bt follows W float2 twiddles
-  lds_fill<8>(reinterpret_cast<float2*>(Bt), reinterpret_cast<const float2*>(a.tbt), NT2 * KSd * 64, tid);
-  for (int t = tid; t < XN; t += BAND_NT) X[t] = 0.f;   // rows past W in a short last chunk stay finite
+  constexpr int KSC = DC > 0 ? (DC / 2 + 1 + 3) / 4 : 1;
+  const int XW = band_fwd_xw(P, NT2, KWT);
+  float2* twW = reinterpret_cast<float2*>(smem);                               // (cos, -sin)(2 pi t / W)
+  float* Bt = reinterpret_cast<float*>(smem + ((W * 8 + 15) & ~15));           // [NT2][KSd][2][64] (DC == 0)
+  float* Xw = Bt + (DC > 0 ? 0 : NT2 * KSd * 128) + wv * XW;                    // this wave's region
   const FastDiv fd = FastDiv::make(D);
-  const int units = H * a.nbc;
-  const int nch = (W + BAND_ROWS_A - 1) / BAND_ROWS_A;
-  const bool contig = a.sw == D;
+  const FwdSplit sp = a.split;
+  const uint32_t nst = sp.nst;
+  const uint32_t gw = (uint32_t)blockIdx.x * 4 + (uint32_t)wv;
+  uint32_t t = 0, t1 = 0;
+  if (gw < sp.G) {
+    t = fwd_start(sp, gw);
+    t1 = fwd_start(sp, gw + 1);
+  }
+  const bool pre = a.vec && (BAND_FWD_ROWS * D + 6) <= 4 * 64 * FWD_PF;
   const int diag = a.diag;
-  int u = (int)blockIdx.x, c = 0;
-  if (u >= units) return;
-  auto xbase = [&](int uu) {
-    const int bcl = uu / H, hh = uu - bcl * H;
-    return a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)hh * a.sh;
+  auto strip_src = [&](uint32_t tt) {
+    StripSrc s;
+    const uint32_t slab = tt / nst, st = tt - slab * nst;
+    const uint32_t bcl = slab / (uint32_t)H, h = slab - bcl * (uint32_t)H;
+    const int w0 = (int)st * BAND_FWD_ROWS;
+    s.src = a.x + (int64_t)(a.bc0 + (int)bcl) * a.sbc + (int64_t)h * a.sh + (int64_t)w0 * a.sw;
+    s.nr = (W - w0) < BAND_FWD_ROWS ? (W - w0) : BAND_FWD_ROWS;
+    s.total = s.nr * D;
+    s.off = (int)((reinterpret_cast<uintptr_t>(s.src) >> 2) & 3);
+    s.nq = (s.total + s.off + 3) >> 2;
+    return s;
   };
-  f32x4 pf[BAND_PF];
-  ChunkSrc cs = chunk_src(xbase(u), a.sw, 0, W < BAND_ROWS_A ? W : BAND_ROWS_A, D);
-  if (contig) chunk_load(pf, cs, tid);
+  // the first strip's loads fly while the tables fill
+  f32x4 pf[FWD_PF];
+  StripSrc ss{};
+  if (t < t1) {
+    ss = strip_src(t);
+    if (pre) Strip<DC>::load(pf, ss, lane);
+  }
+  float btr[NT2][KSC][2];  // compiled D: the D-product B fragments live in registers
+  if (DC > 0) {
+#pragma unroll
+    for (int nt = 0; nt < NT2; ++nt)
+#pragma unroll
+      for (int k = 0; k < KSC; ++k) {
+        btr[nt][k][0] = a.tbt[((nt * KSC + k) * 2) * 64 + lane];
+        btr[nt][k][1] = a.tbt[((nt * KSC + k) * 2 + 1) * 64 + lane];
+      }
+  }
+  lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  // plan table (host double precision); 8-B pieces
+  if (DC == 0) lds_fill<8>(reinterpret_cast<float2*>(Bt), reinterpret_cast<const float2*>(a.tbt), NT2 * KSd * 64, tid);
+  __syncthreads();  // the only workgroup barrier: tables in LDS
+  if (t >= t1) return;
   // O accumulators: [cos/sin][re/im][kw tile][kd tile]
   f32x4 oacc[2][2][KWT][NT2];
 #pragma unroll
@@ -170,70 +212,90 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
         for (int nt = 0; nt < NT2; ++nt)
 #pragma unroll
           for (int j = 0; j < 4; ++j) oacc[m][r][kt][nt][j] = 0.f;
-  const int rbase = 16 * wv;  // this wave's 16 rows of the chunk
-  __syncthreads();            // X zeroed before the first chunk lands
   for (;;) {
-    const int w0 = c * BAND_ROWS_A;
-    const float* xs = X;
+    const uint32_t slab = t / nst, st = t - slab * nst;
+    const int w0 = (int)st * BAND_FWD_ROWS, nr = ss.nr;
+    // 1. this strip into the wave's LDS region
+    const float* xs = Xw;
     if (diag & 2)
-      xs = X;
-    else if (contig)
-      xs = chunk_store(X, pf, cs, D, fd, tid);
+      xs = Xw;
+    else if (pre)
+      xs = Strip<DC>::store(Xw, pf, ss, D, P, fd, lane);
     else
-      chunk_copy_strided(X, P, cs, a.sw, D, fd, tid);
-    __syncthreads();  // the chunk is in LDS
-    int un = u, cn = c + 1;
-    if (cn == nch) { cn = 0; un = u + (int)gridDim.x; }
-    if (un < units) {  // next (unit, chunk): its loads fly while this chunk is computed
-      const int w0n = cn * BAND_ROWS_A;
-      cs = chunk_src(xbase(un), a.sw, w0n, (W - w0n) < BAND_ROWS_A ? (W - w0n) : BAND_ROWS_A, D);
-      if (contig && !(diag & 1)) chunk_load(pf, cs, tid);
+      strip_copy(Xw, P, ss, a.sw, D, fd, lane);
+    if (nr < BAND_FWD_ROWS) {  // a short last strip: the rows past W read as zeros (weight 0 below)
+      float* z = const_cast<float*>(xs) + nr * P;
+      for (int i = lane; i < (BAND_FWD_ROWS - nr) * P; i += 64) z[i] = 0.f;
     }
+    __builtin_amdgcn_wave_barrier();
+    // 2. the next strip's loads fly while this one is computed
+    const uint32_t tn = t + 1;
+    if (tn < t1) {
+      ss = strip_src(tn);
+      if (pre && !(diag & 1)) Strip<DC>::load(pf, ss, lane);
+    }
+    // 3. D product
     f32x4 accc[NT2], accs[NT2];
 #pragma unroll
     for (int nt = 0; nt < NT2; ++nt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) accc[nt][j] = accs[nt][j] = 0.f;
     if (!(diag & 4)) {
-      const float* row = xs + (rbase + l15) * P;
-      for (int k0 = 0; k0 < KSd; k0 += 4) {
-        float sv[4], tv[4];
+      const float* row = xs + l15 * P;
+      if (DC > 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // all LDS reads of 4 k-steps first
-          const int d = 4 * (k0 + q) + l4;
+        for (int k = 0; k < KSC; ++k) {
+          const int d = 4 * k + l4;
           const bool has = d < Ld;
           const bool pair = d >= 1 && 2 * d < D;
           const float xa = has ? row[d] : 0.f;
           const float xm = pair ? row[D - d] : 0.f;
-          sv[q] = xa + xm;
-          tv[q] = pair ? xm - xa : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (k0 + q >= KSd) break;
+          const float sv = xa + xm, tv = pair ? xm - xa : 0.f;
 #pragma unroll
           for (int nt = 0; nt < NT2; ++nt) {
-            const float* bt = Bt + ((nt * KSd + k0 + q) * 2) * 64 + lane;
-            accc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv[q], bt[0], accc[nt], 0, 0, 0);
-            accs[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv[q], bt[64], accs[nt], 0, 0, 0);
+            accc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv, btr[nt][k][0], accc[nt], 0, 0, 0);
+            accs[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv, btr[nt][k][1], accs[nt], 0, 0, 0);
+          }
+        }
+      } else {
+        for (int k0 = 0; k0 < KSd; k0 += 4) {
+          float sv[4], tv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // all LDS reads of 4 k-steps first
+            const int d = 4 * (k0 + q) + l4;
+            const bool has = d < Ld;
+            const bool pair = d >= 1 && 2 * d < D;
+            const float xa = has ? row[d] : 0.f;
+            const float xm = pair ? row[D - d] : 0.f;
+            sv[q] = xa + xm;
+            tv[q] = pair ? xm - xa : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (k0 + q >= KSd) break;
+#pragma unroll
+            for (int nt = 0; nt < NT2; ++nt) {
+              const float* bt = Bt + ((nt * KSd + k0 + q) * 2) * 64 + lane;
+              accc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sv[q], bt[0], accc[nt], 0, 0, 0);
+              accs[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(tv[q], bt[64], accs[nt], 0, 0, 0);
+            }
           }
         }
       }
     }
-    __syncthreads();  // every wave is done reading the chunk in LDS
+    // 4. W product: rows w = w0 + 4 (l/16) + j of the strip; rows >= W weigh 0
     if (!(diag & 8)) {
-      // W product: rows w = w0 + rbase + 4 (l/16) + j of this wave; rows >= W weigh 0
-      const int wl = w0 + rbase + 4 * l4;
+      const int wl = w0 + 4 * l4;
 #pragma unroll
       for (int kt = 0; kt < KWT; ++kt) {
         const int kw = 16 * kt + l15;
-        int t = (int)(((int64_t)kw * wl) % W);
+        int tw = (int)(((int64_t)kw * wl) % W);
         const int step = kw % W;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bool ok = wl + j < W && kw <= KW;
-          const float2 tw = twW[t];
-          const float ca = ok ? tw.x : 0.f, sa = ok ? -tw.y : 0.f;
+          const float2 c = twW[tw];
+          const float ca = ok ? c.x : 0.f, sa = ok ? -c.y : 0.f;
 #pragma unroll
           for (int nt = 0; nt < NT2; ++nt) {
             oacc[0][0][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca, accc[nt][j], oacc[0][0][kt][nt], 0, 0, 0);
@@ -241,14 +303,14 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
             oacc[1][0][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sa, accc[nt][j], oacc[1][0][kt][nt], 0, 0, 0);
             oacc[1][1][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(sa, accs[nt][j], oacc[1][1][kt][nt], 0, 0, 0);
           }
-          t += step;
-          t = t >= W ? t - W : t;
+          tw += step;
+          tw = tw >= W ? tw - W : tw;
         }
       }
     }
-    if (c == nch - 1) {
-      // slab done: the four waves' O through LDS (X is free until the next chunk is stored)
-      float* Ob = X;  // [wave][m][r][kt][nt][64 lanes][4]
+    // 5. end of this wave's part of the slab: O -> LDS region -> the slab's partial-sum slot
+    if (st == nst - 1 || tn == t1) {
+      float* Ob = Xw;  // [m][r][kt][nt][64 lanes][4]; the strip is consumed (LDS ops stay in order)
       constexpr int NB = 2 * 2 * KWT * NT2;
 #pragma unroll
       for (int m = 0; m < 2; ++m)
@@ -259,13 +321,14 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
 #pragma unroll
             for (int nt = 0; nt < NT2; ++nt) {
               const int blk = ((m * 2 + r) * KWT + kt) * NT2 + nt;
-              *reinterpret_cast<f32x4*>(Ob + ((wv * NB + blk) * 64 + lane) * 4) = oacc[m][r][kt][nt];
+              *reinterpret_cast<f32x4*>(Ob + (blk * 64 + lane) * 4) = oacc[m][r][kt][nt];
               oacc[m][r][kt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-      __syncthreads();
-      const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
-      cf* Pb = a.P + ((int64_t)bc * H + h) * ncol;
-      for (int it = tid; it < (KW + 1) * NDk; it += BAND_NT) {
+      __builtin_amdgcn_wave_barrier();
+      const int seg = (int)(gw - fwd_wave_of(sp, slab * nst));
+      const int bcl = (int)(slab / (uint32_t)H), h = (int)(slab - (uint32_t)bcl * (uint32_t)H);
+      cf* Pb = a.P + (((int64_t)(a.bc0 + bcl) * H + h) * BAND_FWD_SEGS + seg) * ncol;
+      for (int it = lane; it < (KW + 1) * NDk; it += 64) {
         const int kw = it / NDk, kd = it - kw * NDk;
         const int kt = kw >> 4, nt = kd >> 4;
         // C layout: lane = 16 (row / 4) + col, register = row % 4 (row = kw % 16, col = kd % 16)
@@ -274,77 +337,110 @@ __global__ __launch_bounds__(BAND_NT) void k_band_fwd(BandFwdArgs) {
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            const int blk = ((m * 2 + r) * KWT + kt) * NT2 + nt;
-            float sum = 0.f;
-#pragma unroll
-            for (int w_ = 0; w_ < 4; ++w_) sum += Ob[((w_ * NB + blk) * 64 + ln) * 4 + rg];
-            o[m][r] = sum;
-          }
+          for (int r = 0; r < 2; ++r) o[m][r] = Ob[((((m * 2 + r) * KWT + kt) * NT2 + nt) * 64 + ln) * 4 + rg];
         // P(kw) = Ac - i As, P(-kw) = Ac + i As
         Pb[(KW + kw) * NDk + kd] = mk(o[0][0] + o[1][1], o[0][1] - o[1][0]);
         if (kw > 0) Pb[(KW - kw) * NDk + kd] = mk(o[0][0] - o[1][1], o[0][1] + o[1][0]);
       }
-      __syncthreads();  // Ob (X) read before the next chunk is stored
+      (void)NB;
+      __builtin_amdgcn_wave_barrier();
     }
-    if (un >= units) break;
-    u = un;
-    c = cn;
+    if (tn >= t1) break;
+    t = tn;
   }
 }
 
 // ----------------------------------------------------------------------------- pass B'
+constexpr int BAND_MID_MAXH = 1024;  // slabs per bc whose twiddles / partial counts pass B' tabulates in LDS
+constexpr int BAND_MID_KG = 4;       // kh per pass-B' workgroup
+
+// One workgroup per (bc, 64 box columns, BAND_MID_KG consecutive kh): the slabs' pass-A' partials
+// are read once per kh group, the four waves split h, each lane holds Q(kh) of its column for the
+// group: Ac(kh) = sum_h P_h cos(2 pi kh h / H), As(kh) = sum_h P_h sin(..).  Then the waves' sums
+// meet in LDS and wave w finishes kh = kh0 + w: the sample's op program on Q(kh) and Q(-kh),
+// stored as their sum and difference AB[bc][kh][col].
 __global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
   const BandMidArgs& a = kargs<BandMidArgs>();
-  __shared__ float4 red[3][64];
+  constexpr int KG = BAND_MID_KG;
+  __shared__ float4 red[4][KG][64];
+  __shared__ float2 twl[BAND_MID_MAXH];         // (cos, -sin)(2 pi t / H)
+  __shared__ unsigned char nsg[BAND_MID_MAXH];  // pass-A' partials per slab
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
-  const int NDk = a.g.NDk, KW = a.g.KW, ncol = a.g.ncol;
-  const int kh = (int)blockIdx.y, bcl = (int)blockIdx.z, bc = a.bc0 + bcl;
+  const int NDk = a.g.NDk, KW = a.g.KW, KH = a.g.KH, ncol = a.g.ncol;
+  const int kh0 = (int)blockIdx.y * KG, bcl = (int)blockIdx.z, bc = a.bc0 + bcl;
   const int col = (int)blockIdx.x * 64 + lane;
   const bool live = col < ncol;
-  const cf* Pc = a.P + (int64_t)bc * H * ncol + (live ? col : 0);
-  const cf* twH = a.pl.tw[0];
-  // Q(kh) = sum_h P_h e^{-i theta}: Ac = sum P cos, As = sum P sin; waves split h
-  float2 ac = make_float2(0.f, 0.f), as = make_float2(0.f, 0.f);
-  int t = (int)(((int64_t)kh * wv) % H);
-  const int step = (int)(((int64_t)kh * 4) % H);
-  for (int hh = wv; hh < H; hh += 4) {
-    const float2 p = ld2(Pc + (int64_t)hh * ncol);
-    const float2 tw = ld2(twH + t);  // uniform: (cos, -sin)
-    ac.x = fmaf(p.x, tw.x, ac.x);
-    ac.y = fmaf(p.y, tw.x, ac.y);
-    as.x = fmaf(p.x, -tw.y, as.x);
-    as.y = fmaf(p.y, -tw.y, as.y);
-    t += step;
-    t = t >= H ? t - H : t;
-  }
-  if (wv > 0) red[wv - 1][lane] = make_float4(ac.x, ac.y, as.x, as.y);
+  const cf* Pc = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol + (live ? col : 0);
+  const bool tab = H <= BAND_MID_MAXH;
+  if (tab)
+    for (int hh = tid; hh < H; hh += BAND_NT) {
+      twl[hh] = ld2(a.pl.tw[0] + hh);
+      nsg[hh] = (unsigned char)fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
+    }
   __syncthreads();
-  if (wv != 0) return;
-  for (int j = 0; j < 3; ++j) {
-    const float4 r = red[j][lane];
-    ac.x += r.x; ac.y += r.y; as.x += r.z; as.y += r.w;
+  float4 acc[KG];  // (Ac.re, Ac.im, As.re, As.im) of kh0 + k
+#pragma unroll
+  for (int k = 0; k < KG; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int U = 4;  // slabs whose loads are in flight together
+  for (int h0 = wv; h0 < H; h0 += 4 * U) {
+    float2 p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int hh = h0 + 4 * u < H ? h0 + 4 * u : H - 1;
+      const int nseg = tab ? (int)nsg[hh] : fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
+      const cf* ph = Pc + (int64_t)hh * BAND_FWD_SEGS * ncol;
+      const float2 p0 = ld2(ph), p1 = ld2(ph + ncol), p2 = ld2(ph + 2 * ncol);  // stale slots masked below
+      p[u].x = p0.x + (nseg > 1 ? p1.x : 0.f) + (nseg > 2 ? p2.x : 0.f);
+      p[u].y = p0.y + (nseg > 1 ? p1.y : 0.f) + (nseg > 2 ? p2.y : 0.f);
+      if (h0 + 4 * u >= H) p[u] = make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int hh = h0 + 4 * u < H ? h0 + 4 * u : 0;
+      int t = (int)(((int64_t)kh0 * hh) % H);
+#pragma unroll
+      for (int k = 0; k < KG; ++k) {  // slots past KH accumulate too (never stored): no branches
+        const float2 tw = tab ? twl[t] : ld2(a.pl.tw[0] + t);  // (cos, -sin)(2 pi (kh0 + k) hh / H)
+        acc[k].x = fmaf(p[u].x, tw.x, acc[k].x);
+        acc[k].y = fmaf(p[u].y, tw.x, acc[k].y);
+        acc[k].z = fmaf(p[u].x, -tw.y, acc[k].z);
+        acc[k].w = fmaf(p[u].y, -tw.y, acc[k].w);
+        t += hh;
+        t = t >= H ? t - H : t;
+      }
+    }
   }
+#pragma unroll
+  for (int k = 0; k < KG; ++k) red[wv][k][lane] = acc[k];
+  __syncthreads();
   const int lb = a.cofs + bcl, s = lb / a.C, chan = lb - s * a.C;
   const tb_sample_ops& so = a.ops.s[s];
   if (live) {
     const int jw = col / NDk, kd = col - jw * NDk;
     const int kw = (jw - KW + W) % W;
     const FreqCol fc = freq_col(kw, kd, W, D);
-    cf qp = apply_ops(so, chan, mk(ac.x + as.y, ac.y - as.x), fc, kh, H);
-    float4 o;
-    if (kh == 0) {
-      o = make_float4(qp.x, qp.y, 0.f, 0.f);
-    } else {
-      const cf qm = apply_ops(so, chan, mk(ac.x - as.y, ac.y + as.x), fc, H - kh, H);
-      o = make_float4(qp.x + qm.x, qp.y + qm.y, qp.x - qm.x, qp.y - qm.y);
+    for (int k = wv; k < KG && kh0 + k <= KH; k += 4) {
+      const int kh = kh0 + k;
+      float4 q = red[0][k][lane];
+      for (int w_ = 1; w_ < 4; ++w_) {
+        const float4 r = red[w_][k][lane];
+        q.x += r.x; q.y += r.y; q.z += r.z; q.w += r.w;
+      }
+      cf qp = apply_ops(so, chan, mk(q.x + q.w, q.y - q.z), fc, kh, H);
+      float4 o;
+      if (kh == 0) {
+        o = make_float4(qp.x, qp.y, 0.f, 0.f);
+      } else {
+        const cf qm = apply_ops(so, chan, mk(q.x - q.w, q.y + q.z), fc, H - kh, H);
+        o = make_float4(qp.x + qm.x, qp.y + qm.y, qp.x - qm.x, qp.y - qm.y);
+      }
+      a.AB[((int64_t)bc * (KH + 1) + kh) * ncol + col] = o;
     }
-    a.AB[((int64_t)bc * (a.g.KH + 1) + kh) * ncol + col] = o;
   }
   // the out-of-box spike points: the program applied to a coefficient the low-pass zeroed
-  if (blockIdx.x == 0 && kh == 0 && lane < BAND_MAX_PTS) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0 && lane < BAND_MAX_PTS) {
     const BandSamplePts& sp = a.sp[s];
     cf c = mk(0.f, 0.f);
     if (lane < sp.n) {
@@ -450,7 +546,6 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
 //   y[w][d] = E - O,  y[w][D - d] = E + O   for d in [0, D/2]  (the C2R folded over d <-> D - d)
 // Each lane ends with 4 consecutive columns of one image row for both halves: 16-B stores.
 __device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
-
 template <int VT>  // 32-row tiles of V (2 (NDk + points) <= 32 VT)
 __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1 ? 3 : 2, 4))) void k_band_inv(BandInvArgs) {
   // The workgroup takes its slabs in batches of BAND_SLOTS: the batch's inputs (V-product
@@ -475,14 +570,21 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   float* Fs = reinterpret_cast<float*>(smem + cv.frag);    // [BAND_SLOTS][fsz]
   float* Ps = reinterpret_cast<float*>(smem + cv.prow);    // [BAND_SLOTS][psz]
   float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 32 * BAND_STG_P;  // this wave's 32 x 32 tile
-  lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
-  lds_fill<4>(reinterpret_cast<float4*>(Bimg), reinterpret_cast<const float4*>(a.tds), 2 * NDk * NCOL / 4, tid);
+  // The tables (band rows of the synthesis table, W twiddles) load in the same round as the first
+  // batch's inputs: one global latency before the first unit, not three.
+  const int nbi4 = 2 * NDk * NCOL / 4;           // float4s of Bimg
+  const bool twv = !(W & 1) && (reinterpret_cast<uintptr_t>(a.pl.tw[1]) & 15) == 0;
+  const int ntw4 = twv ? W / 2 : 0;              // float4s of twW (else filled apart, here)
+  if (!twv) lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  const float4* Tsrc = reinterpret_cast<const float4*>(a.tds);
+  const float4* Wsrc = reinterpret_cast<const float4*>(a.pl.tw[1]);
+  int tb4 = nbi4 + ntw4;                         // table float4s still to load (first batch only)
   const int ntw = (W + 31) / 32;     // 32-row tiles of a slab
   const int nslab = H * a.nbc;
   const int ntn = NCOL / 32;         // 32-column tiles of the folded row
   const int ypad = a.ypad;
-  const int diag = a.diag;
   const bool mal = ((D - 3) & 3) == 0;  // mirrored 4-column groups start 16-B aligned
+  const int diag = a.diag;
   // Each workgroup owns a contiguous range of (slab, row tile) units, dealt round-robin to its
   // waves, so every wave of the grid gets the same number of units (a slab-granular split left
   // half the workgroups with 3 slabs and half with 2); the range's slabs are loaded in batches of
@@ -497,32 +599,44 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
     const int c1 = (s1 + 1) * ntw < ue ? (s1 + 1) * ntw : ue;  // units [c0, c1) of this batch
     const int nb = s1 - s0 + 1;
     __syncthreads();  // the previous batch is done with Fs / Ps
-    {  // the batch's fragments (contiguous slabs) and point rows in one round of loads in flight
-      const int nf4 = nb * fsz / 4, np4 = nb * psz / 4, ntot = nf4 + np4, nc4 = NCOL / 4, pp4 = psz / 4;
+    {  // [tables,] the batch's fragments (contiguous slabs) and point rows: rounds of loads in flight
+      const int nf4 = nb * fsz / 4, np4 = nb * psz / 4, nc4 = NCOL / 4, pp4 = psz / 4;
+      const int ntot = tb4 + nf4 + np4;
       const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
-      for (int base = 0; base < ntot; base += 6 * BAND_NT) {
-        float4 v[6];
+      for (int base = 0; base < ntot; base += 9 * BAND_NT) {
+        float4 v[9];
 #pragma unroll
-        for (int u = 0; u < 6; ++u) {
+        for (int u = 0; u < 9; ++u) {
           const int e = base + u * BAND_NT + tid;
-          if (e < nf4 || e >= ntot) {
-            v[u] = F4[e < nf4 ? e : 0];
+          const int q = e - tb4;
+          if (e < tb4) {
+            v[u] = e < nbi4 ? Tsrc[e] : Wsrc[e - nbi4];
+          } else if (q < nf4 || e >= ntot) {
+            v[u] = F4[(q < nf4 && q >= 0) ? q : 0];
           } else {
-            const int q = e - nf4, i = q / pp4, rem = q - i * pp4, r = rem / nc4, n = rem - r * nc4, j = r >> 1;
+            const int qq = q - nf4, i = qq / pp4, rem = qq - i * pp4, r = rem / nc4, n = rem - r * nc4, j = r >> 1;
             const BandSamplePts& sp = a.sp[(a.cofs + (s0 + i) / H) / a.C];
             v[u] = j < sp.n ? reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n]
                             : make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
 #pragma unroll
-        for (int u = 0; u < 6; ++u) {
+        for (int u = 0; u < 9; ++u) {
           const int e = base + u * BAND_NT + tid;
-          if (e < nf4)
-            reinterpret_cast<float4*>(Fs)[e] = v[u];
-          else if (e < ntot)
-            reinterpret_cast<float4*>(Ps)[e - nf4] = v[u];
+          const int q = e - tb4;
+          if (e < tb4) {
+            if (e < nbi4)
+              reinterpret_cast<float4*>(Bimg)[e] = v[u];
+            else
+              reinterpret_cast<float4*>(twW)[e - nbi4] = v[u];
+          } else if (q < nf4) {
+            reinterpret_cast<float4*>(Fs)[q] = v[u];
+          } else if (e < ntot) {
+            reinterpret_cast<float4*>(Ps)[q - nf4] = v[u];
+          }
         }
       }
+      tb4 = 0;
     }
     __syncthreads();
     for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {  // (un - ub) % 4 == wave
@@ -767,19 +881,42 @@ int band_grid(K kern, int units, size_t lds, int ncu) {
       occ = (int)(163840 / (lds ? lds : 1));
     last_occ = occ;
     last_lds = lds;
+    if (std::getenv("TEXBIAS_BAND_VERBOSE"))
+      std::fprintf(stderr, "[texbias] band grid: lds %zu B, %d workgroups/CU, %d units\n", lds, occ, units);
   }
   const int per_cu = last_occ < 1 ? 1 : (last_occ > 4 ? 4 : last_occ);
   const int g = ncu * per_cu;
   return units < g ? units : g;
 }
 
-template <int NT2, int KWT>
-hipError_t launch_fwd_t(const BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
-  auto kern = k_band_fwd<NT2, KWT>;
+template <int NT2, int KWT, int DC>
+hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
+  auto kern = k_band_fwd<NT2, KWT, DC>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
-  const int units = a.pl.H * a.nbc;
-  hipLaunchKernelGGL(kern, dim3(band_grid(kern, units, lds, ncu)), dim3(BAND_NT), lds, st, a);
+  // waves: as many as are resident at once (LDS / register occupancy), but at most T / ceil(nst / 2)
+  // so that a slab spans at most BAND_FWD_SEGS waves, and (T + 1) G < 2^32 for the 32-bit split
+  static size_t last_lds = ~(size_t)0;
+  static int last_occ = 1;
+  if (lds != last_lds) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BAND_NT, lds) != hipSuccess || occ < 1)
+      occ = (int)(163840 / (lds ? lds : 1));
+    last_occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+    last_lds = lds;
+    if (std::getenv("TEXBIAS_BAND_VERBOSE"))
+      std::fprintf(stderr, "[texbias] band fwd: lds %zu B, %d workgroups/CU\n", lds, occ);
+  }
+  const uint32_t nst = (uint32_t)((a.pl.W + BAND_FWD_ROWS - 1) / BAND_FWD_ROWS);
+  const uint64_t T = (uint64_t)a.pl.H * (uint64_t)a.nbc * nst;
+  uint64_t G = (uint64_t)ncu * (uint64_t)last_occ * 4;
+  const uint64_t gmax = T / ((nst + 1) / 2);
+  G = G < gmax ? G : gmax;
+  while (G > 1 && (T + 1) * G >= (1ull << 32)) G >>= 1;
+  if (G < 1) G = 1;
+  if (T >= (1ull << 31)) return hipErrorInvalidValue;
+  a.split = FwdSplit{(uint32_t)T, (uint32_t)G, nst};
+  hipLaunchKernelGGL(kern, dim3((unsigned)((G + 3) / 4)), dim3(BAND_NT), lds, st, a);
   return hipGetLastError();
 }
 
@@ -796,16 +933,31 @@ hipError_t launch_inv_t(const BandInvArgs& a, int ncu, hipStream_t st) {
 
 }  // namespace
 
-hipError_t launch_band_fwd(const BandFwdArgs& a, int ncu, hipStream_t st) {
-  const size_t lds = band_lds_fwd(a.g, a.pl.W, a.pl.D);
+bool band_fwd_use_ct(int D, int NT2) {
+  static const bool ct_on = [] {  // TEXBIAS_BAND_FWD_CT=0: the runtime-D kernels (measurement)
+    const char* e = std::getenv("TEXBIAS_BAND_FWD_CT");
+    return !(e && e[0] == '0');
+  }();
+  return ct_on && band_fwd_ct(D, NT2);
+}
+
+hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
   const bool n1 = a.g.NDk <= 16, k1 = a.g.KW < 16;
-  if (n1) return k1 ? launch_fwd_t<1, 1>(a, lds, ncu, st) : launch_fwd_t<1, 2>(a, lds, ncu, st);
-  return k1 ? launch_fwd_t<2, 1>(a, lds, ncu, st) : launch_fwd_t<2, 2>(a, lds, ncu, st);
+  const bool ct = band_fwd_use_ct(a.pl.D, n1 ? 1 : 2);
+  const size_t lds = band_lds_fwd(a.g, a.pl.W, a.pl.D, ct);
+  if (ct) {
+    if (a.pl.D == 155) return k1 ? launch_fwd_t<1, 1, 155>(a, lds, ncu, st) : launch_fwd_t<1, 2, 155>(a, lds, ncu, st);
+    return k1 ? launch_fwd_t<1, 1, 128>(a, lds, ncu, st) : launch_fwd_t<1, 2, 128>(a, lds, ncu, st);
+  }
+  if (n1) return k1 ? launch_fwd_t<1, 1, 0>(a, lds, ncu, st) : launch_fwd_t<1, 2, 0>(a, lds, ncu, st);
+  return k1 ? launch_fwd_t<2, 1, 0>(a, lds, ncu, st) : launch_fwd_t<2, 2, 0>(a, lds, ncu, st);
 }
 
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_band_mid, dim3((a.g.ncol + 63) / 64, a.g.KH + 1, a.nbc), dim3(BAND_NT), 0, st, a);
-  hipError_t e = hipGetLastError();
+  const dim3 grid((a.g.ncol + 63) / 64, (a.g.KH + BAND_MID_KG) / BAND_MID_KG, a.nbc);
+  hipLaunchKernelGGL(k_band_mid, grid, dim3(BAND_NT), 0, st, a);
+  hipError_t e;
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4), dim3(BAND_NT), 0, st, a);
   return hipGetLastError();

@@ -586,7 +586,9 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   if (2 * g.KS > 64 || g.KS > 32) return false;  // pass C' holds V in at most two 32-row MFMA tiles
   // worth it only when the box is a small part of the half spectrum
   if ((double)(2 * KH + 1) * g.ncol * 4.0 > (double)H * W * (D / 2 + 1)) return false;
-  if (band_lds_fwd(g, W, D) > 160000 || band_inv_carve(g, W, D).total > 160000) return false;
+  if (band_lds_fwd(g, W, D, false) > 160000 || band_lds_fwd(g, W, D, true) > 160000 ||
+      band_inv_carve(g, W, D).total > 160000)
+    return false;
   if (band_ws(g, H, bcn).total > ws_bytes) return false;
   return true;
 }
@@ -652,10 +654,15 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
   cf* pts = reinterpret_cast<cf*>(ws + wl.off_pts);
   const int nbc = nb * C, bc0 = b0 * C;
   const double pbytes = (double)nbc * H * g.ncol * 8.0, abytes = (double)nbc * (g.KH + 1) * g.ncol * 16.0;
+  tb::FwdSplit split{};
   {
     Timer t(0, st, (double)nbc * H * W * D * 4.0 + pbytes, "k_band_fwd");
     BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g, g_band_diag & 0xff, p->tbt};
+    // 16-B vector strips: contiguous rows, and 16-B aligned strips where the compiled even-D staging needs them
+    const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (xs[0] & 3) == 0 && (xs[1] & 3) == 0;
+    fa.vec = xs[2] == D && ((D & 1) || al || !tb::band_fwd_use_ct(D, g.NDk <= 16 ? 1 : 2));
     TB_HIP(tb::launch_band_fwd(fa, p->ncu, st));
+    split = fa.split;
   }
   {
     Timer t(1, st, pbytes + abytes, "k_band_mid");
@@ -672,6 +679,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ma.cofs = 0;
     ma.nbc = nbc;
     ma.g = g;
+    ma.split = split;
     for (int i = 0; i < nb; ++i) {
       ma.sp[i] = sp[i];
       ma.ops.s[i] = ops[b0 + i];
