@@ -138,7 +138,7 @@ TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D, bool ct) {
 constexpr int BAND_SLOTS = 3;   // slabs whose pass-C' inputs a workgroup holds in LDS at once
 constexpr int BAND_STG_P = 36;  // pitch (floats) of a wave's staged 32 x 32 output half-tile
 struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
-  int bimg, tww, frag, prow, stg, total;
+  int bimg, tww, frag, prow, pkw, stg, total;
 };
 TB_HD int band_al16(int b) { return (b + 15) & ~15; }
 TB_HD int band_vt(const BandGeo& g) { return 2 * g.KS <= 32 ? 1 : 2; }  // 32-row tiles of V
@@ -151,7 +151,8 @@ TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
   c.tww = band_al16(c.bimg + 2 * g.NDk * g.NCOL * 4); // [W] twiddles
   c.frag = band_al16(c.tww + W * 8);                  // [SLOTS][VT KV 64] V-product fragments
   c.prow = band_al16(c.frag + BAND_SLOTS * band_vt(g) * band_kv(g) * 64 * 4);  // [SLOTS][2 npm + 4][NCOL]
-  c.stg = band_al16(c.prow + BAND_SLOTS * (2 * npm + 4) * g.NCOL * 4);  // [4 waves][32][BAND_STG_P] staging
+  c.pkw = band_al16(c.prow + BAND_SLOTS * (2 * npm + 4) * g.NCOL * 4);  // [SLOTS][BAND_MAX_PTS] point kw
+  c.stg = band_al16(c.pkw + BAND_SLOTS * BAND_MAX_PTS * 4);  // [4 waves][32][BAND_STG_P] staging
   c.total = band_al16(c.stg + 4 * 32 * BAND_STG_P * 4);
   return c;
 }

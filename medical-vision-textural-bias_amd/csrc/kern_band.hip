@@ -536,6 +536,7 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
 }
 
 // ----------------------------------------------------------------------------- pass C'
+
 // Per (bc, h) slab, on the matrix cores after a small prologue:
 //   V^T(v, w)  = M2T(v, k) . CS(k, w)       MFMA 32x32x2; v = 2 kd + (re, im) and two rows per
 //                out-of-box point; k = (kw, cos/sin) terms and one pair per point; w on the lane
@@ -570,6 +571,9 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   float* Fs = reinterpret_cast<float*>(smem + cv.frag);    // [BAND_SLOTS][fsz]
   float* Ps = reinterpret_cast<float*>(smem + cv.prow);    // [BAND_SLOTS][psz]
   float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 32 * BAND_STG_P;  // this wave's 32 x 32 tile
+  // the batch slabs' point kw (0 past the sample's points): read from LDS in the unit loop, which
+  // must hold no vector-memory load -- its s_waitcnt vmcnt would also wait out the pending stores
+  int* Pkw = reinterpret_cast<int*>(smem + cv.pkw);  // [BAND_SLOTS][BAND_MAX_PTS]
   // The tables (band rows of the synthesis table, W twiddles) load in the same round as the first
   // batch's inputs: one global latency before the first unit, not three.
   const int nbi4 = 2 * NDk * NCOL / 4;           // float4s of Bimg
@@ -585,6 +589,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int ypad = a.ypad;
   const bool mal = ((D - 3) & 3) == 0;  // mirrored 4-column groups start 16-B aligned
   const int diag = a.diag;
+  if (diag & 64) return;  // measurement: launch only
   // Each workgroup owns a contiguous range of (slab, row tile) units, dealt round-robin to its
   // waves, so every wave of the grid gets the same number of units (a slab-granular split left
   // half the workgroups with 3 slabs and half with 2); the range's slabs are loaded in batches of
@@ -637,12 +642,17 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
         }
       }
       tb4 = 0;
+      if (tid < nb * BAND_MAX_PTS) {
+        const int i = tid / BAND_MAX_PTS, j = tid - i * BAND_MAX_PTS;
+        const BandSamplePts& sp = a.sp[(a.cofs + (s0 + i) / H) / a.C];
+        Pkw[tid] = j < sp.n ? (int)sp.p[j].kw : 0;
+      }
     }
     __syncthreads();
+    if (diag & 32) return;  // measurement: launch + first batch prologue only
     for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {  // (un - ub) % 4 == wave
       const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
       const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
-      const BandSamplePts& sp = a.sp[(a.cofs + bcl) / a.C];
       const float* F = Fs + slot * fsz + lane;  // fragment of (vt, ks): F[(vt KV + ks) 64]
       const float* Pr = Ps + slot * psz;
       const int w = 32 * tw_ + l31;
@@ -653,7 +663,26 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
 #pragma unroll
         for (int j = 0; j < 16; ++j) vacc[vt][j] = 0.f;
       int t = 0;
-      for (int ks = 0; ks <= ((diag & 4) ? -1 : KW); ++ks) {
+      const int kse = (diag & 4) ? 0 : KW + 1;
+      int ks = 0;
+      for (; ks + 4 <= kse; ks += 4) {  // the operands of 4 k-steps in flight before their MFMAs
+        float fa[4][VT], bb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float2 c = twW[t];
+          bb[q] = hl ? -c.y : c.x;
+#pragma unroll
+          for (int vt = 0; vt < VT; ++vt) fa[q][vt] = F[(vt * KV + ks + q) * 64];
+          t += wm;
+          t = t >= W ? t - W : t;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int vt = 0; vt < VT; ++vt)
+            vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][vt], bb[q], vacc[vt], 0, 0, 0);
+      }
+      for (; ks < kse; ++ks) {
         const float2 c = twW[t];
         const float b = hl ? -c.y : c.x;
 #pragma unroll
@@ -663,8 +692,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
         t = t >= W ? t - W : t;
       }
       for (int j = 0; j < npm; ++j) {
-        const int kw = j < sp.n ? sp.p[j].kw : 0;
-        const float2 c = twW[(int)(((int64_t)kw * wm) % W)];
+        const int kw = Pkw[slot * BAND_MAX_PTS + j];
+        const float2 c = twW[(kw * wm) % W];  // kw, wm < W <= 2^15
         const float b = hl ? -c.y : c.x;
 #pragma unroll
         for (int vt = 0; vt < VT; ++vt)
@@ -683,15 +712,34 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
         for (int j = 0; j < 16; ++j) ye[j] = yo[j] = 0.f;
         if (!(diag & 8))
 #pragma unroll
-          for (int vt = 0; vt < VT; ++vt)
+          for (int vt = 0; vt < VT; ++vt) {
+            // even sI: real rows (E); sI + 1: imaginary rows (O).  All 16 table operands are loaded
+            // before the first MFMA (a step whose rows are past the used ones reads row 0 / 4 and
+            // is skipped), so the LDS latency is paid once per tile, not once per k-step.
+            float b0[8], b1[8];
 #pragma unroll
-            for (int sI = 0; sI < 16; sI += 2) {  // even sI: real rows (E); sI + 1: imaginary rows (O)
-              if (32 * vt + acc_row(sI) >= nrv) break;  // both halves' rows past the used ones are zero
-              const int re = 32 * vt + acc_row(sI) + 4 * hl;  // this lane's (real) row of the step
+            for (int i = 0; i < 8; ++i) {
+              const int r = 32 * vt + acc_row(2 * i);
+              const int re = (r < nrv ? r : 0) + 4 * hl;  // this lane's (real) row of the step
               const float* tr = (re < 2 * NDk ? Tb : Tp) + re * NCOL + nt * 32;
-              ye = __builtin_amdgcn_mfma_f32_32x32x2f32(tr[0], vacc[vt][sI], ye, 0, 0, 0);
-              yo = __builtin_amdgcn_mfma_f32_32x32x2f32(tr[NCOL], vacc[vt][sI + 1], yo, 0, 0, 0);
+              b0[i] = tr[0];
+              b1[i] = tr[NCOL];
             }
+            if (32 * vt + acc_row(14) < nrv) {  // every step used (C3): one straight-line block
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                ye = __builtin_amdgcn_mfma_f32_32x32x2f32(b0[i], vacc[vt][2 * i], ye, 0, 0, 0);
+                yo = __builtin_amdgcn_mfma_f32_32x32x2f32(b1[i], vacc[vt][2 * i + 1], yo, 0, 0, 0);
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                if (32 * vt + acc_row(2 * i) >= nrv) break;  // both halves' rows past the used ones are zero
+                ye = __builtin_amdgcn_mfma_f32_32x32x2f32(b0[i], vacc[vt][2 * i], ye, 0, 0, 0);
+                yo = __builtin_amdgcn_mfma_f32_32x32x2f32(b1[i], vacc[vt][2 * i + 1], yo, 0, 0, 0);
+              }
+            }
+          }
         if (diag & 16) continue;
         // y[w][d] = E - O (direct half), then y[w][D - d] = E + O (mirror half), each staged
         // [row][32] through LDS so that every store instruction writes whole 128-B row segments

@@ -90,15 +90,29 @@ __device__ __forceinline__ const A& kargs() {
   return *(const A*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
 }
 
+// Wave-wide min / max on DPP lane moves (VALU, a few cycles each) instead of six dependent
+// ds_bpermute round trips through the LDS pipe: quad swaps, half-row and row mirrors, then the
+// gfx9 row broadcasts of lanes 15 and 31 (rows a broadcast does not write keep their own value);
+// lane 63 ends with the result, read back as a wave-uniform value.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+template <class Op>
+__device__ __forceinline__ float wave_reduce(float v, Op op) {
+  v = op(v, dpp_f32<0xB1, 0xf>(v));   // quad_perm [1, 0, 3, 2]
+  v = op(v, dpp_f32<0x4E, 0xf>(v));   // quad_perm [2, 3, 0, 1]
+  v = op(v, dpp_f32<0x141, 0xf>(v));  // row_half_mirror
+  v = op(v, dpp_f32<0x140, 0xf>(v));  // row_mirror
+  v = op(v, dpp_f32<0x142, 0xa>(v));  // row_bcast:15 into rows 1, 3
+  v = op(v, dpp_f32<0x143, 0xc>(v));  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float x, float y) { return fminf(x, y); });
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float x, float y) { return fmaxf(x, y); });
 }
 
 // block min/max -> atomic order-preserving keys (uses the first 2*NT/64 floats of smem after a barrier)
