@@ -36,7 +36,7 @@ extern "C" {
 /* error codes */
 #define TB_OK 0
 #define TB_ERR_INVALID_ARG 1
-#define TB_ERR_UNSUPPORTED_SIZE 2 /* an FFT length with a prime factor > 31, or a slab above LDS */
+#define TB_ERR_UNSUPPORTED_SIZE 2 /* an axis longer than the direct-DFT fallback takes (10240) */
 #define TB_ERR_HIP 3              /* a HIP runtime call failed; tb_last_hip_error() has the code */
 #define TB_ERR_WORKSPACE 4        /* workspace smaller than tb_workspace_bytes() */
 

@@ -76,6 +76,23 @@ bool kspace_ct_supported(int H);
 int kspace_ct_tile(int ncols);
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st);
 
+// Direct-DFT fallback (kern_generic.hip) for sizes the mixed-radix passes do not take: full complex
+// spectrum in two ping-pong buffers S[2][nbc][H][W][D] (gen_workspace_bytes).
+struct GenLaunch {
+  tb_plan_dev pl;
+  const float* x;
+  const int64_t* xs;
+  float* y;
+  const int64_t* ys;
+  cf* S;
+  int ypad, bc0, C, nbc;  // bc0 = first sample * C; ops->s[i] = the run's i-th sample
+  uint32_t* mm;
+  const BatchOps* ops;
+};
+size_t gen_workspace_bytes(int H, int W, int D, int bc);
+hipError_t launch_gen_filter(const GenLaunch& g, hipStream_t st);
+hipError_t launch_gen_logabs(const GenLaunch& g, double* out, hipStream_t st);
+
 #if defined(__HIPCC__)
 struct DevCtx {
   int tid, nthreads;

@@ -262,6 +262,7 @@ struct tb_plan {
   int NKP = 0;
   float* tds = nullptr;  // band pass C': [D/2 + 1][2][NCOLS] cos / sin(2 pi kd d / D), d < D/2 + 1, else 0
   float* tbt = nullptr;  // band pass A': [2][KSd][2][64] B fragments of the folded D product
+  bool generic = false;  // full-spectrum route on the direct-DFT fallback (kern_generic.hip)
 };
 
 namespace {
@@ -300,7 +301,7 @@ const char* tb_error_string(int code) {
   switch (code) {
     case TB_OK: return "ok";
     case TB_ERR_INVALID_ARG: return "invalid argument";
-    case TB_ERR_UNSUPPORTED_SIZE: return "unsupported transform size (prime factor > 31 or slab exceeds LDS)";
+    case TB_ERR_UNSUPPORTED_SIZE: return "unsupported transform size (an axis above the direct-DFT fallback's 10240)";
     case TB_ERR_HIP: return "HIP runtime error";
     case TB_ERR_WORKSPACE: return "workspace too small";
     default: return "unknown error";
@@ -314,7 +315,28 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   *out = nullptr;
   tb_plan* p = new tb_plan();
   int rc = build_tables(H, W, D, p->host);
-  if (rc != TB_OK) { delete p; return rc; }
+  if (rc == TB_ERR_UNSUPPORTED_SIZE) {
+    // an axis with a prime factor > 31: the full-spectrum route runs on the direct-DFT fallback
+    // (the band passes take any size); the mixed-radix tables are never read
+    p->generic = true;
+    const int n[3] = {H, W, D};
+    for (int a = 0; a < 3; ++a) {
+      if (!factorize(n[a], p->host.ax[a])) {
+        p->host.ax[a].n = n[a];
+        p->host.ax[a].nst = 0;
+      }
+      p->host.tw[a] = twiddles(n[a]);
+    }
+    p->host.rev_d.resize(D);
+    p->host.irev_h.resize(H);
+    p->host.irev_w.resize(W);
+    for (int i = 0; i < D; ++i) p->host.rev_d[i] = i;
+    for (int i = 0; i < H; ++i) p->host.irev_h[i] = i;
+    for (int i = 0; i < W; ++i) p->host.irev_w[i] = i;
+  } else if (rc != TB_OK) {
+    delete p;
+    return rc;
+  }
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { delete p; return hip_fail(hipGetLastError()); }
   int lds = 0;
@@ -324,10 +346,10 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
     p->ncu = ncu;
   // compile-time slab plan: same shape and therefore the same radix order as the runtime plan
-  p->ct_slab = tb::slab_ct_supported(W, D);
-  p->ct_tile = tb::kspace_ct_supported(H);
+  p->ct_slab = !p->generic && tb::slab_ct_supported(W, D);
+  p->ct_tile = !p->generic && tb::kspace_ct_supported(H);
   const SlabGeo sg = slab_geo(W, D);
-  if ((size_t)sg.total_cf * 8 > (size_t)p->lds_max) { delete p; return TB_ERR_UNSUPPORTED_SIZE; }
+  if ((size_t)sg.total_cf * 8 > (size_t)p->lds_max) p->generic = true;  // slab above the LDS: fallback too
   // device tables: tw[H], tw[W], tw[D] (cf) + rev_d[D], irev_h[H], irev_w[W] (int)
   const size_t ncf = (size_t)H + W + D, nint = (size_t)D + H + W;
   const size_t bytes = ncf * sizeof(cf) + nint * sizeof(int);
@@ -435,7 +457,9 @@ size_t tb_workspace_bytes(const tb_plan* plan, int bc) {
   g.KS = 32;
   g.NCOL = 32 * ((plan->dev.D / 2 + 1 + 31) / 32);
   const size_t band = band_ws(g, plan->dev.H, bc).total;
-  return spec > band ? spec : band;
+  const size_t gen = plan->generic ? gen_workspace_bytes(plan->dev.H, plan->dev.W, plan->dev.D, bc) : 0;
+  const size_t m = spec > band ? spec : band;
+  return m > gen ? m : gen;
 }
 
 int tb_plan_radices(const tb_plan* plan, int axis, int* radices) {
@@ -718,6 +742,19 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
   return TB_OK;
 }
 
+// full-spectrum route of a plan the mixed-radix passes do not take (tb_plan::generic)
+static int run_generic(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
+                       void* ws, int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax, hipStream_t st) {
+  BatchOps bo;
+  std::memset(&bo, 0, sizeof(bo));
+  for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
+  const double vox = (double)nb * C * p->dev.H * p->dev.W * p->dev.D;
+  Timer t(1, st, vox * (4.0 + 2.0 * 16.0 * 6.0 + 16.0 + 4.0), "k_gen_dft");
+  const GenLaunch g{p->dev, x, xs, y, ys, static_cast<cf*>(ws), y_pad, b0 * C, C, nb * C, minmax, &bo};
+  TB_HIP(tb::launch_gen_filter(g, st));
+  return TB_OK;
+}
+
 static int run_copy(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad, int b0,
                     int nb, int C, uint32_t* minmax, hipStream_t st) {
   const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
@@ -779,6 +816,8 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     else if (run.route == RUN_BAND)
       rc = run_band(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, run.s0, nb, C, ops, run.g, run.sp, minmax,
                     st);
+    else if (p->generic)
+      rc = run_generic(p, x, xs, y, ys, y_pad, ws, run.s0, nb, C, ops, minmax, st);
     else
       rc = run_full<RA, RB>(p, x, xs, y, ys, y_pad, static_cast<cf*>(ws), run.s0, nb, C, ops, minmax, st);
     if (rc) return rc;
@@ -799,6 +838,17 @@ static int kspace_stats(const tb_plan* p, const float* x, const int64_t* xs, voi
   const size_t lds_b = (size_t)tile_geo(H, T).total_cf * sizeof(cf);
   int rc = TB_OK;
   TB_HIP(hipMemsetAsync(out, 0, sizeof(double) * B * C, st));
+  if (p->generic) {
+    for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
+      const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
+      BatchOps bo;
+      std::memset(&bo, 0, sizeof(bo));
+      for (int i = 0; i < nb; ++i) bo.s[i] = ops[b0 + i];
+      const GenLaunch g{p->dev, x, xs, nullptr, nullptr, S, 0, b0 * C, C, nb * C, nullptr, &bo};
+      TB_HIP(tb::launch_gen_logabs(g, out, st));
+    }
+    return TB_OK;
+  }
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
     BatchOps bo;
