@@ -353,16 +353,18 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
 // ----------------------------------------------------------------------------- pass B'
 constexpr int BAND_MID_MAXH = 1024;  // slabs per bc whose twiddles / partial counts pass B' tabulates in LDS
 constexpr int BAND_MID_KG = 4;       // kh per pass-B' workgroup
+constexpr int BAND_MID_NW = 8;       // waves per pass-B' workgroup (they split h)
+constexpr int BAND_MID_NT = 64 * BAND_MID_NW;
 
 // One workgroup per (bc, 64 box columns, BAND_MID_KG consecutive kh): the slabs' pass-A' partials
 // are read once per kh group, the four waves split h, each lane holds Q(kh) of its column for the
 // group: Ac(kh) = sum_h P_h cos(2 pi kh h / H), As(kh) = sum_h P_h sin(..).  Then the waves' sums
 // meet in LDS and wave w finishes kh = kh0 + w: the sample's op program on Q(kh) and Q(-kh),
 // stored as their sum and difference AB[bc][kh][col].
-__global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
+__global__ __launch_bounds__(BAND_MID_NT) void k_band_mid(BandMidArgs) {
   const BandMidArgs& a = kargs<BandMidArgs>();
-  constexpr int KG = BAND_MID_KG;
-  __shared__ float4 red[4][KG][64];
+  constexpr int KG = BAND_MID_KG, NW = BAND_MID_NW;
+  __shared__ float4 red[NW][KG][64];
   __shared__ float2 twl[BAND_MID_MAXH];         // (cos, -sin)(2 pi t / H)
   __shared__ unsigned char nsg[BAND_MID_MAXH];  // pass-A' partials per slab
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
   const cf* Pc = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol + (live ? col : 0);
   const bool tab = H <= BAND_MID_MAXH;
   if (tab)
-    for (int hh = tid; hh < H; hh += BAND_NT) {
+    for (int hh = tid; hh < H; hh += BAND_MID_NT) {
       twl[hh] = ld2(a.pl.tw[0] + hh);
       nsg[hh] = (unsigned char)fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
     }
@@ -383,22 +385,22 @@ __global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
   float4 acc[KG];  // (Ac.re, Ac.im, As.re, As.im) of kh0 + k
 #pragma unroll
   for (int k = 0; k < KG; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int U = 4;  // slabs whose loads are in flight together
-  for (int h0 = wv; h0 < H; h0 += 4 * U) {
+  constexpr int U = 6;  // slabs whose loads are in flight together (3 partials each)
+  for (int h0 = wv; h0 < H; h0 += NW * U) {
     float2 p[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int hh = h0 + 4 * u < H ? h0 + 4 * u : H - 1;
+      const int hh = h0 + NW * u < H ? h0 + NW * u : H - 1;
       const int nseg = tab ? (int)nsg[hh] : fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
       const cf* ph = Pc + (int64_t)hh * BAND_FWD_SEGS * ncol;
       const float2 p0 = ld2(ph), p1 = ld2(ph + ncol), p2 = ld2(ph + 2 * ncol);  // stale slots masked below
       p[u].x = p0.x + (nseg > 1 ? p1.x : 0.f) + (nseg > 2 ? p2.x : 0.f);
       p[u].y = p0.y + (nseg > 1 ? p1.y : 0.f) + (nseg > 2 ? p2.y : 0.f);
-      if (h0 + 4 * u >= H) p[u] = make_float2(0.f, 0.f);
+      if (h0 + NW * u >= H) p[u] = make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int hh = h0 + 4 * u < H ? h0 + 4 * u : 0;
+      const int hh = h0 + NW * u < H ? h0 + NW * u : 0;
       int t = (int)(((int64_t)kh0 * hh) % H);
 #pragma unroll
       for (int k = 0; k < KG; ++k) {  // slots past KH accumulate too (never stored): no branches
@@ -421,10 +423,10 @@ __global__ __launch_bounds__(BAND_NT) void k_band_mid(BandMidArgs) {
     const int jw = col / NDk, kd = col - jw * NDk;
     const int kw = (jw - KW + W) % W;
     const FreqCol fc = freq_col(kw, kd, W, D);
-    for (int k = wv; k < KG && kh0 + k <= KH; k += 4) {
+    for (int k = wv; k < KG && kh0 + k <= KH; k += NW) {
       const int kh = kh0 + k;
       float4 q = red[0][k][lane];
-      for (int w_ = 1; w_ < 4; ++w_) {
+      for (int w_ = 1; w_ < NW; ++w_) {
         const float4 r = red[w_][k][lane];
         q.x += r.x; q.y += r.y; q.z += r.z; q.w += r.w;
       }
@@ -475,17 +477,21 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
   const int s = (a.cofs + bcl) / a.C;
   const float4* ABb = a.AB + (int64_t)bc * (KH + 1) * ncol;
   for (int col = lane; col < ncol; col += 64) {
-    const float4 a0 = ABb[col];
-    float zx = a0.x, zy = a0.y;
+    float zx = 0.f, zy = 0.f;
     int t = 0;
-    for (int k0 = 1; k0 <= KH; k0 += 4) {
-      float4 ab[4];
+    for (int k0 = 0; k0 <= KH; k0 += 16) {  // 16 kh rows' loads in flight (KH <= 15: one round)
+      float4 ab[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 16; ++q)
         if (k0 + q <= KH) ab[q] = ABb[(int64_t)(k0 + q) * ncol + col];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 16; ++q) {
         if (k0 + q > KH) break;
+        if (k0 + q == 0) {  // A_0
+          zx += ab[q].x;
+          zy += ab[q].y;
+          continue;
+        }
         t += h;
         t = t >= H ? t - H : t;
         const cf tw = a.pl.tw[0][t];  // (cos, -sin), wave-uniform
@@ -1003,7 +1009,7 @@ hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
 
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
   const dim3 grid((a.g.ncol + 63) / 64, (a.g.KH + BAND_MID_KG) / BAND_MID_KG, a.nbc);
-  hipLaunchKernelGGL(k_band_mid, grid, dim3(BAND_NT), 0, st, a);
+  hipLaunchKernelGGL(k_band_mid, grid, dim3(BAND_MID_NT), 0, st, a);
   hipError_t e;
   e = hipGetLastError();
   if (e != hipSuccess) return e;
