@@ -393,9 +393,12 @@ __global__ __launch_bounds__(BAND_MID_NT) void k_band_mid(BandMidArgs) {
       const int hh = h0 + NW * u < H ? h0 + NW * u : H - 1;
       const int nseg = tab ? (int)nsg[hh] : fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
       const cf* ph = Pc + (int64_t)hh * BAND_FWD_SEGS * ncol;
-      const float2 p0 = ld2(ph), p1 = ld2(ph + ncol), p2 = ld2(ph + 2 * ncol);  // stale slots masked below
-      p[u].x = p0.x + (nseg > 1 ? p1.x : 0.f) + (nseg > 2 ? p2.x : 0.f);
-      p[u].y = p0.y + (nseg > 1 ? p1.y : 0.f) + (nseg > 2 ? p2.y : 0.f);
+      // only the slab's live partial slots are read (nseg is wave-uniform: no divergence)
+      const float2 p0 = ld2(ph);
+      const float2 p1 = nseg > 1 ? ld2(ph + ncol) : make_float2(0.f, 0.f);
+      const float2 p2 = nseg > 2 ? ld2(ph + 2 * ncol) : make_float2(0.f, 0.f);
+      p[u].x = p0.x + p1.x + p2.x;
+      p[u].y = p0.y + p1.y + p2.y;
       if (h0 + NW * u >= H) p[u] = make_float2(0.f, 0.f);
     }
 #pragma unroll
