@@ -480,21 +480,17 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
   const int s = (a.cofs + bcl) / a.C;
   const float4* ABb = a.AB + (int64_t)bc * (KH + 1) * ncol;
   for (int col = lane; col < ncol; col += 64) {
-    float zx = 0.f, zy = 0.f;
+    const float4 a0 = ABb[col];
+    float zx = a0.x, zy = a0.y;
     int t = 0;
-    for (int k0 = 0; k0 <= KH; k0 += 16) {  // 16 kh rows' loads in flight (KH <= 15: one round)
-      float4 ab[16];
+    for (int k0 = 1; k0 <= KH; k0 += 4) {
+      float4 ab[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q)
+      for (int q = 0; q < 4; ++q)
         if (k0 + q <= KH) ab[q] = ABb[(int64_t)(k0 + q) * ncol + col];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < 4; ++q) {
         if (k0 + q > KH) break;
-        if (k0 + q == 0) {  // A_0
-          zx += ab[q].x;
-          zy += ab[q].y;
-          continue;
-        }
         t += h;
         t = t >= H ? t - H : t;
         const cf tw = a.pl.tw[0][t];  // (cos, -sin), wave-uniform

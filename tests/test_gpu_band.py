@@ -47,7 +47,10 @@ def spike(idx, spatial, li, phase=None, chan=-1, grouped=False):
     return op
 
 
-SHAPES = [(2, 4, 32, 30, 16), (2, 3, 24, 20, 15), (1, 2, 31, 17, 30), (1, 4, 128, 128, 128), (2, 4, 240, 240, 155)]
+# D mod 4 = 0, 3, 2, 1, 0, 0, 3: every mirror-store alignment of pass C'; D = 64, 128: the Nyquist
+# column summed on the VALU (D % 64 == 0)
+SHAPES = [(2, 4, 32, 30, 16), (2, 3, 24, 20, 15), (1, 2, 31, 17, 30), (1, 3, 20, 22, 33), (1, 2, 40, 36, 64),
+          (1, 4, 128, 128, 128), (2, 4, 240, 240, 155)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
