@@ -135,7 +135,10 @@ TB_HD size_t band_lds_fwd(const BandGeo& g, int W, int D, bool ct) {
   const size_t bt = ct ? 0 : (size_t)NT2 * KSd * 128 * 4;
   return tw + bt + (size_t)4 * band_fwd_xw(band_fwd_pitch(D, ct), NT2, KWT) * 4;
 }
-constexpr int BAND_SLOTS = 3;   // slabs whose pass-C' inputs a workgroup holds in LDS at once
+#ifndef TB_BAND_SLOTS
+#define TB_BAND_SLOTS 3
+#endif
+constexpr int BAND_SLOTS = TB_BAND_SLOTS;  // slabs whose pass-C' inputs a workgroup holds in LDS at once
 constexpr int BAND_STG_P = 36;  // pitch (floats) of a wave's staged 32 x 32 output half-tile
 struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
   int bimg, tww, frag, prow, pkw, stg, total;

@@ -552,8 +552,11 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
 //   y[w][d] = E - O,  y[w][D - d] = E + O   for d in [0, D/2]  (the C2R folded over d <-> D - d)
 // Each lane ends with 4 consecutive columns of one image row for both halves: 16-B stores.
 __device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
+#ifndef TB_INV_WPE
+#define TB_INV_WPE 3  // waves per SIMD the VT = 1 kernel is compiled for (register budget)
+#endif
 template <int VT>  // 32-row tiles of V (2 (NDk + points) <= 32 VT)
-__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1 ? 3 : 2, 4))) void k_band_inv(BandInvArgs) {
+__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1 ? TB_INV_WPE : 2, 4))) void k_band_inv(BandInvArgs) {
   // The workgroup takes its slabs in batches of BAND_SLOTS: the batch's inputs (V-product
   // fragments from pass B2', the samples' point rows of the synthesis table) are loaded into LDS
   // first, so that the (slab, 32-row tile) units the four waves then work through issue only
