@@ -182,8 +182,7 @@ hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st);  // sets a.
 bool band_fwd_use_ct(int D, int NT2);  // the compiled-D pass-A' kernel runs for this D
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st);
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);
-int band_inv_tiles(const BandGeo& g, int W);  // row tiles per slab of the pass-C' kernel that runs
-hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int ntw, hipStream_t st);
+hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st);
 
 // identity samples (empty program): strided copy + zero D-padding + min/max
 struct CopyArgs {

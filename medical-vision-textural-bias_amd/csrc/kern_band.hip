@@ -841,288 +841,13 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   }
 }
 
-// ----------------------------------------------------------------------------- pass C' (16-row units)
-// The k_band_inv<1> arithmetic on 16-row units and the 16x16x4 f32 MFMA, so that a wave holds half
-// the accumulators (V^T 8, E/O 16 registers instead of 16 + 32): <= 128 VGPRs and 34 KB of LDS per
-// workgroup give 4 waves per SIMD instead of 3 -- the grid sweep of DESIGN.md found C' bound by the
-// units in flight.  Layouts (16x16x4: A[l & 15][k = l >> 4], B[k = l >> 4][l & 15],
-// D[row 4 (l >> 4) + r][col l & 15]):
-//   V^T(v, w)  rows v = 16 vb + i, columns w = 16 tile + j;  k = (kw, cos/sin) terms, 4 per step,
-//              A = the pass-B2' fragments (their 32x32x2 order re-indexed), B = the twiddles
-//   E/O(d, w)  rows d, columns w;  k = rows v of V^T: step (vb, r) takes v = 16 vb + 4 (l >> 4) + r,
-//              i.e. V^T accumulator register r of block vb as it stands (r even: real rows -> E,
-//              r odd: imaginary rows -> O), A = the synthesis table at (v, d)
-constexpr int INV16_SLOTS = 2;
-struct Inv16Carve {
-  int bimg, tww, frag, prow, pkw, stg, total;
-};
-TB_HD Inv16Carve inv16_carve(const BandGeo& g, int W) {
-  const int npm = g.KS - g.NDk;
-  Inv16Carve c;
-  c.bimg = 0;
-  c.tww = band_al16(2 * g.NDk * g.NCOL * 4);
-  c.frag = band_al16(c.tww + W * 8);
-  c.prow = band_al16(c.frag + INV16_SLOTS * band_kv(g) * 64 * 4);
-  c.pkw = band_al16(c.prow + INV16_SLOTS * (2 * npm + 4) * g.NCOL * 4);
-  c.stg = band_al16(c.pkw + INV16_SLOTS * BAND_MAX_PTS * 4);
-  c.total = band_al16(c.stg + 4 * 16 * BAND_STG_P * 4);
-  return c;
-}
-
-__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_band_inv16(BandInvArgs) {
-  const BandInvArgs& a = kargs<BandInvArgs>();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = (int)threadIdx.x, lane = tid & 63, g4 = lane >> 4, l15 = lane & 15;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
-  const int NDk = a.g.NDk, KW = a.g.KW, NCOL = a.g.NCOL;
-  const int npm = a.g.KS - NDk;
-  const int KV = KW + 1 + npm;
-  const int Dh = D / 2 + 1;
-  const int nrv = 2 * (NDk + npm);
-  const int fsz = KV * 64;
-  const int psz = (2 * npm + 4) * NCOL;
-  const Inv16Carve cv = inv16_carve(a.g, W);
-  float* Bimg = reinterpret_cast<float*>(smem + cv.bimg);
-  float2* twW = reinterpret_cast<float2*>(smem + cv.tww);
-  float* Fs = reinterpret_cast<float*>(smem + cv.frag);
-  float* Ps = reinterpret_cast<float*>(smem + cv.prow);
-  float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 16 * BAND_STG_P;  // this wave's 16 x 32 tile
-  int* Pkw = reinterpret_cast<int*>(smem + cv.pkw);
-  const int nbi4 = 2 * NDk * NCOL / 4;
-  const bool twv = !(W & 1) && (reinterpret_cast<uintptr_t>(a.pl.tw[1]) & 15) == 0;
-  const int ntw4 = twv ? W / 2 : 0;
-  if (!twv) lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
-  const float4* Tsrc = reinterpret_cast<const float4*>(a.tds);
-  const float4* Wsrc = reinterpret_cast<const float4*>(a.pl.tw[1]);
-  int tb4 = nbi4 + ntw4;
-  const int ntw = (W + 15) / 16;     // 16-row tiles of a slab
-  const int nslab = H * a.nbc;
-  const int ntn = NCOL / 32;
-  const int ypad = a.ypad;
-  const bool mal = ((D - 3) & 3) == 0;
-  const int diag = a.diag;
-  const int nst = (2 * KV + 3) / 4;  // V-product k-steps of 4 terms
-  const int nunit = nslab * ntw;
-  const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int ub = (int)blockIdx.x * per, ue = ub + per < nunit ? ub + per : nunit;
-  for (int c0 = ub; c0 < ue;) {
-    const int s0 = c0 / ntw;
-    const int slast = (ue - 1) / ntw;
-    const int s1 = slast < s0 + INV16_SLOTS - 1 ? slast : s0 + INV16_SLOTS - 1;
-    const int c1 = (s1 + 1) * ntw < ue ? (s1 + 1) * ntw : ue;
-    const int nb = s1 - s0 + 1;
-    __syncthreads();
-    {
-      const int nf4 = nb * fsz / 4, np4 = nb * psz / 4, nc4 = NCOL / 4, pp4 = psz / 4;
-      const int ntot = tb4 + nf4 + np4;
-      const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
-      for (int base = 0; base < ntot; base += 9 * BAND_NT) {
-        float4 v[9];
-#pragma unroll
-        for (int u = 0; u < 9; ++u) {
-          const int e = base + u * BAND_NT + tid;
-          const int q = e - tb4;
-          if (e < tb4) {
-            v[u] = e < nbi4 ? Tsrc[e] : Wsrc[e - nbi4];
-          } else if (q < nf4 || e >= ntot) {
-            v[u] = F4[(q < nf4 && q >= 0) ? q : 0];
-          } else {
-            const int qq = q - nf4, i = qq / pp4, rem = qq - i * pp4, r = rem / nc4, n = rem - r * nc4, j = r >> 1;
-            const BandSamplePts& sp = a.sp[(a.cofs + (s0 + i) / H) / a.C];
-            v[u] = j < sp.n ? reinterpret_cast<const float4*>(a.tds + (2 * sp.p[j].kd + (r & 1)) * NCOL)[n]
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 9; ++u) {
-          const int e = base + u * BAND_NT + tid;
-          const int q = e - tb4;
-          if (e < tb4) {
-            if (e < nbi4)
-              reinterpret_cast<float4*>(Bimg)[e] = v[u];
-            else
-              reinterpret_cast<float4*>(twW)[e - nbi4] = v[u];
-          } else if (q < nf4) {
-            reinterpret_cast<float4*>(Fs)[q] = v[u];
-          } else if (e < ntot) {
-            reinterpret_cast<float4*>(Ps)[q - nf4] = v[u];
-          }
-        }
-      }
-      tb4 = 0;
-      if (tid < nb * BAND_MAX_PTS) {
-        const int i = tid / BAND_MAX_PTS, j = tid - i * BAND_MAX_PTS;
-        const BandSamplePts& sp = a.sp[(a.cofs + (s0 + i) / H) / a.C];
-        Pkw[tid] = j < sp.n ? (int)sp.p[j].kw : 0;
-      }
-    }
-    __syncthreads();
-    for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {
-      const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
-      const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
-      const float* Fb = Fs + slot * fsz;
-      const float* Pr = Ps + slot * psz;
-      const int wm = (16 * tw_ + l15) % W;
-      f32x4 vacc[2];
-#pragma unroll
-      for (int vb = 0; vb < 2; ++vb) vacc[vb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // V product: this lane's k-term of step s is kk = 4 s + g4 = 2 ks + c (ks: kw or point slot)
-      const int c = g4 & 1;
-      const int inc = (2 * wm) % W;  // ks advances by 2 per step
-      int t = ((g4 >> 1) * wm) % W;  // (ks wm) mod W for the band terms
-      for (int s = 0; s < ((diag & 4) ? 0 : nst); ++s) {
-        const int kk = 4 * s + g4, ks = kk >> 1;
-        float b;
-        if (ks <= KW) {
-          const float2 tw = twW[t];
-          b = c ? -tw.y : tw.x;
-        } else {
-          const int kw = ks < KV ? Pkw[slot * BAND_MAX_PTS + ks - KW - 1] : 0;
-          const float2 tw = twW[(kw * wm) % W];
-          b = c ? -tw.y : tw.x;
-        }
-        const int fo = kk < 2 * KV ? ks * 64 + c * 32 + l15 : -1;
-#pragma unroll
-        for (int vb = 0; vb < 2; ++vb) {
-          const float av = fo >= 0 ? Fb[fo + 16 * vb] : 0.f;
-          vacc[vb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b, vacc[vb], 0, 0, 0);
-        }
-        t += inc;
-        t = t >= W ? t - W : t;
-      }
-      float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
-      const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
-      float lo = 3.402823466e38f, hi = -3.402823466e38f;
-      for (int nt = 0; nt < ntn; ++nt) {
-        f32x4 ye[2], yo[2];
-#pragma unroll
-        for (int db = 0; db < 2; ++db) ye[db] = yo[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!(diag & 8)) {
-          float at[2][2][4];  // [db][vb][r]: the table at (v = 16 vb + 4 g4 + r, d = 32 nt + 16 db + l15)
-#pragma unroll
-          for (int db = 0; db < 2; ++db)
-#pragma unroll
-            for (int vb = 0; vb < 2; ++vb)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int v0 = 16 * vb + 4 * g4 + r;
-                const int v = v0 < nrv ? v0 : 0;  // rows past nrv meet zero V^T rows
-                const int d = 32 * nt + 16 * db + l15;
-                at[db][vb][r] = v < 2 * NDk ? Bimg[v * NCOL + d] : Pr[(v - 2 * NDk) * NCOL + d];
-              }
-#pragma unroll
-          for (int vb = 0; vb < 2; ++vb) {
-            if (16 * vb >= nrv) break;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              if (16 * vb + r >= nrv) break;  // every lane group's row past nrv: zero step
-#pragma unroll
-              for (int db = 0; db < 2; ++db) {
-                if (r & 1)
-                  yo[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(at[db][vb][r], vacc[vb][r], yo[db], 0, 0, 0);
-                else
-                  ye[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(at[db][vb][r], vacc[vb][r], ye[db], 0, 0, 0);
-              }
-            }
-          }
-        }
-        if (diag & 16) continue;
-        const int c4 = lane & 7;
-        const int dbase = nt * 32 + 4 * c4, dmir = nt * 32 + 31 - 4 * c4;
-        const bool padlane = nt == 0 && c4 == 7 && ypad > 0;
-        int nd = 0, nm = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          nd += dbase + q < Dh ? 1 : 0;
-          const int d = dmir - q;
-          nm += ((d >= 1 && 2 * d < D && d < Dh) || (padlane && d == 0)) ? 1 : 0;
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            f32x4 v;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (half == 0)
-                v[q] = ye[db][q] - yo[db][q];
-              else
-                v[3 - q] = ye[db][q] + yo[db][q];
-            }
-            const int col = half == 0 ? 16 * db + 4 * g4 : 28 - 16 * db - 4 * g4;
-            *reinterpret_cast<f32x4*>(stg + l15 * BAND_STG_P + col) = v;
-          }
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int r = (lane >> 3) + 8 * k;
-            const int wr = 16 * tw_ + r;
-            if (wr >= W) continue;
-            f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 4 * c4);
-            float* yrr = yb + (int64_t)wr * a.sw;
-            if (half == 0) {
-              if (vec && nd == 4) {
-                *reinterpret_cast<f32x4*>(yrr + dbase) = v;
-                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], v[3])));
-                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-              } else if (nd > 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                  if (q < nd) {
-                    yrr[dbase + q] = v[q];
-                    lo = fminf(lo, v[q]);
-                    hi = fmaxf(hi, v[q]);
-                  }
-              }
-            } else {
-              if (padlane) v[3] = 0.f;
-              if (vec && mal && nm == 4) {
-                *reinterpret_cast<f32x4*>(yrr + D - dmir) = v;
-                const float m3 = padlane ? v[2] : v[3];
-                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], m3)));
-                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], m3)));
-              } else if (nm > 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  const int d = dmir - q;
-                  if (d >= 1 && 2 * d < D && d < Dh) {
-                    yrr[D - d] = v[q];
-                    lo = fminf(lo, v[q]);
-                    hi = fmaxf(hi, v[q]);
-                  } else if (padlane && d == 0) {
-                    yrr[D] = 0.f;
-                  }
-                }
-              }
-              if (padlane) {
-                int p = 1;
-                for (; p < ypad && ((D + p) & 3); ++p) yrr[D + p] = 0.f;
-                if (vec)
-                  for (; p + 4 <= ypad; p += 4) *reinterpret_cast<f32x4*>(yrr + D + p) = f32x4{0.f, 0.f, 0.f, 0.f};
-                for (; p < ypad; ++p) yrr[D + p] = 0.f;
-              }
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-      if (a.mm) {  // per-(slab, 16-row tile) partial
-        lo = wave_min(lo);
-        hi = wave_max(hi);
-        if (lane == 0) a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
-      }
-    }
-    c0 = c1;
-  }
-}
-
 // per-sample keys of the slab partials: one workgroup per sample
 __global__ __launch_bounds__(256) void k_band_minmax(const float2* __restrict__ mmp, uint32_t* __restrict__ mm, int bc0,
-                                                     int C, int H, int ntw) {
+                                                     int C, int H, int W) {
   __shared__ float red[2 * 256 / 64];
   const int b = (int)blockIdx.x;
-  const int64_t n = (int64_t)C * H * ntw;  // one partial per (slab, row tile)
+  const int ntw = (W + 31) / 32;
+  const int64_t n = (int64_t)C * H * ntw;  // one partial per (slab, 32-row tile)
   const float2* p = mmp + (int64_t)b * C * H * ntw;
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
   int64_t i0 = 0;
@@ -1296,43 +1021,12 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
 
 
 
-// the 16-row kernel for V^T of <= 32 rows, while a slab's (min, max) partials fit the workspace
-static bool use_inv16(const BandGeo& g, int W) {
-  static const bool on = [] {  // TEXBIAS_INV16=1: the 16-row kernel (measurement; off by default)
-    const char* e = std::getenv("TEXBIAS_INV16");
-    return e && e[0] == '1';
-  }();
-  return on && 2 * g.KS <= 32 && (W + 15) / 16 <= 32;
-}
-
-int band_inv_tiles(const BandGeo& g, int W) { return use_inv16(g, W) ? (W + 15) / 16 : (W + 31) / 32; }
-
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
-  if (use_inv16(a.g, a.pl.W)) {
-    const size_t lds = inv16_carve(a.g, a.pl.W).total;
-    hipError_t e = allow_lds(k_band_inv16, lds);
-    if (e != hipSuccess) return e;
-    static size_t last_lds = ~(size_t)0;
-    static int last_occ = 1;
-    if (lds != last_lds) {
-      int occ = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_band_inv16, BAND_NT, lds) != hipSuccess || occ < 1)
-        occ = (int)(163840 / lds);
-      last_occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
-      last_lds = lds;
-      if (std::getenv("TEXBIAS_BAND_VERBOSE"))
-        std::fprintf(stderr, "[texbias] band inv16: lds %zu B, %d workgroups/CU\n", lds, occ);
-    }
-    const int units = a.pl.H * a.nbc;
-    const int g = ncu * last_occ;
-    hipLaunchKernelGGL(k_band_inv16, dim3(units < g ? units : g), dim3(BAND_NT), lds, st, a);
-    return hipGetLastError();
-  }
   return 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
 }
 
-hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int ntw, hipStream_t st) {
-  hipLaunchKernelGGL(k_band_minmax, dim3(nbc / C), dim3(256), 0, st, mmp, mm, bc0, C, H, ntw);
+hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(k_band_minmax, dim3(nbc / C), dim3(256), 0, st, mmp, mm, bc0, C, H, W);
   return hipGetLastError();
 }
 

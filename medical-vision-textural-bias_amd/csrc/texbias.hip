@@ -738,9 +738,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
     TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
   }
-  if (minmax)
-    TB_HIP(tb::launch_band_minmax(reinterpret_cast<float2*>(ws + wl.off_mmp), minmax, b0 * C, C, nbc, H,
-                                  tb::band_inv_tiles(g, W), st));
+  if (minmax) TB_HIP(tb::launch_band_minmax(reinterpret_cast<float2*>(ws + wl.off_mmp), minmax, b0 * C, C, nbc, H, W, st));
   return TB_OK;
 }
 
