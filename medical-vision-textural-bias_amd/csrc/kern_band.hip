@@ -552,6 +552,9 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
 //   y[w][d] = E - O,  y[w][D - d] = E + O   for d in [0, D/2]  (the C2R folded over d <-> D - d)
 // Each lane ends with 4 consecutive columns of one image row for both halves: 16-B stores.
 __device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
+#ifndef TB_INV_PRIO
+#define TB_INV_PRIO 2  // 2: store phases at raised wave priority (C3 -2 %, C2 -5 %); 1: MFMA phases; 0: off
+#endif
 #ifndef TB_INV_WPE
 #define TB_INV_WPE 3  // waves per SIMD the VT = 1 kernel is compiled for (register budget)
 #endif
@@ -670,6 +673,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
       for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
         for (int j = 0; j < 16; ++j) vacc[vt][j] = 0.f;
+      if (TB_INV_PRIO) __builtin_amdgcn_s_setprio(TB_INV_PRIO == 1 ? 2 : 0);
       int t = 0;
       const int kse = (diag & 4) ? 0 : KW + 1;
       int ks = 0;
@@ -715,6 +719,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
       const float* Tb = Bimg + l31;
       const float* Tp = Pr + l31 - 2 * NDk * NCOL;
       for (int nt = 0; nt < ntn; ++nt) {
+        if (TB_INV_PRIO) __builtin_amdgcn_s_setprio(TB_INV_PRIO == 1 ? 2 : 0);
         f32x16 ye, yo;
 #pragma unroll
         for (int j = 0; j < 16; ++j) ye[j] = yo[j] = 0.f;
@@ -748,6 +753,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
               }
             }
           }
+        if (TB_INV_PRIO) __builtin_amdgcn_s_setprio(TB_INV_PRIO == 1 ? 0 : 2);
         if (diag & 16) continue;
         // y[w][d] = E - O (direct half), then y[w][D - d] = E + O (mirror half), each staged
         // [row][32] through LDS so that every store instruction writes whole 128-B row segments
