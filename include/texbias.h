@@ -282,6 +282,15 @@ const char* tb_pass_kernel(int slot);
  */
 int tb_set_band_plans(int enable);
 
+/*
+ * Pass C' of the band-limited plans synthesises the image on the f16 matrix cores in split
+ * precision (table and V each as an f16 hi/lo pair, three products, f32 accumulation; agrees with
+ * the f32 synthesis to a few 1e-7 of max |y|) whenever the launch's band columns plus all of its
+ * samples' out-of-box spike points number at most 32; otherwise, or after tb_set_band_inv16(0)
+ * (TEXBIAS_INV16=0 in the environment), the f32 MFMA synthesis.  Default on.
+ */
+int tb_set_band_inv16(int enable);
+
 #ifdef __cplusplus
 }
 #endif

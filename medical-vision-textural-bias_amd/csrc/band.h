@@ -53,7 +53,11 @@ struct BandGeo {
   int NW, ncol;     // 2 KW + 1, NW * NDk  (a "column" = one (kw, kd) pair of the box)
   int KS;           // k-steps of the inverse D MFMA: NDk band columns + the launch's max points
   int NCOL;         // folded output columns of the MFMA n-tiles: 32 * ceil((D/2 + 1) / 32)
+  int cat;          // 1: split-f16 pass C' (k_band_inv16) -- every sample's points get their own V rows
+  int PT;           // cat: points of the whole launch (rows 2 (NDk + p0[s] + j) hold sample s's point j)
 };
+// rows of V (2 per kd band column / point) and its 32-row MFMA tiles
+TB_HD int band_rows(const BandGeo& g) { return 2 * (g.cat ? g.NDk + g.PT : g.KS); }
 
 // Pass A''s division of the launch's T = slabs x nst 16-row strips among G waves: wave w takes
 // strips [w T / G, (w + 1) T / G).  G <= T / ceil(nst / 2), so a slab spans at most 3 waves.
@@ -96,6 +100,9 @@ struct BandMidArgs {
   BandGeo g;
   FwdSplit split;   // pass A''s strip division (how many partial sums each slab has)
   BandSamplePts sp[TB_MAX_BATCH];
+  int p0[TB_MAX_BATCH];  // g.cat: the first V point row (pair) of each sample of the launch
+  void* T16;        // g.cat: synthesis-table fragments for pass C' (written by k_band_tab16)
+  const float* tds; // g.cat: [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   BatchOps ops;
 };
 
@@ -114,6 +121,7 @@ struct BandInvArgs {
   BandSamplePts sp[TB_MAX_BATCH];
   int diag;
   const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
+  const void* T16;  // g.cat: split-f16 synthesis-table fragments (k_band_tab16)
 };
 
 // Pass A': LDS row pitch of a staged strip.  Odd D: D (the strip is one contiguous run, 16-B
@@ -144,7 +152,7 @@ struct BandInvCarve {  // byte offsets of the pass-C' LDS regions (16-B aligned)
   int bimg, tww, frag, prow, pkw, stg, total;
 };
 TB_HD int band_al16(int b) { return (b + 15) & ~15; }
-TB_HD int band_vt(const BandGeo& g) { return 2 * g.KS <= 32 ? 1 : 2; }  // 32-row tiles of V
+TB_HD int band_vt(const BandGeo& g) { return band_rows(g) <= 32 ? 1 : 2; }  // 32-row tiles of V
 TB_HD int band_kv(const BandGeo& g) { return g.KW + 1 + (g.KS - g.NDk); }
 TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
   (void)D;
@@ -160,9 +168,29 @@ TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
   return c;
 }
 
+// Split-f16 pass C' (k_band_inv16): the synthesis table as MFMA A fragments
+// [ntn][nch][dir/mirror][hi/lo][64 lanes][8 halves] (ntn = NCOL / 32 column tiles, nch = 16-row
+// chunks of V), then the W twiddles, BAND_SLOTS16 slabs' V-product fragments, point kw, staging.
+constexpr int BAND_SLOTS16 = 2;
+TB_HD int band_nch(const BandGeo& g) { return (band_rows(g) + 15) / 16; }
+TB_HD int band_t16_bytes(const BandGeo& g) { return (g.NCOL / 32) * band_nch(g) * 4 * 64 * 16; }
+struct BandInv16Carve {
+  int tab, tww, frag, pkw, stg, total;
+};
+TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W) {
+  BandInv16Carve c;
+  c.tab = 0;
+  c.tww = band_al16(band_t16_bytes(g));
+  c.frag = band_al16(c.tww + W * 8);
+  c.pkw = band_al16(c.frag + BAND_SLOTS16 * band_vt(g) * band_kv(g) * 64 * 4);
+  c.stg = band_al16(c.pkw + BAND_SLOTS16 * BAND_MAX_PTS * 4);
+  c.total = band_al16(c.stg + 4 * 32 * BAND_STG_P * 4);
+  return c;
+}
+
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels
 struct BandWs {
-  size_t off_P, off_AB, off_pts, off_mmp, off_m2f, total;
+  size_t off_P, off_AB, off_pts, off_mmp, off_m2f, off_t16, total;
 };
 TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   BandWs w;
@@ -173,7 +201,9 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   w.off_mmp = w.off_pts + (size_t)bcn * BAND_MAX_PTS * 8;
   w.off_m2f = w.off_mmp + (size_t)bcn * H * 32 * 8;  // (min, max) per (slab, 32-row tile), W <= 1024
   w.off_m2f = (w.off_m2f + 255) & ~(size_t)255;
-  w.total = w.off_m2f + (size_t)bcn * H * band_vt(g) * band_kv(g) * 64 * 4;
+  w.off_t16 = w.off_m2f + (size_t)bcn * H * band_vt(g) * band_kv(g) * 64 * 4;
+  w.off_t16 = (w.off_t16 + 255) & ~(size_t)255;
+  w.total = w.off_t16 + (size_t)band_t16_bytes(g);
   return w;
 }
 
@@ -181,7 +211,7 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
 hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st);  // sets a.split
 bool band_fwd_use_ct(int D, int NT2);  // the compiled-D pass-A' kernel runs for this D
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st);
-hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);
+hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);  // g.cat: k_band_inv16
 hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st);
 
 // identity samples (empty program): strided copy + zero D-padding + min/max

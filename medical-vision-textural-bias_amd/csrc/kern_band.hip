@@ -10,6 +10,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "band.h"
 
@@ -514,7 +517,8 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes have landed
   __builtin_amdgcn_wave_barrier();
   const float2* Zb = zs[wv];
-  const int nrv = 2 * (NDk + npm);
+  const int nrv = band_rows(a.g);
+  const int pbase = a.g.cat ? a.p0[s] : 0;  // g.cat: this sample's first point row pair past the band rows
   float* F = a.M2F + (int64_t)u * VT * KV * 64;
   for (int vt = 0; vt < VT; ++vt)
     for (int ks = 0; ks < KV; ++ks) {
@@ -531,9 +535,12 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
             const float wt = ((kd == 0 || 2 * kd == D) ? 1.f : 2.f) * a.scale;
             v = (im ? (sn ? bx : ay) : (sn ? -by : ax)) * wt;
           }
-        } else if (ks == KW + 1 + (kd - NDk)) {
-          const float2 c = phs[wv][kd - NDk];
-          v = im ? (sn ? c.x : c.y) : (sn ? -c.y : c.x);
+        } else {
+          const int j = kd - NDk - pbase;  // the sample's point j (its own V-product k-step KW + 1 + j)
+          if (j >= 0 && j < sp.n && ks == KW + 1 + j) {
+            const float2 c = phs[wv][j];
+            v = im ? (sn ? c.x : c.y) : (sn ? -c.y : c.x);
+          }
         }
       }
       F[((int64_t)vt * KV + ks) * 64 + lane] = v;
@@ -847,6 +854,322 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   }
 }
 
+// ----------------------------------------------------------------------------- pass C' (split f16)
+// The C2R synthesis y = T . V in split precision on the f16 matrix cores (16x the f32 MFMA rate):
+// T = Th + Tl (the constant cos/sin table, scaled by 2^8), V = Vh + Vl (the V-product accumulators,
+// scaled by a power of two per unit so that max |V| < 2^15), y = (Th Vh + Th Vl + Tl Vh) / scale.
+// Each f16 pair carries 22 bits of the value and the dropped Tl Vl term is 2^-22 relative, so the
+// result matches the f32 synthesis to a few 1e-7 of max |y|.  Both halves of the folded C2R come
+// straight out of the MFMA (dir: cos, -sin; mirror: cos, +sin) instead of E -/+ O on the VALU.
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+constexpr float BAND_T16_SCALE = 256.f;
+
+__device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
+  h = (_Float16)x;
+  l = (_Float16)(x - (float)h);
+}
+
+// One thread per (column tile, 16-row chunk, dir/mirror, lane): the lane's 8 A-fragment entries,
+// k-permuted to match the accumulator-as-B-operand order of the V tile (element j of lane half h is
+// V row 16 c + 8 (j >> 2) + 4 h + (j & 3)); rows 2 kd + (re, im), band columns first, then every
+// sample's out-of-box points in launch order.
+__global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
+  const BandMidArgs& a = kargs<BandMidArgs>();
+  const int nch = band_nch(a.g), ntn = a.g.NCOL / 32, NCOL = a.g.NCOL, NDk = a.g.NDk;
+  const int t = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (t >= ntn * nch * 2 * 64) return;
+  const int lane = t & 63, dm = (t >> 6) & 1, cc = t >> 7, c = cc % nch, nt = cc / nch;
+  const int d = 32 * nt + (lane & 31), hl = lane >> 5;
+  h16x8 fh, fl;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int v = 16 * c + 8 * (j >> 2) + 4 * hl + (j & 3);
+    const int pr = v >> 1, im = v & 1;
+    int kd = -1;
+    if (pr < NDk) {
+      kd = pr;
+    } else {
+      int gp = pr - NDk;
+      for (int s = 0; s < TB_MAX_BATCH && kd < 0; ++s)
+        if (gp >= a.p0[s] && gp < a.p0[s] + a.sp[s].n) kd = a.sp[s].p[gp - a.p0[s]].kd;
+    }
+    float tv = 0.f;
+    if (kd >= 0) {
+      tv = a.tds[(2 * kd + im) * NCOL + d];  // zero past d = D/2
+      if (im && !dm) tv = -tv;               // dir: cos, -sin; mirror: cos, +sin
+    }
+    _Float16 h, l;
+    split_f16(tv * BAND_T16_SCALE, h, l);
+    fh[j] = h;
+    fl[j] = l;
+  }
+  h16x8* T = reinterpret_cast<h16x8*>(a.T16);
+  const int base = ((cc * 2 + dm) * 2) * 64 + lane;
+  T[base] = fh;
+  T[base + 64] = fl;
+}
+
+template <int VT>  // 32-row tiles of V
+__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4))) void k_band_inv16(BandInvArgs) {
+  // Same unit structure as k_band_inv (V product on f32 MFMA from LDS-resident fragments, LDS-staged
+  // 128-B row-segment stores, per-unit min/max partials); the synthesis table is the launch's
+  // split-f16 fragment image (k_band_tab16), copied to LDS once per workgroup.
+  const BandInvArgs& a = kargs<BandInvArgs>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63, hl = lane >> 5, l31 = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
+  const int KW = a.g.KW, NCOL = a.g.NCOL;
+  const int npm = a.g.KS - a.g.NDk;    // point k-steps of the V product (max points per sample)
+  const int KV = KW + 1 + npm;
+  const int Dh = D / 2 + 1;
+  const int nch = band_nch(a.g);       // 16-row chunks of V in use
+  const int fsz = VT * KV * 64;
+  const BandInv16Carve cv = band_inv16_carve(a.g, W);
+  const h16x8* Tab = reinterpret_cast<const h16x8*>(smem + cv.tab);  // [nt][c][dm][part][64]
+  float2* twW = reinterpret_cast<float2*>(smem + cv.tww);
+  float* Fs = reinterpret_cast<float*>(smem + cv.frag);
+  int* Pkw = reinterpret_cast<int*>(smem + cv.pkw);
+  float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 32 * BAND_STG_P;
+  const int ntab4 = band_t16_bytes(a.g) / 16;
+  const bool twv = !(W & 1) && (reinterpret_cast<uintptr_t>(a.pl.tw[1]) & 15) == 0;
+  const int ntw4 = twv ? W / 2 : 0;
+  if (!twv) lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  const float4* Tsrc = reinterpret_cast<const float4*>(a.T16);
+  const float4* Wsrc = reinterpret_cast<const float4*>(a.pl.tw[1]);
+  int tb4 = ntab4 + ntw4;
+  const int ntw = (W + 31) / 32;
+  const int nslab = H * a.nbc;
+  const int ntn = NCOL / 32;
+  const int ypad = a.ypad;
+  const bool mal = ((D - 3) & 3) == 0;
+  const int nunit = nslab * ntw;
+  const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int ub = (int)blockIdx.x * per, ue = ub + per < nunit ? ub + per : nunit;
+  for (int c0 = ub; c0 < ue;) {
+    const int s0 = c0 / ntw;
+    const int slast = (ue - 1) / ntw;
+    const int s1 = slast < s0 + BAND_SLOTS16 - 1 ? slast : s0 + BAND_SLOTS16 - 1;
+    const int c1 = (s1 + 1) * ntw < ue ? (s1 + 1) * ntw : ue;
+    const int nb = s1 - s0 + 1;
+    __syncthreads();
+    {  // [tables,] the batch's V-product fragments: rounds of loads in flight
+      const int nf4 = nb * fsz / 4;
+      const int ntot = tb4 + nf4;
+      const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
+      for (int base = 0; base < ntot; base += 9 * BAND_NT) {
+        float4 v[9];
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+          const int e = base + u * BAND_NT + tid;
+          const int q = e - tb4;
+          if (e < tb4)
+            v[u] = e < ntab4 ? Tsrc[e] : Wsrc[e - ntab4];
+          else
+            v[u] = F4[(q < nf4 && q >= 0) ? q : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+          const int e = base + u * BAND_NT + tid;
+          const int q = e - tb4;
+          if (e < tb4) {
+            if (e < ntab4)
+              reinterpret_cast<float4*>(smem + cv.tab)[e] = v[u];
+            else
+              reinterpret_cast<float4*>(twW)[e - ntab4] = v[u];
+          } else if (q < nf4) {
+            reinterpret_cast<float4*>(Fs)[q] = v[u];
+          }
+        }
+      }
+      tb4 = 0;
+      if (tid < nb * BAND_MAX_PTS) {
+        const int i = tid / BAND_MAX_PTS, j = tid - i * BAND_MAX_PTS;
+        const BandSamplePts& sp = a.sp[(a.cofs + (s0 + i) / H) / a.C];
+        Pkw[tid] = j < sp.n ? (int)sp.p[j].kw : 0;
+      }
+    }
+    __syncthreads();
+    for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {
+      const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
+      const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
+      const float* F = Fs + slot * fsz + lane;
+      const int w = 32 * tw_ + l31;
+      const int wm = w % W;
+      f32x16 vacc[VT];
+#pragma unroll
+      for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) vacc[vt][j] = 0.f;
+      __builtin_amdgcn_s_setprio(0);
+      int t = 0;
+      int ks = 0;
+      for (; ks + 4 <= KW + 1; ks += 4) {
+        float fa[4][VT], bb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float2 c = twW[t];
+          bb[q] = hl ? -c.y : c.x;
+#pragma unroll
+          for (int vt = 0; vt < VT; ++vt) fa[q][vt] = F[(vt * KV + ks + q) * 64];
+          t += wm;
+          t = t >= W ? t - W : t;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int vt = 0; vt < VT; ++vt)
+            vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][vt], bb[q], vacc[vt], 0, 0, 0);
+      }
+      for (; ks < KW + 1; ++ks) {
+        const float2 c = twW[t];
+        const float b = hl ? -c.y : c.x;
+#pragma unroll
+        for (int vt = 0; vt < VT; ++vt)
+          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(F[(vt * KV + ks) * 64], b, vacc[vt], 0, 0, 0);
+        t += wm;
+        t = t >= W ? t - W : t;
+      }
+      for (int j = 0; j < npm; ++j) {
+        const int kw = Pkw[slot * BAND_MAX_PTS + j];
+        const float2 c = twW[(kw * wm) % W];
+        const float b = hl ? -c.y : c.x;
+#pragma unroll
+        for (int vt = 0; vt < VT; ++vt)
+          vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(F[(vt * KV + KW + 1 + j) * 64], b, vacc[vt], 0, 0, 0);
+      }
+      // V as split-f16 B operands: chunk c = 2 vt + q is registers 8 q .. 8 q + 7 of vacc[vt]
+      float m = 0.f;
+#pragma unroll
+      for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(vacc[vt][j]));
+      m = wave_max(m);
+      int ex;
+      (void)frexpf(m, &ex);          // m < 2^ex
+      const float sv = ldexpf(1.f, 15 - ex), inv = ldexpf(1.f, ex - 15) * (1.f / BAND_T16_SCALE);
+      h16x8 bh[2 * VT], bl[2 * VT];
+#pragma unroll
+      for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            _Float16 hh, ll;
+            split_f16(vacc[vt][8 * q + j] * sv, hh, ll);
+            bh[2 * vt + q][j] = hh;
+            bl[2 * vt + q][j] = ll;
+          }
+      float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
+      const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
+      float lo = 3.402823466e38f, hi = -3.402823466e38f;
+      for (int nt = 0; nt < ntn; ++nt) {
+        __builtin_amdgcn_s_setprio(0);
+        f32x16 ye, yo;  // ye: y[d] (dir), yo: y[D - d] (mirror), d = 32 nt + row
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ye[j] = yo[j] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 2 * VT; ++c) {
+          if (c >= nch) break;
+          const h16x8* tp = Tab + ((nt * nch + c) * 4) * 64 + lane;
+          const h16x8 adh = tp[0], adl = tp[64], amh = tp[128], aml = tp[192];
+          ye = __builtin_amdgcn_mfma_f32_32x32x16_f16(adl, bh[c], ye, 0, 0, 0);
+          yo = __builtin_amdgcn_mfma_f32_32x32x16_f16(aml, bh[c], yo, 0, 0, 0);
+          ye = __builtin_amdgcn_mfma_f32_32x32x16_f16(adh, bl[c], ye, 0, 0, 0);
+          yo = __builtin_amdgcn_mfma_f32_32x32x16_f16(amh, bl[c], yo, 0, 0, 0);
+          ye = __builtin_amdgcn_mfma_f32_32x32x16_f16(adh, bh[c], ye, 0, 0, 0);
+          yo = __builtin_amdgcn_mfma_f32_32x32x16_f16(amh, bh[c], yo, 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(2);
+        const int c4 = lane & 7;
+        const int dbase = nt * 32 + 4 * c4, dmir = nt * 32 + 31 - 4 * c4;
+        const bool padlane = nt == 0 && c4 == 7 && ypad > 0;
+        int nd = 0, nm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          nd += dbase + q < Dh ? 1 : 0;
+          const int d = dmir - q;
+          nm += ((d >= 1 && 2 * d < D && d < Dh) || (padlane && d == 0)) ? 1 : 0;
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (half == 0)
+                v[q] = ye[4 * g + q] * inv;
+              else
+                v[3 - q] = yo[4 * g + q] * inv;
+            }
+            const int col = half == 0 ? 8 * g + 4 * hl : 28 - 8 * g - 4 * hl;
+            *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + col) = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int r = (lane >> 3) + 8 * k;
+            const int wr = 32 * tw_ + r;
+            if (wr >= W) continue;
+            f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 4 * c4);
+            float* yrr = yb + (int64_t)wr * a.sw;
+            if (half == 0) {
+              if (vec && nd == 4) {
+                *reinterpret_cast<f32x4*>(yrr + dbase) = v;
+                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], v[3])));
+                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+              } else if (nd > 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (q < nd) {
+                    yrr[dbase + q] = v[q];
+                    lo = fminf(lo, v[q]);
+                    hi = fmaxf(hi, v[q]);
+                  }
+              }
+            } else {
+              if (padlane) v[3] = 0.f;
+              if (vec && mal && nm == 4) {
+                *reinterpret_cast<f32x4*>(yrr + D - dmir) = v;
+                const float m3 = padlane ? v[2] : v[3];
+                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], m3)));
+                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], m3)));
+              } else if (nm > 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const int d = dmir - q;
+                  if (d >= 1 && 2 * d < D && d < Dh) {
+                    yrr[D - d] = v[q];
+                    lo = fminf(lo, v[q]);
+                    hi = fmaxf(hi, v[q]);
+                  } else if (padlane && d == 0) {
+                    yrr[D] = 0.f;
+                  }
+                }
+              }
+              if (padlane) {
+                int p = 1;
+                for (; p < ypad && ((D + p) & 3); ++p) yrr[D + p] = 0.f;
+                if (vec)
+                  for (; p + 4 <= ypad; p += 4) *reinterpret_cast<f32x4*>(yrr + D + p) = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (; p < ypad; ++p) yrr[D + p] = 0.f;
+              }
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      if (a.mm) {
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane == 0) a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
+      }
+    }
+    c0 = c1;
+  }
+}
+
 // per-sample keys of the slab partials: one workgroup per sample
 __global__ __launch_bounds__(256) void k_band_minmax(const float2* __restrict__ mmp, uint32_t* __restrict__ mm, int bc0,
                                                      int C, int H, int W) {
@@ -933,20 +1256,30 @@ __global__ __launch_bounds__(256) void k_copy_pad(CopyArgs a) {
 
 // Persistent grid: the workgroups that are resident at once (LDS and register occupancy, at most
 // 4 per CU), never more than there are units -- no second, partial round of workgroups.
+// Occupancy per (kernel, LDS bytes), computed once and cached under a lock (host threads may drive
+// one device each; the instantiations of one template share a function type, so the kernel's
+// address is part of the key).
+template <class K>
+int band_occupancy(K kern, size_t lds, int nt, int cap) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> cache;
+  const auto key = std::make_pair(reinterpret_cast<const void*>(kern), lds);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, nt, lds) != hipSuccess || occ < 1)
+    occ = (int)(163840 / (lds ? lds : 1));
+  occ = occ < 1 ? 1 : (occ > cap ? cap : occ);
+  if (std::getenv("TEXBIAS_BAND_VERBOSE"))
+    std::fprintf(stderr, "[texbias] band kernel %p: lds %zu B, %d workgroups/CU\n", key.first, lds, occ);
+  cache[key] = occ;
+  return occ;
+}
+
 template <class K>
 int band_grid(K kern, int units, size_t lds, int ncu) {
-  static size_t last_lds = ~(size_t)0;
-  static int last_occ = 1;
-  if (lds != last_lds) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BAND_NT, lds) != hipSuccess || occ < 1)
-      occ = (int)(163840 / (lds ? lds : 1));
-    last_occ = occ;
-    last_lds = lds;
-    if (std::getenv("TEXBIAS_BAND_VERBOSE"))
-      std::fprintf(stderr, "[texbias] band grid: lds %zu B, %d workgroups/CU, %d units\n", lds, occ, units);
-  }
-  const int per_cu = last_occ < 1 ? 1 : (last_occ > 4 ? 4 : last_occ);
+  const int per_cu = band_occupancy(kern, lds, BAND_NT, 4);
   const int g = ncu * per_cu;
   return units < g ? units : g;
 }
@@ -958,17 +1291,7 @@ hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
   if (e != hipSuccess) return e;
   // waves: as many as are resident at once (LDS / register occupancy), but at most T / ceil(nst / 2)
   // so that a slab spans at most BAND_FWD_SEGS waves, and (T + 1) G < 2^32 for the 32-bit split
-  static size_t last_lds = ~(size_t)0;
-  static int last_occ = 1;
-  if (lds != last_lds) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BAND_NT, lds) != hipSuccess || occ < 1)
-      occ = (int)(163840 / (lds ? lds : 1));
-    last_occ = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
-    last_lds = lds;
-    if (std::getenv("TEXBIAS_BAND_VERBOSE"))
-      std::fprintf(stderr, "[texbias] band fwd: lds %zu B, %d workgroups/CU\n", lds, occ);
-  }
+  const int last_occ = band_occupancy(kern, lds, BAND_NT, 8);
   const uint32_t nst = (uint32_t)((a.pl.W + BAND_FWD_ROWS - 1) / BAND_FWD_ROWS);
   const uint64_t T = (uint64_t)a.pl.H * (uint64_t)a.nbc * nst;
   uint64_t G = (uint64_t)ncu * (uint64_t)last_occ * 4;
@@ -979,6 +1302,16 @@ hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
   if (T >= (1ull << 31)) return hipErrorInvalidValue;
   a.split = FwdSplit{(uint32_t)T, (uint32_t)G, nst};
   hipLaunchKernelGGL(kern, dim3((unsigned)((G + 3) / 4)), dim3(BAND_NT), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int VT>
+hipError_t launch_inv16_t(const BandInvArgs& a, int ncu, hipStream_t st) {
+  const size_t lds = band_inv16_carve(a.g, a.pl.W).total;
+  auto kern = k_band_inv16<VT>;
+  hipError_t e = allow_lds(kern, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(band_grid(kern, a.pl.H * a.nbc, lds, ncu)), dim3(BAND_NT), lds, st, a);
   return hipGetLastError();
 }
 
@@ -1022,13 +1355,18 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4), dim3(BAND_NT), 0, st, a);
+  e = hipGetLastError();
+  if (e != hipSuccess || !a.g.cat) return e;
+  const int nth = (a.g.NCOL / 32) * band_nch(a.g) * 2 * 64;
+  hipLaunchKernelGGL(k_band_tab16, dim3((nth + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 
 
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
-  return 2 * a.g.KS <= 32 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
+  if (a.g.cat) return band_vt(a.g) == 1 ? launch_inv16_t<1>(a, ncu, st) : launch_inv16_t<2>(a, ncu, st);
+  return band_vt(a.g) == 1 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
 }
 
 hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st) {

@@ -456,6 +456,8 @@ size_t tb_workspace_bytes(const tb_plan* plan, int bc) {
   g.ncol = BAND_MAX_ZCOL;
   g.KS = 32;
   g.NCOL = 32 * ((plan->dev.D / 2 + 1 + 31) / 32);
+  g.cat = 0;  // 2 KS = 64 rows: the most either layout uses
+  g.PT = 0;
   const size_t band = band_ws(g, plan->dev.H, bc).total;
   const size_t gen = plan->generic ? gen_workspace_bytes(plan->dev.H, plan->dev.W, plan->dev.D, bc) : 0;
   const size_t m = spec > band ? spec : band;
@@ -502,6 +504,12 @@ static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, 
 // TEXBIAS_BAND=0 or tb_set_band_plans(0) forces the full-spectrum passes for every program.
 static bool g_band = [] {
   const char* e = std::getenv("TEXBIAS_BAND");
+  return !(e && e[0] == '0');
+}();
+// Pass C' synthesis in split f16 on the matrix cores (k_band_inv16) when the launch's V rows fit
+// (band columns + every sample's points <= 64); TEXBIAS_INV16=0 or tb_set_band_inv16(0): the f32 kernel.
+static bool g_inv16 = [] {
+  const char* e = std::getenv("TEXBIAS_INV16");
   return !(e && e[0] == '0');
 }();
 // measurement only: TEXBIAS_BAND_DIAG=0xIIFF skips stages of A' (FF) / C' (II); results invalid
@@ -605,13 +613,21 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   g.ncol = g.NW * g.NDk;
   g.KS = g.NDk + npt;
   g.NCOL = 32 * ((D / 2 + 1 + 31) / 32);
+  int ptot = 0;
+  for (int s = s0; s < s1; ++s) ptot += sp[s - s0].n;
+  g.cat = (g_inv16 && g.NDk + ptot <= 32) ? 1 : 0;
+  g.PT = g.cat ? ptot : 0;
   if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || KW >= 32 || KH > BAND_MAX_KH) return false;
   if (g.ncol > BAND_MAX_ZCOL || W > 1024) return false;
   if (2 * g.KS > 64 || g.KS > 32) return false;  // pass C' holds V in at most two 32-row MFMA tiles
   // worth it only when the box is a small part of the half spectrum
   if ((double)(2 * KH + 1) * g.ncol * 4.0 > (double)H * W * (D / 2 + 1)) return false;
+  if (g.cat && band_inv16_carve(g, W).total > 160000) {
+    g.cat = 0;
+    g.PT = 0;
+  }
   if (band_lds_fwd(g, W, D, false) > 160000 || band_lds_fwd(g, W, D, true) > 160000 ||
-      band_inv_carve(g, W, D).total > 160000)
+      (!g.cat && band_inv_carve(g, W, D).total > 160000))
     return false;
   if (band_ws(g, H, bcn).total > ws_bytes) return false;
   return true;
@@ -704,16 +720,21 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ma.nbc = nbc;
     ma.g = g;
     ma.split = split;
+    int p0 = 0;
     for (int i = 0; i < nb; ++i) {
       ma.sp[i] = sp[i];
       ma.ops.s[i] = ops[b0 + i];
+      ma.p0[i] = p0;
+      p0 += sp[i].n;
     }
+    ma.T16 = ws + wl.off_t16;
+    ma.tds = p->tds;
     TB_HIP(tb::launch_band_mid(ma, st));
   }
   {
     // the events bracket k_band_inv alone (the per-sample min/max reduction after it runs untimed),
     // so the pass time is that kernel's duration, as rocprofv3 reports it
-    Timer t(2, st, abytes + (double)nbc * H * W * (D + y_pad) * 4.0, "k_band_inv");
+    Timer t(2, st, abytes + (double)nbc * H * W * (D + y_pad) * 4.0, g.cat ? "k_band_inv16" : "k_band_inv");
     BandInvArgs ia;
     std::memset(&ia, 0, sizeof(ia));
     ia.pl = p->dev;
@@ -733,6 +754,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.mm = minmax;
     ia.mmp = reinterpret_cast<float2*>(ws + wl.off_mmp);
     ia.tds = p->tds;
+    ia.T16 = ws + wl.off_t16;
     ia.g = g;
     ia.diag = (g_band_diag >> 8) & 0xff;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
@@ -981,6 +1003,11 @@ int tb_set_compiled_plans(int enable) {
 
 int tb_set_band_plans(int enable) {
   g_band = enable != 0;
+  return TB_OK;
+}
+
+int tb_set_band_inv16(int enable) {
+  g_inv16 = enable != 0;
   return TB_OK;
 }
 

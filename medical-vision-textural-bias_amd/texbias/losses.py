@@ -8,11 +8,15 @@ MONAI's published one.  On HIP tensors the three per-instance sums come from one
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
 
 from ._lib import check, lib
+
+# TEXBIAS_DICE=0 (or ENABLED = False at run time) computes the sums with plain ATen reductions
+ENABLED = os.environ.get("TEXBIAS_DICE", "1") != "0"
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -60,7 +64,8 @@ class DiceLoss(nn.Module):
     def forward(self, input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         if input.shape != target.shape:
             raise AssertionError(f"ground truth has differing shape ({target.shape}) from input ({input.shape})")
-        if input.is_cuda and input.dtype == torch.float32 and target.dtype == torch.float32 and input.dim() > 2:
+        if ENABLED and input.is_cuda and input.dtype == torch.float32 and target.dtype == torch.float32 and \
+                input.dim() > 2:
             s = _DiceSums.apply(input, target, self.sigmoid, self.squared)
             if self.batch:
                 s = s.sum(0)

@@ -9,10 +9,14 @@ tensors only -- the library raises if it is missing; CPU tensors keep the plain 
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from ._lib import check, lib
+
+# TEXBIAS_NORM=0 (or ENABLED = False at run time) leaves ADN blocks on ATen's InstanceNorm3d + PReLU
+ENABLED = os.environ.get("TEXBIAS_NORM", "1") != "0"
 
 
 def _stream(t: torch.Tensor) -> int:

@@ -330,6 +330,12 @@ def set_band_plans(enable: bool) -> None:
     check(lib().tb_set_band_plans(1 if enable else 0))
 
 
+def set_band_inv16(enable: bool) -> None:
+    """Pass C' synthesis in split f16 on the matrix cores when True (default, where the launch's
+    V rows fit), else the f32 MFMA synthesis (tb_set_band_inv16)."""
+    check(lib().tb_set_band_inv16(1 if enable else 0))
+
+
 def set_chain_chunk(n: int) -> None:
     """Channel-volumes per pass A -> B -> C chain (tb_set_chain_chunk): n > 0 chunks, 0 = whole
     batch group per pass, n < 0 = default (Infinity-Cache-sized chunks)."""

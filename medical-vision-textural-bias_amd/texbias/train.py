@@ -106,13 +106,15 @@ def gibbs_gd(inputs: torch.Tensor, labels: torch.Tensor, model: torch.nn.Module,
     reference's ``.item()`` calls are left to the caller)."""
     if layer is None:
         layer = getattr(model, "module", model).gibbs
+    # alpha is updated IN PLACE: the Gibbs kernel reads it through its device address (ops.py
+    # _layer_apply), so a captured HIP graph keeps reading the live value after this update
     old = layer.alpha.clone()
     l0 = loss_fn(model(inputs), labels)
-    layer.alpha = old + h
+    layer.alpha.copy_(old + h)
     lh = loss_fn(model(inputs), labels)
     buf = torch.stack([(lh - l0) / h, l0]).to(torch.float32)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM)
         buf /= dist.get_world_size()
-    layer.alpha = old - learning_rate * buf[0].to(old.dtype)
-    return buf[1], layer.alpha
+    layer.alpha.copy_(old - learning_rate * buf[0].to(old.dtype))
+    return buf[1], layer.alpha.clone()

@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from .conv import Conv3d, ConvTranspose3d
+from . import norm as _norm
 from .norm import instnorm_prelu
 
 
@@ -40,7 +41,7 @@ class ADN(nn.Sequential):
 
     def forward(self, x):
         # On the GPU the N -> D(0) -> A chain is one fused texbias op (two HBM sweeps per direction).
-        if x.is_cuda and x.dtype == torch.float32 and (self.D.p == 0.0 or not self.training):
+        if _norm.ENABLED and x.is_cuda and x.dtype == torch.float32 and (self.D.p == 0.0 or not self.training):
             return instnorm_prelu(x, self.A.weight, self.N.eps)
         return super().forward(x)
 

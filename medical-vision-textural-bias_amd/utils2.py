@@ -9,8 +9,13 @@ device hashes (key, channel, frequency) into the uniform -- the same Bernoulli(1
 a different stream (parity hook: ``RandZF.last_seed``, replayed by ``oracle.filters_oracle``).
 
 ``FourierTransform`` and ``weights_init`` keep the reference's definitions (:6-31, :77-83);
-the former is plain torch.fft (differentiable, used by the frequency-consistency loss of
-reconGan_freq.py:131-142).
+the former is plain torch.fft (differentiable).
+
+``freq_consistency_loss`` is the frequency-consistency term of reconGan_freq.py:131-142,
+``MSE(Re F r, Re F f) + MSE(Im F r, Im F f)`` with F the unnormalised ``fftn`` over the last two
+axes, in closed form: by Parseval, ``sum |F(r - f)|^2 = H W sum |r - f|^2``, so the term equals
+``H * W * MSE(r, f)`` exactly -- one fused reduction over the images instead of two forward FFTs
+(and two more in the backward pass).
 """
 from __future__ import annotations
 
@@ -23,7 +28,7 @@ from filters_and_operators import _kspace
 from texbias import kprog as _K
 from texbias.transform_base import Transform
 
-__all__ = ["FourierTransform", "RandZF", "weights_init"]
+__all__ = ["FourierTransform", "RandZF", "freq_consistency_loss", "FreqConsistencyLoss", "weights_init"]
 
 
 class FourierTransform:
@@ -55,6 +60,24 @@ class RandZF(Transform, FourierTransform):
         self.last_seed = seed
         geo = _K.geometry(tuple(img.shape[1:]))
         return _kspace(img, n_dims, [_K.zf_op(self.p, seed, geo.hwd)])
+
+
+def freq_consistency_loss(real: torch.Tensor, fake: torch.Tensor) -> torch.Tensor:
+    """``l2(Re fftn(real), Re fftn(fake)) + l2(Im .., Im ..)`` over dims (-2, -1) with
+    ``l2 = nn.MSELoss()`` (reconGan_freq.py:60, :131-142), as ``H W MSE(real, fake)`` (Parseval)."""
+    if real.shape != fake.shape:
+        raise ValueError(f"shape mismatch {tuple(real.shape)} vs {tuple(fake.shape)}")
+    if real.dim() < 2:
+        raise ValueError("need at least two (transformed) axes")
+    hw = real.shape[-2] * real.shape[-1]
+    return hw * nn.functional.mse_loss(fake, real)
+
+
+class FreqConsistencyLoss(nn.Module):
+    """Module form of :func:`freq_consistency_loss` (``forward(real, fake)``)."""
+
+    def forward(self, real: torch.Tensor, fake: torch.Tensor) -> torch.Tensor:
+        return freq_consistency_loss(real, fake)
 
 
 def weights_init(m):

@@ -63,7 +63,7 @@ def test_band_disk_spike_wrap_matches_full(rt, shape):
     idx = tuple(int(n * 0.8) for n in sp)
     progs = [[K.disk_op(r, False), spike(idx, sp, 10.0, phase=0.3 + b), K.wrap_op(0.5)] for b in range(shape[0])]
     yb, yf, names, mmb, mmf = both(rt, x, progs, shape[1], pad=5)
-    assert names[0] == "k_band_fwd" and names[2] == "k_band_inv"
+    assert names[0] == "k_band_fwd" and names[2] == "k_band_inv16"
     assert torch.all(yb[..., sp[-1]:] == 0)
     assert (yb - yf).abs().max().item() / yf.abs().max().item() < 2e-6
     vb = yb[..., : sp[-1]].reshape(shape[0], -1)
@@ -189,7 +189,63 @@ def test_band_c3_kernels_and_bytes(rt):
     rt.kspace_filter(x, 3, [prog, prog], 4, pad=5)
     ms, cnt, nbytes, names = rt.pass_stats()
     rt.set_pass_timing(False)
-    assert names[:3] == ["k_band_fwd", "k_band_mid", "k_band_inv"]
+    assert names[:3] == ["k_band_fwd", "k_band_mid", "k_band_inv16"]
     img = 8 * 240 * 240 * 155 * 4
     assert img < nbytes[0] < 1.05 * img
     assert 8 * 240 * 240 * 160 * 4 < nbytes[2] < 1.05 * 8 * 240 * 240 * 160 * 4
+
+
+def _inv_both(rt, x, progs, C, pad=0):
+    """(split-f16 C', f32 C', kernel names of each)"""
+    out = []
+    for on in (True, False):
+        rt.set_band_inv16(on)
+        try:
+            rt.set_pass_timing(True)
+            y = rt.kspace_filter(x, 3, progs, C, pad=pad)
+            torch.cuda.synchronize()
+            names = rt.pass_stats()[3]
+            rt.set_pass_timing(False)
+        finally:
+            rt.set_band_inv16(True)
+        out += [y, names[2]]
+    return out
+
+
+@pytest.mark.parametrize("shape,r,npts", [((2, 4, 240, 240, 155), 12.5, 1), ((2, 4, 240, 240, 155), 25.1, 1),
+                                          ((4, 4, 128, 128, 128), 12.5, 0), ((3, 2, 40, 36, 33), 7.0, 3),
+                                          ((2, 3, 40, 40, 30), 9.0, 2)])
+def test_band_inv16_matches_f32(rt, shape, r, npts):
+    """Pass C' in split f16 (k_band_inv16) against the f32 MFMA synthesis (k_band_inv) on the same
+    band spectrum: max|d| / max|y| <= 1e-6; both routes' kernels identified."""
+    torch.manual_seed(7)
+    x = torch.randn(shape, device="cuda") * 3.0 + 1.5
+    sp = shape[2:]
+    progs = []
+    for b in range(shape[0]):
+        prog = [K.disk_op(r, False)]
+        for j in range(npts):
+            idx = tuple(int(n * (0.8 - 0.1 * j)) - b for n in sp)
+            prog.append(spike(idx, sp, 9.0 + j, phase=0.3 * b + j))
+        prog.append(K.wrap_op(0.5))
+        progs.append(prog)
+    y16, n16, y32, n32 = _inv_both(rt, x, progs, shape[1], pad=5)
+    assert n16 == "k_band_inv16" and n32 == "k_band_inv", (n16, n32)
+    assert torch.all(y16[..., sp[-1]:] == 0)
+    assert (y16 - y32).abs().max().item() / y32.abs().max().item() < 1e-6
+
+
+def test_band_inv16_falls_back_past_32_rows(rt):
+    """More band columns + launch points than the split-f16 kernel's 64 V rows: the f32 kernel runs."""
+    torch.manual_seed(8)
+    shape = (8, 1, 96, 96, 80)
+    sp = shape[2:]
+    x = torch.randn(shape, device="cuda")
+    progs = [[K.disk_op(20.0, False)] + [spike((40 + j, 30 - b, 50 - j), sp, 8.0) for j in range(3)]
+             for b in range(shape[0])]
+    rt.set_pass_timing(True)
+    rt.kspace_filter(x, 3, progs, 1)
+    torch.cuda.synchronize()
+    names = rt.pass_stats()[3]
+    rt.set_pass_timing(False)
+    assert names[2] == "k_band_inv", names

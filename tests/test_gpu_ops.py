@@ -113,3 +113,34 @@ def test_graph_capture_chain_and_train_step(ops):
         losses.append(loss_static.item())
     torch.testing.assert_close(y_static, y_ref, rtol=0, atol=0)
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+
+
+def test_graph_capture_gibbs_unet_survives_gibbs_gd(ops):
+    """A captured Gibbs_UNet forward keeps reading the layer's live alpha: gibbs_gd updates the
+    buffer in place (its device address never changes), so a replay after the update equals an
+    eager forward at the new alpha, bit for bit."""
+    import stylization_layers as SL
+    from texbias.losses import DiceLoss
+    from texbias.train import gibbs_gd
+    torch.manual_seed(3)
+    net = SL.Gibbs_UNet().cuda().eval()
+    x = torch.randn((2, 1, 32, 32, 16), device="cuda")
+    lab = (torch.rand((2, 1, 32, 32, 16), device="cuda") > 0.7).float()
+    ptr0 = net.gibbs.alpha.data_ptr()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.no_grad():
+        for _ in range(2):
+            net(x)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        y_static = net(x)
+    a0 = net.gibbs.alpha.clone()
+    _, a1 = gibbs_gd(x, lab, net, DiceLoss(sigmoid=True, squared_pred=True), h=0.1, learning_rate=1.0)
+    assert net.gibbs.alpha.data_ptr() == ptr0
+    assert not torch.equal(a0, a1)
+    g.replay()
+    with torch.no_grad():
+        y_eager = net(x)
+    torch.testing.assert_close(y_static, y_eager, rtol=0, atol=0)

@@ -195,3 +195,41 @@ def test_train_step_full_volume_finite_and_fast_paths(gpu):
     assert all(torch.isfinite(p).all().item() for p in model.parameters())
     # the full- and half-resolution layers (the expensive ones) are all on the texbias kernels
     assert sum(fast) >= 10, fast
+
+
+def test_train_step_full_volume_matches_aten(gpu):
+    """The whole bench-shaped step (U-Net 4->3 on 2 x 4 x 240 x 240 x 160, DiceLoss(sigmoid,
+    squared_pred), backward) through the texbias kernels against the same weights and batch with
+    every texbias path switched off (MIOpen/ATen convolutions and gradients, ATen InstanceNorm3d +
+    PReLU, ATen Dice reductions).  Both are float32; the bar is normwise per parameter gradient
+    (max|g - g_aten| / max|g_aten| <= 2e-3) and 1e-5 absolute on the loss."""
+    import copy
+
+    from texbias import conv as C
+    from texbias import losses as L
+    from texbias import norm as N
+    from texbias.train import reference_model
+    torch.manual_seed(6)
+    model = reference_model(4, 3).cuda()
+    aten = copy.deepcopy(model)
+    x = torch.randn((2, 4, 240, 240, 160), device="cuda")
+    lab = (torch.rand((2, 3, 240, 240, 160), device="cuda") > 0.85).float()
+    loss_fn = L.DiceLoss(sigmoid=True, squared_pred=True)
+    l_tb = loss_fn(model(x), lab)
+    l_tb.backward()
+    saved = (C.ENABLED, N.ENABLED, L.ENABLED)
+    try:
+        C.ENABLED = N.ENABLED = L.ENABLED = False
+        l_at = loss_fn(aten(x), lab)
+        l_at.backward()
+    finally:
+        C.ENABLED, N.ENABLED, L.ENABLED = saved
+    errs = {}
+    for (n, p), (n2, q) in zip(model.named_parameters(), aten.named_parameters()):
+        assert n == n2 and p.grad is not None and q.grad is not None, n
+        errs[n] = relmax(p.grad, q.grad.double())
+    worst = max(errs, key=errs.get)
+    print(f"loss texbias {l_tb.item():.8f} aten {l_at.item():.8f}; worst grad {worst} {errs[worst]:.3e}; "
+          f"median {sorted(errs.values())[len(errs) // 2]:.3e} over {len(errs)} tensors")
+    assert abs(l_tb.item() - l_at.item()) < 1e-5
+    assert errs[worst] < 2e-3, errs

@@ -46,3 +46,27 @@ def test_zf_inside_band_program(gpu):
     keep = O.zf_keep_mask(xs.shape, 0.4, 77)
     ref = O.wrap_artifact(O.rand_zf(O.fourier_disk(xs, 9.0), keep), 0.5)
     assert relerr(yb[1].cpu().numpy(), ref) < 1e-5
+
+
+def _freq_loss_fft(real, fake):
+    """reconGan_freq.py:131-142 as written: MSE of the real and imaginary parts of fftn(dim=(-2, -1))."""
+    l2 = torch.nn.MSELoss()
+    rk = torch.fft.fftn(real, dim=(-2, -1))
+    fk = torch.fft.fftn(fake, dim=(-2, -1))
+    return l2(rk.real, fk.real) + l2(rk.imag, fk.imag)
+
+
+@pytest.mark.parametrize("shape", [(4, 2, 128, 128), (3, 1, 33, 17)])
+def test_freq_consistency_closed_form_gpu(gpu, shape):
+    """The Parseval closed form equals the reference's FFT formulation (value and gradient, 1e-5)."""
+    import utils2
+    torch.manual_seed(1)
+    real = torch.randn(shape, device="cuda")
+    fake = (real + 0.3 * torch.randn(shape, device="cuda")).requires_grad_(True)
+    v = utils2.freq_consistency_loss(real, fake)
+    g, = torch.autograd.grad(v, fake)
+    f2 = fake.detach().clone().requires_grad_(True)
+    r = _freq_loss_fft(real, f2)
+    gr, = torch.autograd.grad(r, f2)
+    assert abs(v.item() - r.item()) <= 1e-5 * abs(r.item())
+    assert (g - gr).abs().max().item() <= 1e-5 * gr.abs().max().item()
