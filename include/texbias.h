@@ -223,6 +223,12 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
  *             (when `normalize`)                                   NormalizeIntensityd(nonzero, channel_wise)
  *   scale     x * scale  (scale = 1 + factor, or 1)                RandScaleIntensityd
  *   shift     x + shift on every voxel (or 0)                      RandShiftIntensityd
+ * With `resample` = 1 the spatial part is instead one affine gather map per sample, built on the host
+ * from Spacingd(pixdim, mode=("bilinear", "nearest")) -> Orientationd(axcodes) -> the crop ->
+ * the flips (MONAI 0.5 semantics; …3modalities.py:156-161, val CenterSpatialCropd :186): output
+ * voxel (i, j, k) samples the input at c = m[0..2] . (i, j, k) + m[3] (row a of the 3 x 4 map m
+ * gives coordinate a), the image trilinearly and the label at the nearest voxel (round half to
+ * even), both with border clamping (grid_sample padding_mode "border"); h0/w0/d0/flip are unused.
  * out [B][C][h][w][d]; out_lab [B][3][h][w][d] = (TC: 2|3, WT: 1|2|3, ET: 2) as 0/1 floats --
  * ConvertToMultiChannelBasedOnBratsClassesd, source_code/filters_and_operators.py:61-87.
  * Driver call site: 10_scripts/127_gibbs_spikes_wraparound_sap_OneChannel/
@@ -234,7 +240,8 @@ typedef struct tb_prep_params {
   float scale;    /* 1 + factor, or 1 */
   float shift;    /* offset, or 0 */
   int normalize;  /* 1: NormalizeIntensity(nonzero=True, channel_wise=True) */
-  int reserved;
+  int resample;   /* 1: spatial map m instead of crop + flip */
+  float m[12];    /* resample: input coordinate a = m[4a] i + m[4a + 1] j + m[4a + 2] k + m[4a + 3] */
 } tb_prep_params;
 size_t tb_brats_prep_workspace_bytes(int B, int C);
 int tb_brats_prep_f32(const float* img, const float* lab, int B, int C, int H0, int W0, int D0,

@@ -38,7 +38,7 @@ constexpr int BAND_MAX_PTS = 8;    // out-of-box half-spectrum spike points per 
 constexpr int BAND_ROWS_A = 64;    // image rows per pass-A' chunk (one per lane)
 constexpr int BAND_MAX_NDK = 32;
 constexpr int BAND_MAX_KH = 31;    // box half-height
-constexpr int BAND_MAX_ZCOL = 1024; // box columns (kw, kd) per slab held in pass B2''s LDS
+constexpr int BAND_MAX_ZCOL = 1536; // box columns (kw, kd) per slab in pass B2''s LDS (r = 25.1 at 240^2 x 155: 1,326)
 
 struct BandPt {
   int16_t kh, kw, kd, pad;  // unsigned frequency of the stored (kd <= D/2) coefficient
@@ -55,6 +55,7 @@ struct BandGeo {
   int NCOL;         // folded output columns of the MFMA n-tiles: 32 * ceil((D/2 + 1) / 32)
   int cat;          // 1: split-f16 pass C' (k_band_inv16) -- every sample's points get their own V rows
   int PT;           // cat: points of the whole launch (rows 2 (NDk + p0[s] + j) hold sample s's point j)
+  int NTD;          // cat: 32-column tiles of a stored output row, ceil((D + pad) / 32)
 };
 // rows of V (2 per kd band column / point) and its 32-row MFMA tiles
 TB_HD int band_rows(const BandGeo& g) { return 2 * (g.cat ? g.NDk + g.PT : g.KS); }
@@ -168,14 +169,14 @@ TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
   return c;
 }
 
-// Split-f16 pass C' (k_band_inv16): the synthesis table as MFMA A fragments
-// [ntn][nch][dir/mirror][hi/lo][64 lanes][8 halves] (ntn = NCOL / 32 column tiles, nch = 16-row
-// chunks of V), then the W twiddles, BAND_SLOTS16 slabs' V-product fragments, point kw, staging.
-constexpr int BAND_SLOTS16 = 2;
+// Split-f16 pass C' (k_band_inv16): the unfolded synthesis table as MFMA B fragments
+// [NTD][nch][hi/lo][64 lanes][8 halves] (NTD 32-column tiles of the stored row, nch 16-row chunks
+// of V), then the W twiddles, BAND_SLOTS16 slabs' V-product fragments, the slabs' point kw.
+constexpr int BAND_SLOTS16 = 3;
 TB_HD int band_nch(const BandGeo& g) { return (band_rows(g) + 15) / 16; }
-TB_HD int band_t16_bytes(const BandGeo& g) { return (g.NCOL / 32) * band_nch(g) * 4 * 64 * 16; }
+TB_HD int band_t16_bytes(const BandGeo& g) { return g.NTD * band_nch(g) * 2 * 64 * 16; }
 struct BandInv16Carve {
-  int tab, tww, frag, pkw, stg, total;
+  int tab, tww, frag, pkw, total;
 };
 TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W) {
   BandInv16Carve c;
@@ -183,8 +184,7 @@ TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W) {
   c.tww = band_al16(band_t16_bytes(g));
   c.frag = band_al16(c.tww + W * 8);
   c.pkw = band_al16(c.frag + BAND_SLOTS16 * band_vt(g) * band_kv(g) * 64 * 4);
-  c.stg = band_al16(c.pkw + BAND_SLOTS16 * BAND_MAX_PTS * 4);
-  c.total = band_al16(c.stg + 4 * 32 * BAND_STG_P * 4);
+  c.total = band_al16(c.pkw + BAND_SLOTS16 * BAND_MAX_PTS * 4);
   return c;
 }
 

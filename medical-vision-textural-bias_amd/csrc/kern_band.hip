@@ -855,12 +855,16 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
 }
 
 // ----------------------------------------------------------------------------- pass C' (split f16)
-// The C2R synthesis y = T . V in split precision on the f16 matrix cores (16x the f32 MFMA rate):
-// T = Th + Tl (the constant cos/sin table, scaled by 2^8), V = Vh + Vl (the V-product accumulators,
-// scaled by a power of two per unit so that max |V| < 2^15), y = (Th Vh + Th Vl + Tl Vh) / scale.
-// Each f16 pair carries 22 bits of the value and the dropped Tl Vl term is 2^-22 relative, so the
-// result matches the f32 synthesis to a few 1e-7 of max |y|.  Both halves of the folded C2R come
-// straight out of the MFMA (dir: cos, -sin; mirror: cos, +sin) instead of E -/+ O on the VALU.
+// The C2R synthesis in split precision on the f16 matrix cores (16x the f32 MFMA rate), unfolded:
+//   Y^T(w, d) = sum_v V^T(w, v) T(v, d),   T(2 kd, d) = cos(2 pi kd d / D), T(2 kd + 1, d) = -sin(..)
+// for every output column d < D + pad (T = 0 past D: the U-Net's zero padding comes out of the
+// MFMA).  V^T is the V-product accumulator tile used as the A operand as it stands (its rows are
+// the k index); T is the launch's fragment image (k_band_tab16) in LDS.  Split precision:
+// V = Vh + Vl (scaled by a power of two per unit so that max |V| < 2^15), T = Th + Tl (scaled by
+// 2^8), Y = (Vh Th + Vh Tl + Vl Th) / scale -- 22 bits per operand, the dropped Vl Tl term
+// 2^-22 relative, so Y matches the f32 synthesis to a few 1e-7 of max |y|.  The accumulator has
+// the image row w in its registers and the column d on the lane, so each register is stored
+// straight to HBM as two whole 128-B row segments: no LDS staging, no mirror stores.
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 constexpr float BAND_T16_SCALE = 256.f;
 
@@ -869,17 +873,20 @@ __device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
   l = (_Float16)(x - (float)h);
 }
 
-// One thread per (column tile, 16-row chunk, dir/mirror, lane): the lane's 8 A-fragment entries,
-// k-permuted to match the accumulator-as-B-operand order of the V tile (element j of lane half h is
-// V row 16 c + 8 (j >> 2) + 4 h + (j & 3)); rows 2 kd + (re, im), band columns first, then every
+// One thread per (column tile, 16-row chunk, lane): the lane's 8 B-fragment entries of T, k-permuted
+// to match the accumulator-as-A-operand order of V^T (element j of lane half h is V row
+// 16 c + 8 (j >> 2) + 4 h + (j & 3)); rows 2 kd + (re, im), the band columns first, then every
 // sample's out-of-box points in launch order.
 __global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
   const BandMidArgs& a = kargs<BandMidArgs>();
-  const int nch = band_nch(a.g), ntn = a.g.NCOL / 32, NCOL = a.g.NCOL, NDk = a.g.NDk;
+  const int nch = band_nch(a.g), ntd = a.g.NTD, NCOL = a.g.NCOL, NDk = a.g.NDk, D = a.pl.D, Dh = D / 2 + 1;
   const int t = (int)(blockIdx.x * 256 + threadIdx.x);
-  if (t >= ntn * nch * 2 * 64) return;
-  const int lane = t & 63, dm = (t >> 6) & 1, cc = t >> 7, c = cc % nch, nt = cc / nch;
+  if (t >= ntd * nch * 64) return;
+  const int lane = t & 63, cc = t >> 6, c = cc % nch, nt = cc / nch;
   const int d = 32 * nt + (lane & 31), hl = lane >> 5;
+  // column d of the unfolded table from the folded one: d > D/2 mirrors to D - d (sin changes sign)
+  const bool in = d < D, mir = d >= Dh;
+  const int dd = mir ? D - d : d;
   h16x8 fh, fl;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -889,14 +896,14 @@ __global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
     if (pr < NDk) {
       kd = pr;
     } else {
-      int gp = pr - NDk;
+      const int gp = pr - NDk;
       for (int s = 0; s < TB_MAX_BATCH && kd < 0; ++s)
         if (gp >= a.p0[s] && gp < a.p0[s] + a.sp[s].n) kd = a.sp[s].p[gp - a.p0[s]].kd;
     }
     float tv = 0.f;
-    if (kd >= 0) {
-      tv = a.tds[(2 * kd + im) * NCOL + d];  // zero past d = D/2
-      if (im && !dm) tv = -tv;               // dir: cos, -sin; mirror: cos, +sin
+    if (kd >= 0 && in) {
+      tv = a.tds[(2 * kd + im) * NCOL + dd];
+      if (im && !mir) tv = -tv;  // -sin(2 pi kd d / D) = +sin(2 pi kd (D - d) / D)
     }
     _Float16 h, l;
     split_f16(tv * BAND_T16_SCALE, h, l);
@@ -904,33 +911,31 @@ __global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
     fl[j] = l;
   }
   h16x8* T = reinterpret_cast<h16x8*>(a.T16);
-  const int base = ((cc * 2 + dm) * 2) * 64 + lane;
-  T[base] = fh;
-  T[base + 64] = fl;
+  T[(cc * 2) * 64 + lane] = fh;
+  T[(cc * 2 + 1) * 64 + lane] = fl;
 }
 
 template <int VT>  // 32-row tiles of V
-__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4))) void k_band_inv16(BandInvArgs) {
-  // Same unit structure as k_band_inv (V product on f32 MFMA from LDS-resident fragments, LDS-staged
-  // 128-B row-segment stores, per-unit min/max partials); the synthesis table is the launch's
-  // split-f16 fragment image (k_band_tab16), copied to LDS once per workgroup.
+__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5))) void k_band_inv16(BandInvArgs) {
+  // Same unit structure as k_band_inv: (slab, 32-row tile) units dealt to a persistent grid, each
+  // workgroup's slabs in batches whose V-product fragments are loaded to LDS first (the unit loop
+  // then issues no vector-memory loads), per-unit min/max partials.
   const BandInvArgs& a = kargs<BandInvArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63, hl = lane >> 5, l31 = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
-  const int KW = a.g.KW, NCOL = a.g.NCOL;
+  const int KW = a.g.KW;
   const int npm = a.g.KS - a.g.NDk;    // point k-steps of the V product (max points per sample)
   const int KV = KW + 1 + npm;
-  const int Dh = D / 2 + 1;
   const int nch = band_nch(a.g);       // 16-row chunks of V in use
+  const int ntd = a.g.NTD;             // 32-column tiles of the output row (D + pad)
   const int fsz = VT * KV * 64;
   const BandInv16Carve cv = band_inv16_carve(a.g, W);
-  const h16x8* Tab = reinterpret_cast<const h16x8*>(smem + cv.tab);  // [nt][c][dm][part][64]
+  const h16x8* Tab = reinterpret_cast<const h16x8*>(smem + cv.tab);  // [nt][c][hi/lo][64]
   float2* twW = reinterpret_cast<float2*>(smem + cv.tww);
   float* Fs = reinterpret_cast<float*>(smem + cv.frag);
   int* Pkw = reinterpret_cast<int*>(smem + cv.pkw);
-  float* stg = reinterpret_cast<float*>(smem + cv.stg) + wv * 32 * BAND_STG_P;
   const int ntab4 = band_t16_bytes(a.g) / 16;
   const bool twv = !(W & 1) && (reinterpret_cast<uintptr_t>(a.pl.tw[1]) & 15) == 0;
   const int ntw4 = twv ? W / 2 : 0;
@@ -940,9 +945,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4)))
   int tb4 = ntab4 + ntw4;
   const int ntw = (W + 31) / 32;
   const int nslab = H * a.nbc;
-  const int ntn = NCOL / 32;
-  const int ypad = a.ypad;
-  const bool mal = ((D - 3) & 3) == 0;
+  const int ncolo = D + a.ypad;        // stored columns of a row
   const int nunit = nslab * ntw;
   const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
   const int ub = (int)blockIdx.x * per, ue = ub + per < nunit ? ub + per : nunit;
@@ -1001,7 +1004,6 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4)))
       for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
         for (int j = 0; j < 16; ++j) vacc[vt][j] = 0.f;
-      __builtin_amdgcn_s_setprio(0);
       int t = 0;
       int ks = 0;
       for (; ks + 4 <= KW + 1; ks += 4) {
@@ -1038,7 +1040,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4)))
         for (int vt = 0; vt < VT; ++vt)
           vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(F[(vt * KV + KW + 1 + j) * 64], b, vacc[vt], 0, 0, 0);
       }
-      // V as split-f16 B operands: chunk c = 2 vt + q is registers 8 q .. 8 q + 7 of vacc[vt]
+      // V^T as split-f16 A operands: chunk c = 2 vt + q is registers 8 q .. 8 q + 7 of vacc[vt]
       float m = 0.f;
 #pragma unroll
       for (int vt = 0; vt < VT; ++vt)
@@ -1046,9 +1048,9 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4)))
         for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(vacc[vt][j]));
       m = wave_max(m);
       int ex;
-      (void)frexpf(m, &ex);          // m < 2^ex
+      (void)frexpf(m, &ex);  // m < 2^ex
       const float sv = ldexpf(1.f, 15 - ex), inv = ldexpf(1.f, ex - 15) * (1.f / BAND_T16_SCALE);
-      h16x8 bh[2 * VT], bl[2 * VT];
+      h16x8 ah[2 * VT], al[2 * VT];
 #pragma unroll
       for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
@@ -1057,107 +1059,41 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 4)))
           for (int j = 0; j < 8; ++j) {
             _Float16 hh, ll;
             split_f16(vacc[vt][8 * q + j] * sv, hh, ll);
-            bh[2 * vt + q][j] = hh;
-            bl[2 * vt + q][j] = ll;
+            ah[2 * vt + q][j] = hh;
+            al[2 * vt + q][j] = ll;
           }
       float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
-      const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
       float lo = 3.402823466e38f, hi = -3.402823466e38f;
-      for (int nt = 0; nt < ntn; ++nt) {
-        __builtin_amdgcn_s_setprio(0);
-        f32x16 ye, yo;  // ye: y[d] (dir), yo: y[D - d] (mirror), d = 32 nt + row
+      const int wb = 32 * tw_ + 4 * hl;  // image row of accumulator register r: wb + acc_row(r)
+      for (int nt = 0; nt < ntd; ++nt) {
+        f32x16 acc;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) ye[j] = yo[j] = 0.f;
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
 #pragma unroll
         for (int c = 0; c < 2 * VT; ++c) {
           if (c >= nch) break;
-          const h16x8* tp = Tab + ((nt * nch + c) * 4) * 64 + lane;
-          const h16x8 adh = tp[0], adl = tp[64], amh = tp[128], aml = tp[192];
-          ye = __builtin_amdgcn_mfma_f32_32x32x16_f16(adl, bh[c], ye, 0, 0, 0);
-          yo = __builtin_amdgcn_mfma_f32_32x32x16_f16(aml, bh[c], yo, 0, 0, 0);
-          ye = __builtin_amdgcn_mfma_f32_32x32x16_f16(adh, bl[c], ye, 0, 0, 0);
-          yo = __builtin_amdgcn_mfma_f32_32x32x16_f16(amh, bl[c], yo, 0, 0, 0);
-          ye = __builtin_amdgcn_mfma_f32_32x32x16_f16(adh, bh[c], ye, 0, 0, 0);
-          yo = __builtin_amdgcn_mfma_f32_32x32x16_f16(amh, bh[c], yo, 0, 0, 0);
+          const h16x8* tp = Tab + ((nt * nch + c) * 2) * 64 + lane;
+          const h16x8 th = tp[0], tl = tp[64];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], th, acc, 0, 0, 0);
         }
-        __builtin_amdgcn_s_setprio(2);
-        const int c4 = lane & 7;
-        const int dbase = nt * 32 + 4 * c4, dmir = nt * 32 + 31 - 4 * c4;
-        const bool padlane = nt == 0 && c4 == 7 && ypad > 0;
-        int nd = 0, nm = 0;
+        const int col = 32 * nt + l31;
+        if (col < ncolo) {
+          float* yc = yb + col;
+          const bool img = col < D;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          nd += dbase + q < Dh ? 1 : 0;
-          const int d = dmir - q;
-          nm += ((d >= 1 && 2 * d < D && d < Dh) || (padlane && d == 0)) ? 1 : 0;
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 v;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (half == 0)
-                v[q] = ye[4 * g + q] * inv;
-              else
-                v[3 - q] = yo[4 * g + q] * inv;
-            }
-            const int col = half == 0 ? 8 * g + 4 * hl : 28 - 8 * g - 4 * hl;
-            *reinterpret_cast<f32x4*>(stg + l31 * BAND_STG_P + col) = v;
-          }
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int r = (lane >> 3) + 8 * k;
-            const int wr = 32 * tw_ + r;
-            if (wr >= W) continue;
-            f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * BAND_STG_P + 4 * c4);
-            float* yrr = yb + (int64_t)wr * a.sw;
-            if (half == 0) {
-              if (vec && nd == 4) {
-                *reinterpret_cast<f32x4*>(yrr + dbase) = v;
-                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], v[3])));
-                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-              } else if (nd > 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                  if (q < nd) {
-                    yrr[dbase + q] = v[q];
-                    lo = fminf(lo, v[q]);
-                    hi = fmaxf(hi, v[q]);
-                  }
-              }
-            } else {
-              if (padlane) v[3] = 0.f;
-              if (vec && mal && nm == 4) {
-                *reinterpret_cast<f32x4*>(yrr + D - dmir) = v;
-                const float m3 = padlane ? v[2] : v[3];
-                lo = fminf(lo, fminf(fminf(v[0], v[1]), fminf(v[2], m3)));
-                hi = fmaxf(hi, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], m3)));
-              } else if (nm > 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  const int d = dmir - q;
-                  if (d >= 1 && 2 * d < D && d < Dh) {
-                    yrr[D - d] = v[q];
-                    lo = fminf(lo, v[q]);
-                    hi = fmaxf(hi, v[q]);
-                  } else if (padlane && d == 0) {
-                    yrr[D] = 0.f;
-                  }
-                }
-              }
-              if (padlane) {
-                int p = 1;
-                for (; p < ypad && ((D + p) & 3); ++p) yrr[D + p] = 0.f;
-                if (vec)
-                  for (; p + 4 <= ypad; p += 4) *reinterpret_cast<f32x4*>(yrr + D + p) = f32x4{0.f, 0.f, 0.f, 0.f};
-                for (; p < ypad; ++p) yrr[D + p] = 0.f;
+          for (int r = 0; r < 16; ++r) {
+            const int wr = wb + acc_row(r);
+            if (wr < W) {
+              const float v = acc[r] * inv;  // exactly 0 in the pad columns (T = 0 there)
+              yc[(int64_t)wr * a.sw] = v;
+              if (img) {
+                lo = fminf(lo, v);
+                hi = fmaxf(hi, v);
               }
             }
           }
-          __builtin_amdgcn_wave_barrier();
         }
       }
       if (a.mm) {
@@ -1357,7 +1293,7 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4), dim3(BAND_NT), 0, st, a);
   e = hipGetLastError();
   if (e != hipSuccess || !a.g.cat) return e;
-  const int nth = (a.g.NCOL / 32) * band_nch(a.g) * 2 * 64;
+  const int nth = a.g.NTD * band_nch(a.g) * 64;
   hipLaunchKernelGGL(k_band_tab16, dim3((nth + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }

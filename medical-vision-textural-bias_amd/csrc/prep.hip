@@ -16,6 +16,7 @@
 // the crop window read twice (stats, apply) + the output written once.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 
 #include "texbias.h"
@@ -46,6 +47,48 @@ __device__ __forceinline__ const float* row_src(const PrepArgs& a, const tb_prep
   return base + ((int64_t)(q.h0 + si) * a.W0 + (q.w0 + sj)) * a.D0 + q.d0;
 }
 
+// Resample mode: the input coordinate of output voxel (i, j, k) under the sample's 3 x 4 map.
+struct Coord3 {
+  float x, y, z;
+};
+__device__ __forceinline__ Coord3 map_row(const tb_prep_params& q, int i, int j) {
+  return Coord3{fmaf(q.m[0], (float)i, fmaf(q.m[1], (float)j, q.m[3])),
+                fmaf(q.m[4], (float)i, fmaf(q.m[5], (float)j, q.m[7])),
+                fmaf(q.m[8], (float)i, fmaf(q.m[9], (float)j, q.m[11]))};
+}
+__device__ __forceinline__ Coord3 map_at(const tb_prep_params& q, const Coord3& r, int k) {
+  return Coord3{fmaf(q.m[2], (float)k, r.x), fmaf(q.m[6], (float)k, r.y), fmaf(q.m[10], (float)k, r.z)};
+}
+// one axis of the border-clamped trilinear stencil: (i0, i1, weight of i1)
+__device__ __forceinline__ void axis_lin(float c, int n, int& i0, int& i1, float& f) {
+  c = fminf(fmaxf(c, 0.f), (float)(n - 1));
+  const float fl = floorf(c);
+  i0 = (int)fl;
+  i1 = i0 + 1 < n ? i0 + 1 : n - 1;
+  f = c - fl;
+}
+__device__ __forceinline__ float trilinear(const float* v, const PrepArgs& a, const Coord3& c) {
+  int x0, x1, y0, y1, z0, z1;
+  float fx, fy, fz;
+  axis_lin(c.x, a.H0, x0, x1, fx);
+  axis_lin(c.y, a.W0, y0, y1, fy);
+  axis_lin(c.z, a.D0, z0, z1, fz);
+  auto at = [&](int x, int y, int z) { return v[((int64_t)x * a.W0 + y) * a.D0 + z]; };
+  const float c00 = fmaf(fz, at(x0, y0, z1) - at(x0, y0, z0), at(x0, y0, z0));
+  const float c01 = fmaf(fz, at(x0, y1, z1) - at(x0, y1, z0), at(x0, y1, z0));
+  const float c10 = fmaf(fz, at(x1, y0, z1) - at(x1, y0, z0), at(x1, y0, z0));
+  const float c11 = fmaf(fz, at(x1, y1, z1) - at(x1, y1, z0), at(x1, y1, z0));
+  const float c0 = fmaf(fy, c01 - c00, c00), c1 = fmaf(fy, c11 - c10, c10);
+  return fmaf(fx, c1 - c0, c0);
+}
+__device__ __forceinline__ int axis_near(float c, int n) {
+  const int i = (int)rintf(c);  // round half to even (grid_sample's nearbyint)
+  return i < 0 ? 0 : (i >= n ? n - 1 : i);
+}
+__device__ __forceinline__ float nearest(const float* v, const PrepArgs& a, const Coord3& c) {
+  return v[((int64_t)axis_near(c.x, a.H0) * a.W0 + axis_near(c.y, a.W0)) * a.D0 + axis_near(c.z, a.D0)];
+}
+
 __global__ __launch_bounds__(PNT) void k_prep_stats(PrepArgs a) {
   __shared__ double red[3][PNT / 64];
   const int bc = (int)blockIdx.y, b = bc / a.C, c = bc - b * a.C;
@@ -56,6 +99,18 @@ __global__ __launch_bounds__(PNT) void k_prep_stats(PrepArgs a) {
   double s = 0.0, s2 = 0.0, n = 0.0;
   for (int r = (int)blockIdx.x * (PNT / 64) + wid; r < rows; r += PCHUNK * (PNT / 64)) {  // a row per wave
     const int i = r / a.w, j = r - i * a.w;
+    if (q.resample) {
+      const Coord3 rb = map_row(q, i, j);
+      for (int k = lane; k < a.d; k += 64) {
+        const float v = trilinear(base, a, map_at(q, rb, k));
+        if (v != 0.f) {
+          s += v;
+          s2 += (double)v * v;
+          n += 1.0;
+        }
+      }
+      continue;
+    }
     const float* src = row_src(a, q, base, i, j);
     for (int k = lane; k < a.d; k += 64) {
       const float v = src[k];
@@ -126,9 +181,18 @@ __global__ __launch_bounds__(PNT) void k_prep_apply(PrepArgs a, int B) {
       const int64_t bc = r / nrow;
       const int rr = (int)(r - bc * nrow), i = rr / a.w, j = rr - i * a.w;
       const int b = (int)(bc / a.C), c = (int)(bc - (int64_t)b * a.C);
-      const float* src = row_src(a, a.p[b], a.img + b * a.isb + c * a.isc, i, j);
       const float ca = a.coef[bc * 3], cb = a.coef[bc * 3 + 1], cg = a.coef[bc * 3 + 2];
       float* dst = a.out + r * a.d;
+      if (a.p[b].resample) {
+        const float* base = a.img + b * a.isb + c * a.isc;
+        const Coord3 rb = map_row(a.p[b], i, j);
+        for (int k = lane; k < a.d; k += 64) {
+          const float v = trilinear(base, a, map_at(a.p[b], rb, k));
+          dst[k] = v != 0.f ? fmaf(ca, v, cb) : cg;
+        }
+        continue;
+      }
+      const float* src = row_src(a, a.p[b], a.img + b * a.isb + c * a.isc, i, j);
       const bool fd = a.p[b].flip & 4;
       for (int k = lane; k < a.d; k += 64) {
         const float v = src[fd ? a.d - 1 - k : k];
@@ -138,12 +202,14 @@ __global__ __launch_bounds__(PNT) void k_prep_apply(PrepArgs a, int B) {
       const int64_t lr = r - nimg;
       const int b = (int)(lr / nrow);
       const int rr = (int)(lr - (int64_t)b * nrow), i = rr / a.w, j = rr - i * a.w;
-      const float* src = row_src(a, a.p[b], a.lab + b * a.lsb, i, j);
+      const bool rs = a.p[b].resample;
+      const float* src = rs ? a.lab + b * a.lsb : row_src(a, a.p[b], a.lab + b * a.lsb, i, j);
+      const Coord3 rb = rs ? map_row(a.p[b], i, j) : Coord3{0.f, 0.f, 0.f};
       const int64_t plane = (int64_t)nrow * a.d;
       float* dst = a.olab + (int64_t)b * 3 * plane + (int64_t)rr * a.d;
       const bool fd = a.p[b].flip & 4;
       for (int k = lane; k < a.d; k += 64) {
-        const float v = src[fd ? a.d - 1 - k : k];
+        const float v = rs ? nearest(src, a, map_at(a.p[b], rb, k)) : src[fd ? a.d - 1 - k : k];
         const bool l1 = v == 1.f, l2 = v == 2.f, l3 = v == 3.f;
         dst[k] = (l2 || l3) ? 1.f : 0.f;             // TC: labels 2, 3
         dst[plane + k] = (l1 || l2 || l3) ? 1.f : 0.f;  // WT: labels 1, 2, 3
@@ -164,12 +230,19 @@ int tb_brats_prep_f32(const float* img, const float* lab, int B, int C, int H0, 
                       size_t ws_bytes, void* stream) {
   if (!img || !params || !out || B < 1 || C < 1 || H0 < 1 || W0 < 1 || D0 < 1 || h < 1 || w < 1 || d < 1)
     return TB_ERR_INVALID_ARG;
-  if (h > H0 || w > W0 || d > D0) return TB_ERR_INVALID_ARG;
+  bool crop_only = true;
+  for (int b = 0; b < B; ++b) crop_only &= params[b].resample == 0;
+  if (crop_only && (h > H0 || w > W0 || d > D0)) return TB_ERR_INVALID_ARG;
   if (out_lab && !lab) return TB_ERR_INVALID_ARG;
   if (!ws || ws_bytes < tb_brats_prep_workspace_bytes(B < TB_MAX_BATCH ? B : TB_MAX_BATCH, C))
     return TB_ERR_WORKSPACE;
   for (int b = 0; b < B; ++b) {
     const tb_prep_params& q = params[b];
+    if (q.resample) {  // any finite map: the sampling clamps to the volume
+      for (int e = 0; e < 12; ++e)
+        if (!std::isfinite(q.m[e])) return TB_ERR_INVALID_ARG;
+      continue;
+    }
     if (q.h0 < 0 || q.w0 < 0 || q.d0 < 0 || q.h0 + h > H0 || q.w0 + w > W0 || q.d0 + d > D0 || (q.flip & ~7))
       return TB_ERR_INVALID_ARG;
   }

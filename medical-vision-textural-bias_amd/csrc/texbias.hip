@@ -458,6 +458,7 @@ size_t tb_workspace_bytes(const tb_plan* plan, int bc) {
   g.NCOL = 32 * ((plan->dev.D / 2 + 1 + 31) / 32);
   g.cat = 0;  // 2 KS = 64 rows: the most either layout uses
   g.PT = 0;
+  g.NTD = (plan->dev.D + 31) / 32 + 64;  // the split-f16 table for any pad up to 2048 columns
   const size_t band = band_ws(g, plan->dev.H, bc).total;
   const size_t gen = plan->generic ? gen_workspace_bytes(plan->dev.H, plan->dev.W, plan->dev.D, bc) : 0;
   const size_t m = spec > band ? spec : band;
@@ -617,6 +618,7 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   for (int s = s0; s < s1; ++s) ptot += sp[s - s0].n;
   g.cat = (g_inv16 && g.NDk + ptot <= 32) ? 1 : 0;
   g.PT = g.cat ? ptot : 0;
+  g.NTD = (D + y_pad + 31) / 32;
   if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || KW >= 32 || KH > BAND_MAX_KH) return false;
   if (g.ncol > BAND_MAX_ZCOL || W > 1024) return false;
   if (2 * g.KS > 64 || g.KS > 32) return false;  // pass C' holds V in at most two 32-row MFMA tiles

@@ -62,4 +62,5 @@ def programs_array(programs):
 class TbPrepParams(C.Structure):
     """tb_prep_params (include/texbias.h): one sample's preprocessing draws."""
     _fields_ = [("h0", C.c_int), ("w0", C.c_int), ("d0", C.c_int), ("flip", C.c_int),
-                ("scale", C.c_float), ("shift", C.c_float), ("normalize", C.c_int), ("reserved", C.c_int)]
+                ("scale", C.c_float), ("shift", C.c_float), ("normalize", C.c_int), ("resample", C.c_int),
+                ("m", C.c_float * 12)]

@@ -14,6 +14,15 @@ stylized_gibbs12p5_spikes15_wrap0p5_sap0p05_3modalities.py:151-170.
   of each channel along the spatial axis; ``(x - mean) / std`` over the nonzero voxels of each
   channel (float32 ``np.mean`` / ``np.std``, std 0 -> 1); ``x * (1 + factor)``; ``x + offset``.
   MONAI is not installed here, so these are **parity unpinned** (no reference output to pin them).
+* ``spacing_orientation`` restates Spacingd(pixdim, mode=("bilinear", "nearest")) ->
+  Orientationd(axcodes="RAS") (…3modalities.py:156-161) step by step on arrays, for voxel-to-world
+  affines that are signed, scaled axis permutations (the BraTS case): the Spacing grid has
+  ``round((n - 1) |zoom| / pixdim + 1)`` voxels per axis and samples the input at
+  ``o * pixdim / |zoom|`` (trilinear image, nearest label rounding half to even, border clamp --
+  grid_sample's modes; a map within 1e-3 of the identity copies the data), then the axes are
+  flipped where the affine points away from R/A/S and transposed into (R, A, S) order.  Written
+  independently of the product's composed-affine host code (texbias/affine.py); **parity unpinned**
+  (MONAI and nibabel are absent).
 """
 from __future__ import annotations
 
@@ -71,4 +80,76 @@ def prep(img: np.ndarray, lab: Optional[np.ndarray], corner, roi, flip_axes=(), 
     y = None
     if lab is not None:
         y = flip(crop(convert_brats_classes(lab), corner, roi), flip_axes)
+    return x, y
+
+
+def _trilinear_border(v: np.ndarray, cx, cy, cz) -> np.ndarray:
+    """v [H, W, D]; coordinate grids (float64) -> float32 samples, border clamp."""
+    out = []
+    idx = []
+    for c, n in zip((cx, cy, cz), v.shape):
+        c = np.clip(c, 0.0, n - 1.0)
+        i0 = np.floor(c).astype(np.int64)
+        i1 = np.minimum(i0 + 1, n - 1)
+        idx.append((i0, i1, (c - i0).astype(np.float64)))
+    (x0, x1, fx), (y0, y1, fy), (z0, z1, fz) = idx
+    vv = v.astype(np.float64)
+    c00 = vv[x0, y0, z0] * (1 - fz) + vv[x0, y0, z1] * fz
+    c01 = vv[x0, y1, z0] * (1 - fz) + vv[x0, y1, z1] * fz
+    c10 = vv[x1, y0, z0] * (1 - fz) + vv[x1, y0, z1] * fz
+    c11 = vv[x1, y1, z0] * (1 - fz) + vv[x1, y1, z1] * fz
+    c0 = c00 * (1 - fy) + c01 * fy
+    c1 = c10 * (1 - fy) + c11 * fy
+    out = c0 * (1 - fx) + c1 * fx
+    return out.astype(np.float32)
+
+
+def _nearest_border(v: np.ndarray, cx, cy, cz) -> np.ndarray:
+    ii = [np.clip(np.rint(c).astype(np.int64), 0, n - 1) for c, n in zip((cx, cy, cz), v.shape)]
+    return v[ii[0], ii[1], ii[2]]
+
+
+def spacing_orientation(x: np.ndarray, affine: np.ndarray, pixdim: Sequence[float], nearest: bool = False,
+                        ras: bool = True) -> np.ndarray:
+    """[C, H, W, D] -> Spacing(pixdim) then Orientation("RAS") for a signed, scaled axis-permutation
+    affine (each voxel axis along one world axis)."""
+    R = np.asarray(affine, dtype=np.float64)[:3, :3]
+    zoom = np.sqrt((R * R).sum(axis=0))              # voxel size of each voxel axis
+    ratio = np.asarray(pixdim, dtype=np.float64) / zoom
+    shape = x.shape[1:]
+    if np.allclose(ratio, 1.0, atol=1e-3):
+        y = x.copy()
+    else:
+        out = [int(np.round((n - 1) / r + 1.0)) for n, r in zip(shape, ratio)]
+        g = np.meshgrid(*[np.arange(n, dtype=np.float64) * r for n, r in zip(out, ratio)], indexing="ij")
+        f = _nearest_border if nearest else _trilinear_border
+        y = np.stack([f(x[c], *g) for c in range(x.shape[0])])
+    if not ras:
+        return y
+    world = np.argmax(np.abs(R), axis=0)             # world axis of each voxel axis
+    sign = np.sign(R[world, np.arange(3)])
+    for ax in range(3):
+        if sign[ax] < 0:
+            y = np.flip(y, axis=1 + ax)
+    perm = [int(np.nonzero(world == a)[0][0]) for a in range(3)]   # output axis a <- voxel axis
+    return np.ascontiguousarray(y.transpose([0] + [1 + p for p in perm]))
+
+
+def prep_resampled(img: np.ndarray, lab: Optional[np.ndarray], affine: np.ndarray, pixdim, corner, roi,
+                   flip_axes=(), scale: Optional[float] = None, shift: Optional[float] = None,
+                   normalize: bool = True):
+    """Validation/training order of the drivers: labels to classes, Spacingd, Orientationd, crop,
+    flip, normalise, scale, shift (…3modalities.py:151-170, :179-190)."""
+    x = spacing_orientation(img, affine, pixdim)
+    x = flip(crop(x, corner, roi), flip_axes)
+    if normalize:
+        x = normalize_nonzero_channelwise(x)
+    if scale is not None:
+        x = (x * np.float32(scale)).astype(np.float32)
+    if shift is not None:
+        x = (x + np.float32(shift)).astype(np.float32)
+    y = None
+    if lab is not None:
+        y = spacing_orientation(convert_brats_classes(lab), affine, pixdim, nearest=True)
+        y = flip(crop(y, corner, roi), flip_axes)
     return x, y

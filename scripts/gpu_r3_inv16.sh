@@ -13,7 +13,7 @@ for cfg in c3 c2; do
     cat $O/pass_${cfg}_$v.json
   done
 done
-timeout -k 10 900 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests/test_gpu_c4_extremes.py tests/test_gpu_train_prod.py tests/test_gpu_ops.py tests/test_gpu_zf.py > $O/tests_new.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests/test_gpu_c4_extremes.py tests/test_gpu_prep.py tests/test_gpu_train_prod.py tests/test_gpu_ops.py tests/test_gpu_zf.py > $O/tests_new.log 2>&1
 rc=$?; grep -E "PASSED|FAILED|loss texbias" $O/tests_new.log | tail -40; [ $rc = 0 ] || { tail -60 $O/tests_new.log; exit $rc; }
 timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > $O/tests_all.log 2>&1
 rc=$?; tail -3 $O/tests_all.log; [ $rc = 0 ] || { tail -60 $O/tests_all.log; exit $rc; }

@@ -20,3 +20,23 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def heartbeat(request):
+    """Print a progress line every 30 s while a long GPU test runs (fresh boxes compile MIOpen kernels
+    for minutes; the line shows the test is alive, not hung)."""
+    import threading
+    import time
+    stop = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not stop.wait(30.0):
+            print(f"[heartbeat] {request.node.name} {time.time() - t0:.0f} s", flush=True)
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
+    th.join(timeout=1.0)

@@ -67,3 +67,76 @@ def test_dataset_eval_multi_matches_reference_loop(gpu, tmp_path):
     ev2 = ModelEvaluation()
     ev2.load_dict(f)
     assert ev2.eval_dict == ev.eval_dict
+
+
+def _raw_cases(n, sp, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        img = (rng.standard_normal((4,) + sp) * 2.0 + 1.0).astype(np.float32)
+        img[:, :2] = 0.0                                   # background slab
+        lab = rng.integers(0, 4, size=sp).astype(np.float32)
+        out.append((img, lab, np.diag([-1.0, -1.0, 1.0, 1.0])))
+    return out
+
+
+def test_brats_val_iter_dataset_disk_matches_oracle(gpu):
+    """utils.py:159-235: the fixed split's test half through Spacing -> Orientation(RAS) ->
+    CenterSpatialCrop -> NormalizeIntensity -> the named filter, on the device; the disk filter's
+    output against the oracle chain (1e-5), labels exact; loaders batch 2, unshuffled."""
+    import filters_and_operators as F
+    from oracle import filters_oracle as O
+    from oracle import prep_oracle as PO
+    from texbias.evaluation import BratsValIterDataset, ModelEvaluation
+    from texbias.train import reference_model
+    sp, roi = (40, 36, 30), (16, 16, 8)
+    src = _raw_cases(8, sp, 4)
+    tr = {"disk": F.RandFourierDiskMaskd(keys="image", r=5.5, inside_off=False, prob=1.0),
+          "sap": F.SaltAndPepper(0.1)}
+    ds = BratsValIterDataset(src, tr, return_loader=True, split=(4, 4), roi=roi)
+    names = []
+    for name, loader in ds:
+        names.append(name)
+        batches = list(loader)
+        assert [b["image"].shape[0] for b in batches] == [2, 2]
+        for bi, b in enumerate(batches):
+            for j in range(2):
+                img, lab, aff = src[ds.test_indices[2 * bi + j]]
+                shp = PO.spacing_orientation(img, aff, (1.5, 1.5, 2.0)).shape[1:]
+                corner = tuple(n // 2 - r // 2 for n, r in zip(shp, roi))   # CenterSpatialCrop
+                xr, yr = PO.prep_resampled(img, lab, aff, (1.5, 1.5, 2.0), corner, roi)
+                np.testing.assert_array_equal(b["label"][j].cpu().numpy(), yr)
+                got = b["image"][j].cpu().numpy()
+                if name == "disk":
+                    ref = O.fourier_disk(xr, 5.5)
+                    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-5
+                else:   # salt and pepper: every voxel kept or set to the sample's min/2 or max/2
+                    keep = got == xr
+                    lo, hi = np.float32(xr.min()) / 2, np.float32(xr.max()) / 2
+                    assert np.all(keep | (got == lo) | (got == hi)) and 0.8 < keep.mean() < 0.97
+    assert names == ["disk", "sap"]
+    # the per-sample view and the evaluation harness on a named set
+    one = BratsValIterDataset(src, tr, split=(4, 4), roi=roi)["disk"]
+    assert len(one) == 4 and one[0]["image"].shape == (4,) + roi
+    ev = ModelEvaluation(model=reference_model(4, 3), instance_name="val")
+    ev.add_eval("disk", ds["disk"])
+    assert set(ev.eval_dict["disk"]) == {"mean", "et", "tc", "wt"}
+
+
+def test_load_gibbs_and_spikes_unet(gpu, tmp_path):
+    """ModelEvaluation(model_path, gibbs_unet=True / spikes_unet=True) loads like utils.py:286-297;
+    a reference-style Gibbs_UNet state dict (no alpha entry) loads with alpha 0.5."""
+    import stylization_layers as SL
+    from texbias.evaluation import ModelEvaluation
+    torch.manual_seed(0)
+    g = SL.Gibbs_UNet()
+    sd = {k: v for k, v in g.state_dict().items() if k != "gibbs.alpha"}
+    torch.save(sd, tmp_path / "g.pth")
+    ev = ModelEvaluation(str(tmp_path / "g.pth"), gibbs_unet=True, in_channels=1, out_channels=1)
+    assert isinstance(ev.model, SL.Gibbs_UNet) and float(ev.model.gibbs.alpha) == 0.5
+    for k, v in sd.items():
+        assert torch.equal(ev.model.state_dict()[k].cpu(), v.cpu()), k
+    s = SL.Spikes_UNet()
+    torch.save(s.state_dict(), tmp_path / "s.pth")
+    ev2 = ModelEvaluation(str(tmp_path / "s.pth"), spikes_unet=True, in_channels=1, out_channels=1)
+    assert isinstance(ev2.model, SL.Spikes_UNet)

@@ -66,3 +66,76 @@ def test_prep_feeds_fused_chain(gpu):
     chain, _ = reference_c3_chain(0)
     out = chain(x)
     assert out.shape == x.shape and torch.isfinite(out).all()
+
+
+RESAMPLE_CASES = [
+    # (raw shape, affine, pixdim, roi, center crop)
+    ((60, 54, 40), np.diag([-1.0, -1.0, 1.0, 1.0]), (1.5, 1.5, 2.0), (32, 32, 16), True),    # BraTS LPS -> RAS
+    ((60, 54, 40), np.diag([-1.0, -1.0, 1.0, 1.0]), (1.5, 1.5, 2.0), (24, 32, 16), False),   # random crop + flips
+    ((44, 50, 36), np.array([[0.0, -0.75, 0.0, 3.0], [1.0, 0.0, 0.0, -2.0], [0.0, 0.0, 1.25, 7.0],
+                             [0.0, 0.0, 0.0, 1.0]]), (1.5, 1.5, 2.5), (16, 24, 16), True),  # permuted axes
+]
+
+
+@pytest.mark.parametrize("case", range(len(RESAMPLE_CASES)))
+def test_prep_spacing_orientation_matches_oracle(gpu, case):
+    """Spacingd(pixdim, bilinear/nearest) -> Orientationd(RAS) -> crop -> flip -> normalise -> scale
+    -> shift as one affine gather on the GPU (texbias.affine + tb_brats_prep_f32 resample mode)
+    against the step-by-step oracle: image 1e-5, label classes bit-exact (nearest, half to even)."""
+    from texbias.prep import BratsPrep
+    sp, aff, pixdim, roi, center = RESAMPLE_CASES[case]
+    B, C = 2, 4
+    img, lab = _raw(B, C, sp, 10 + case)
+    prep = BratsPrep(roi_size=roi, pixdim=pixdim, axcodes="RAS", center_crop=center,
+                     flip_axis=(0, 2), flip_prob=0.0 if center else 1.0, scale_prob=1.0,
+                     shift_prob=1.0).set_random_state(case)
+    affs = [aff, aff]
+    M, shp = prep.spatial_map(sp, aff)
+    params = prep.draw(B, sp, affs)
+    x, y = prep(torch.from_numpy(img).cuda(), torch.from_numpy(lab).cuda(), params=params, affines=affs)
+    for b, q in enumerate(params):
+        G = np.array(list(q.m)).reshape(3, 4)
+        # the crop corner the host drew: the map's translation at output voxel 0, back through M
+        corner = np.rint(np.linalg.solve(M[:3, :3], G[:, 3] - M[:3, 3])).astype(int)
+        if not center:   # flips (0, 2) drawn with prob 1: the corner is at the window's far end there
+            corner[[0, 2]] -= np.array(roi)[[0, 2]] - 1
+        xr, yr = PO.prep_resampled(img[b], lab[b], aff, pixdim, tuple(corner), roi,
+                                   flip_axes=() if center else (0, 2), scale=q.scale, shift=q.shift)
+        assert xr.shape == (C,) + roi
+        np.testing.assert_allclose(x[b].cpu().numpy(), xr, rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(y[b].cpu().numpy(), yr)
+
+
+def test_prep_spacing_identity_at_matching_pixdim(gpu):
+    """A volume already at the target voxel size: Spacing is the identity (MONAI copies), so the
+    resample path equals the crop-only path bit for bit."""
+    from texbias.prep import BratsPrep
+    B, C, sp, roi = 2, 4, (40, 36, 30), (32, 24, 16)
+    img, lab = _raw(B, C, sp, 21)
+    aff = np.diag([1.5, 1.5, 2.0, 1.0])
+    rs = BratsPrep(roi_size=roi, pixdim=(1.5, 1.5, 2.0), axcodes="RAS", flip_prob=1.0).set_random_state(4)
+    plain = BratsPrep(roi_size=roi, flip_prob=1.0).set_random_state(4)
+    pr = rs.draw(B, sp, [aff, aff])
+    pp = plain.draw(B, sp)
+    assert all(q.resample == 1 for q in pr)
+    xi, li = torch.from_numpy(img).cuda(), torch.from_numpy(lab).cuda()
+    x1, y1 = rs(xi, li, params=pr)
+    x2, y2 = plain(xi, li, params=pp)
+    assert torch.equal(x1, x2) and torch.equal(y1, y2)
+
+
+def test_brats_val_shapes(gpu):
+    """The validation Compose's spatial part on a BraTS-sized raw volume (240 x 240 x 155 at 1 mm,
+    LPS): Spacing (1.5, 1.5, 2.0) -> 160 x 160 x 78, RAS, CenterSpatialCrop 128 x 128 x 64."""
+    from texbias.prep import BratsPrep
+    prep = BratsPrep(pixdim=(1.5, 1.5, 2.0), axcodes="RAS", center_crop=True, flip_prob=0.0, scale_prob=0.0,
+                     shift_prob=0.0)
+    M, shp = prep.spatial_map((240, 240, 155), np.diag([-1.0, -1.0, 1.0, 1.0]))
+    assert shp == (160, 160, 78)
+    img, lab = _raw(1, 4, (240, 240, 155), 5)
+    x, y = prep(torch.from_numpy(img).cuda(), torch.from_numpy(lab).cuda(), affines=[np.diag([-1.0, -1.0, 1.0, 1.0])])
+    assert x.shape == (1, 4, 128, 128, 64) and y.shape == (1, 3, 128, 128, 64)
+    xr, yr = PO.prep_resampled(img[0], lab[0], np.diag([-1.0, -1.0, 1.0, 1.0]), (1.5, 1.5, 2.0), (16, 16, 7),
+                               (128, 128, 64))
+    np.testing.assert_allclose(x[0].cpu().numpy(), xr, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(y[0].cpu().numpy(), yr)

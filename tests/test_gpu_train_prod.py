@@ -197,7 +197,7 @@ def test_train_step_full_volume_finite_and_fast_paths(gpu):
     assert sum(fast) >= 10, fast
 
 
-def test_train_step_full_volume_matches_aten(gpu):
+def test_train_step_full_volume_matches_aten(gpu, heartbeat):
     """The whole bench-shaped step (U-Net 4->3 on 2 x 4 x 240 x 240 x 160, DiceLoss(sigmoid,
     squared_pred), backward) through the texbias kernels against the same weights and batch with
     every texbias path switched off (MIOpen/ATen convolutions and gradients, ATen InstanceNorm3d +
@@ -231,5 +231,10 @@ def test_train_step_full_volume_matches_aten(gpu):
     worst = max(errs, key=errs.get)
     print(f"loss texbias {l_tb.item():.8f} aten {l_at.item():.8f}; worst grad {worst} {errs[worst]:.3e}; "
           f"median {sorted(errs.values())[len(errs) // 2]:.3e} over {len(errs)} tensors")
+    pa = dict(aten.named_parameters())
+    for n in sorted(errs, key=errs.get)[-8:]:
+        g, q = dict(model.named_parameters())[n].grad, pa[n].grad
+        print(f"  {n}: err {errs[n]:.3e} max|g| {g.abs().max().item():.6e} max|g_aten| {q.abs().max().item():.6e} "
+              f"g {g.flatten()[:3].tolist()} aten {q.flatten()[:3].tolist()}")
     assert abs(l_tb.item() - l_at.item()) < 1e-5
     assert errs[worst] < 2e-3, errs

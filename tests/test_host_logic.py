@@ -102,3 +102,14 @@ def test_product_path_fails_loudly_without_gpu():
         F.WrapArtifact(0.5)(torch.zeros(1, 8, 8, 8))
     with pytest.raises(TexbiasError):
         F.GibbsNoise(0.5)(np.zeros((1, 8, 8, 8), np.float32))
+
+
+def test_brats_val_split_is_random_split():
+    """BratsValIterDataset keeps the second half of random_split(ds, [48, 48], manual_seed(0))
+    (utils.py:216) -- the same 48 validation cases as the reference."""
+    import torch
+    from texbias.evaluation import BratsValIterDataset
+    src = [None] * 96
+    ds = BratsValIterDataset(src, {}, device=torch.device("cpu"))
+    _, test = torch.utils.data.random_split(range(96), [48, 48], torch.Generator().manual_seed(0))
+    assert ds.test_indices == list(test.indices)

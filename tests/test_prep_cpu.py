@@ -44,3 +44,44 @@ def test_oracle_prep_composition():
     nz = c[0] != 0
     ref = np.where(nz, (c[0] - c[0][nz].mean()) / c[0][nz].std(), 0) * np.float32(1.05) + np.float32(-0.02)
     np.testing.assert_allclose(x[0], ref, rtol=1e-5, atol=1e-6)
+
+
+def _gather_with_map(vol, G, roi, nearest=False):
+    """Numpy emulation of the device's resample gather: output voxel o samples vol at G[:, :3] o + G[:, 3]."""
+    from oracle import prep_oracle as PO
+    o = np.meshgrid(*[np.arange(n, dtype=np.float64) for n in roi], indexing="ij")
+    c = [G[a, 0] * o[0] + G[a, 1] * o[1] + G[a, 2] * o[2] + G[a, 3] for a in range(3)]
+    f = PO._nearest_border if nearest else PO._trilinear_border
+    return np.stack([f(vol[k], *c) for k in range(vol.shape[0])])
+
+
+@pytest.mark.parametrize("aff,pixdim,sp,roi,center", [
+    (np.diag([-1.0, -1.0, 1.0, 1.0]), (1.5, 1.5, 2.0), (60, 54, 40), (32, 32, 16), True),
+    (np.diag([-1.0, -1.0, 1.0, 1.0]), (1.5, 1.5, 2.0), (60, 54, 40), (24, 32, 16), False),
+    (np.array([[0.0, -0.75, 0.0, 3.0], [1.0, 0.0, 0.0, -2.0], [0.0, 0.0, 1.25, 7.0], [0, 0, 0, 1.0]]),
+     (1.5, 1.5, 2.5), (44, 50, 36), (16, 24, 16), True),
+    (np.diag([1.0, 1.0, 1.0, 1.0]), (1.0, 1.0, 1.0), (20, 22, 18), (16, 16, 8), False),
+])
+def test_composed_affine_map_matches_stepwise_oracle(aff, pixdim, sp, roi, center):
+    """texbias.affine's one-map composition of Spacing -> Orientation -> crop -> flip (host logic of
+    tb_brats_prep_f32's resample mode) equals the oracle's step-by-step arrays (image 1e-6, labels exact)."""
+    from oracle import prep_oracle as PO
+    from texbias.prep import BratsPrep
+    rng = np.random.default_rng(0)
+    img = rng.standard_normal((2,) + sp).astype(np.float32)
+    lab = rng.integers(0, 5, size=sp).astype(np.float32)
+    prep = BratsPrep(roi_size=roi, pixdim=pixdim, axcodes="RAS", center_crop=center, flip_axis=(0, 2),
+                     flip_prob=0.0 if center else 1.0).set_random_state(1)
+    M, shp = prep.spatial_map(sp, aff)
+    q = prep.draw(1, sp, [aff])[0]
+    G = np.array(list(q.m), dtype=np.float64).reshape(3, 4)
+    cf = np.linalg.solve(M[:3, :3], G[:, 3] - M[:3, 3])
+    corner = np.rint(cf).astype(int)
+    flips = () if center else (0, 2)
+    for a in flips:
+        corner[a] -= roi[a] - 1
+    ref = PO.flip(PO.crop(PO.spacing_orientation(img, aff, pixdim), corner, roi), flips)
+    got = _gather_with_map(img, G, roi)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-6)
+    lref = PO.flip(PO.crop(PO.spacing_orientation(lab[None], aff, pixdim, nearest=True), corner, roi), flips)
+    np.testing.assert_array_equal(_gather_with_map(lab[None], G, roi, nearest=True), lref)
