@@ -172,7 +172,10 @@ TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
 // Split-f16 pass C' (k_band_inv16): the unfolded synthesis table as MFMA B fragments
 // [NTD][nch][hi/lo][64 lanes][8 halves] (NTD 32-column tiles of the stored row, nch 16-row chunks
 // of V), then the W twiddles, BAND_SLOTS16 slabs' V-product fragments, the slabs' point kw.
-constexpr int BAND_SLOTS16 = 3;
+#ifndef TB_BAND_SLOTS16
+#define TB_BAND_SLOTS16 3
+#endif
+constexpr int BAND_SLOTS16 = TB_BAND_SLOTS16;
 TB_HD int band_nch(const BandGeo& g) { return (band_rows(g) + 15) / 16; }
 TB_HD int band_t16_bytes(const BandGeo& g) { return g.NTD * band_nch(g) * 2 * 64 * 16; }
 struct BandInv16Carve {

@@ -915,8 +915,11 @@ __global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
   T[(cc * 2 + 1) * 64 + lane] = fl;
 }
 
+#ifndef TB_INV16_WPE
+#define TB_INV16_WPE 4  // waves per SIMD the VT = 1 split-f16 kernel is compiled for (register budget)
+#endif
 template <int VT>  // 32-row tiles of V
-__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5))) void k_band_inv16(BandInvArgs) {
+__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1 ? TB_INV16_WPE : 3, 8))) void k_band_inv16(BandInvArgs) {
   // Same unit structure as k_band_inv: (slab, 32-row tile) units dealt to a persistent grid, each
   // workgroup's slabs in batches whose V-product fragments are loaded to LDS first (the unit loop
   // then issues no vector-memory loads), per-unit min/max partials.
@@ -946,6 +949,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
   const int ntw = (W + 31) / 32;
   const int nslab = H * a.nbc;
   const int ncolo = D + a.ypad;        // stored columns of a row
+  const int diag = a.diag;             // measurement only (TEXBIAS_BAND_DIAG >> 8): skipped stages
+  if (diag & 64) return;
   const int nunit = nslab * ntw;
   const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
   const int ub = (int)blockIdx.x * per, ue = ub + per < nunit ? ub + per : nunit;
@@ -993,6 +998,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
       }
     }
     __syncthreads();
+    if (diag & 32) return;
     for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {
       const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
       const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
@@ -1006,7 +1012,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
         for (int j = 0; j < 16; ++j) vacc[vt][j] = 0.f;
       int t = 0;
       int ks = 0;
-      for (; ks + 4 <= KW + 1; ks += 4) {
+      const int kse = (diag & 4) ? 0 : KW + 1;
+      for (; ks + 4 <= kse; ks += 4) {
         float fa[4][VT], bb[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1023,7 +1030,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
           for (int vt = 0; vt < VT; ++vt)
             vacc[vt] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[q][vt], bb[q], vacc[vt], 0, 0, 0);
       }
-      for (; ks < KW + 1; ++ks) {
+      for (; ks < kse; ++ks) {
         const float2 c = twW[t];
         const float b = hl ? -c.y : c.x;
 #pragma unroll
@@ -1032,7 +1039,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
         t += wm;
         t = t >= W ? t - W : t;
       }
-      for (int j = 0; j < npm; ++j) {
+      for (int j = 0; j < (kse ? npm : 0); ++j) {
         const int kw = Pkw[slot * BAND_MAX_PTS + j];
         const float2 c = twW[(kw * wm) % W];
         const float b = hl ? -c.y : c.x;
@@ -1071,7 +1078,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
         for (int j = 0; j < 16; ++j) acc[j] = 0.f;
 #pragma unroll
         for (int c = 0; c < 2 * VT; ++c) {
-          if (c >= nch) break;
+          if (c >= nch || (diag & 8)) break;
           const h16x8* tp = Tab + ((nt * nch + c) * 2) * 64 + lane;
           const h16x8 th = tp[0], tl = tp[64];
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, acc, 0, 0, 0);
@@ -1079,6 +1086,13 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(3, 5)))
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], th, acc, 0, 0, 0);
         }
         const int col = 32 * nt + l31;
+        if (diag & 16) {  // no stores: keep the results live
+          float z = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) z += acc[r];
+          lo = fminf(lo, z);
+          continue;
+        }
         if (col < ncolo) {
           float* yc = yb + col;
           const bool img = col < D;
@@ -1214,8 +1228,8 @@ int band_occupancy(K kern, size_t lds, int nt, int cap) {
 }
 
 template <class K>
-int band_grid(K kern, int units, size_t lds, int ncu) {
-  const int per_cu = band_occupancy(kern, lds, BAND_NT, 4);
+int band_grid(K kern, int units, size_t lds, int ncu, int cap = 4) {
+  const int per_cu = band_occupancy(kern, lds, BAND_NT, cap);
   const int g = ncu * per_cu;
   return units < g ? units : g;
 }
@@ -1247,7 +1261,7 @@ hipError_t launch_inv16_t(const BandInvArgs& a, int ncu, hipStream_t st) {
   auto kern = k_band_inv16<VT>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(band_grid(kern, a.pl.H * a.nbc, lds, ncu)), dim3(BAND_NT), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(band_grid(kern, a.pl.H * a.nbc, lds, ncu, 8)), dim3(BAND_NT), lds, st, a);
   return hipGetLastError();
 }
 

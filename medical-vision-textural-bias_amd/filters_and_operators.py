@@ -12,6 +12,10 @@ device-side stage ``texbias.pipeline.FusedChain`` after collation instead of
 per-sample calls inside DataLoader workers.  The arithmetic goes through the
 ``torch.ops.texbias.*`` custom operators (``texbias/ops.py``).
 
+Inside ``DataLoader`` worker processes (forked: no HIP context) the dictionary transforms defer:
+they make their draws and record the sample's stage for one batched GPU pass in the main process
+(``texbias.deferred``: ``deferred_collate`` + ``run_deferred`` / ``DeferredLoader``).
+
 Reference line numbers are cited per class (``filters_and_operators.py:N``).
 """
 from __future__ import annotations
@@ -23,6 +27,7 @@ from typing import Any, Dict, Hashable, List, Mapping, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from texbias import deferred as _D
 from texbias import kprog as _K
 from texbias import ops as _ops  # registers torch.ops.texbias.*
 from texbias import runtime as _rt
@@ -36,7 +41,7 @@ __all__ = [
     "SelectChanneld", "ConvertToMultiChannelBasedOnBratsClassesd", "WholeTumorTCGA", "disk_mask",
     "RandFourierDiskMaskd", "ellipsoid", "RandPlaneWaves_ellipsoid", "SaltAndPepper", "WrapArtifact",
     "WrapArtifactd", "SegmentationSlicesd", "Fourier", "GibbsNoise", "RandGibbsNoise", "RandGibbsNoised",
-    "KSpaceSpikeNoise", "RandKSpaceSpikeNoise", "RandKSpaceSpikeNoised",
+    "KSpaceSpikeNoise", "RandKSpaceSpikeNoise", "RandKSpaceSpikeNoised", "MultimodalSlicesd",
 ]
 
 
@@ -44,6 +49,10 @@ __all__ = [
 def _device_of(t) -> torch.device:
     if isinstance(t, torch.Tensor) and t.device.type == "cuda":
         return t.device
+    if torch.utils.data.get_worker_info() is not None:
+        raise _rt.TexbiasError(
+            "texbias filters cannot run inside a (forked) DataLoader worker: use the dictionary transforms, which "
+            "defer there, with collate_fn=texbias.deferred.deferred_collate and texbias.deferred.DeferredLoader")
     if not torch.cuda.is_available():
         raise _rt.TexbiasError("texbias filters need a HIP device (there is no CPU implementation)")
     return torch.device("cuda", torch.cuda.current_device())
@@ -64,7 +73,8 @@ def _kspace(img: torch.Tensor, n_dims: int, program: Sequence, pad: int = 0) -> 
     lead = x.shape[: x.dim() - n_dims]
     chans = int(np.prod(lead)) if len(lead) else 1
     xb = x.reshape((1, chans) + tuple(x.shape[x.dim() - n_dims:]))
-    y, _ = torch.ops.texbias.kspace_filter(xb, n_dims, _ops.pack_programs([list(program)]), chans, 0)
+    geo = _K.geometry(tuple(x.shape[x.dim() - n_dims:]))
+    y, _ = torch.ops.texbias.kspace_filter(xb, n_dims, _ops.pack_programs_split([list(program)], geo.hwd), chans, 0)
     y = y.reshape(tuple(x.shape))
     return y if img.device == dev else y.to(img.device)
 
@@ -85,14 +95,21 @@ class SelectChanneld(MapTransform):
                     if d[key].shape[0] <= i:
                         raise AssertionError(
                             f"Provided channel index {i} larger than max channel index for key = {key}")
-                    d[key] = d[key][i][None, :]
+                    self._select(d, key, i)
             else:
                 for key in self.key_iterator(d):
-                    d[key] = d[key][self.chan_num[0]][None, :]
+                    self._select(d, key, self.chan_num[0])
         else:
             for key in self.key_iterator(d):
-                d[key] = data[key][self.chan_num][None, :]
+                self._select(d, key, self.chan_num)
         return d
+
+    @staticmethod
+    def _select(d, key, c) -> None:
+        if _D.active() and _D.has_plan(d, key):  # a deferred filter is pending: select after it
+            _D.record(d, key, ("sel", int(c)))
+        else:
+            d[key] = d[key][c][None, :]
 
 
 class ConvertToMultiChannelBasedOnBratsClassesd(MapTransform):
@@ -174,6 +191,10 @@ class RandFourierDiskMaskd(RandomizableTransform, MapTransform):
     def __call__(self, data):
         d = dict(data)
         self.randomize()
+        if _D.active():
+            for key in self.key_iterator(d):
+                _D.record(d, key, ("k", self.program() if self._do_transform else []))
+            return d
         if not self._do_transform:
             return d
         for key in self.key_iterator(d):
@@ -253,6 +274,13 @@ class RandPlaneWaves_ellipsoid(RandomizableTransform, MapTransform):
     def __call__(self, data, phase: Optional[Sequence[float]] = None):
         d = dict(data)
         self.randomize(None)
+        if _D.active():
+            for key in self.key_iterator(d):
+                prog = self.program_for(tuple(d[key].shape[-3:]), phase) if self._do_transform else []
+                for op in prog[1:]:
+                    op.reserved = 1
+                _D.record(d, key, ("k", prog))
+            return d
         if not self._do_transform:
             return d
         for key in self.key_iterator(d):
@@ -298,6 +326,10 @@ class SaltAndPepper(MapTransform, RandomizableTransform):
     def __call__(self, data):
         d = dict(data)
         self.randomize(None)
+        if _D.active():   # the Philox key is drawn here, in the worker, as the eager call draws it
+            for key in self.key_iterator(d):
+                _D.record(d, key, ("sap", self.p, _philox_seed()) if self._do_transform else ("sap", None, None))
+            return d
         if not self._do_transform:
             return d
         for key in self.key_iterator(d):
@@ -364,7 +396,10 @@ class WrapArtifactd(MapTransform):
     def __call__(self, data: Mapping[Hashable, torch.Tensor]):
         d = dict(data)
         for key in self.key_iterator(d):
-            d[key] = self.transform(d[key])
+            if _D.active():
+                _D.record(d, key, ("k", self.transform.program()))
+            else:
+                d[key] = self.transform(d[key])
         return d
 
 
@@ -477,6 +512,11 @@ class RandGibbsNoised(RandomizableTransform, MapTransform):
     def __call__(self, data: Mapping[Hashable, Union[torch.Tensor, np.ndarray]]) -> Dict[Hashable, Any]:
         d = dict(data)
         self._randomize(None)
+        if _D.active():
+            for key in self.key_iterator(d):
+                sp = tuple(d[key].shape[1:])
+                _D.record(d, key, ("k", [_K.gibbs_op(self.sampled_alpha, sp)] if self._do_transform else []))
+            return d
         transform = None
         for i, key in enumerate(self.key_iterator(d)):
             if self._do_transform:
@@ -685,6 +725,14 @@ class RandKSpaceSpikeNoised(RandomizableTransform, MapTransform):
         if self.common_sampling:
             for k in self.keys:
                 self.transforms[k].set_random_state(self.common_seed)
+        if _D.active():
+            from texbias.pipeline import spike_program
+            for key, t in self.key_iterator(d, self.transforms):
+                img = d[key]
+                prog = spike_program(self.transforms[t], int(img.shape[0]), tuple(img.shape[1:])) \
+                    if self._do_transform else []
+                _D.record(d, key, ("k", prog))
+            return d
         for key, t in self.key_iterator(d, self.transforms):
             if self._do_transform:
                 d[key] = self.transforms[t](d[key])
@@ -702,3 +750,34 @@ class RandKSpaceSpikeNoised(RandomizableTransform, MapTransform):
 
     def _to_numpy(self, d: Union[torch.Tensor, np.ndarray]) -> np.ndarray:
         return d.cpu().detach().numpy() if isinstance(d, torch.Tensor) else d
+
+
+class MultimodalSlicesd(Randomizable, MapTransform):
+    """One random image channel and one label channel per sample: the drivers' own glue class
+    (10_scripts/127_gibbs_spikes_wraparound_sap_OneChannel/
+    stylized_gibbs12p5_spikes15_wrap0p5_sap0p05_3modalities.py:82-109), provided here so that a
+    deferred Compose (texbias.deferred) can select AFTER the deferred filters: ``c =
+    R.choice(img_chan_indices)`` once per call, image -> image[c], label -> label[label_idx]."""
+
+    def __init__(self, keys, img_chan_indices: list = [0], label_idx: int = 0, seed: int = None,  # noqa: B006
+                 allow_missing_keys: bool = False):
+        Randomizable.set_random_state(self, seed=seed)
+        MapTransform.__init__(self, keys, allow_missing_keys)
+        self.img_chan_indices = img_chan_indices
+        self.label_idx = label_idx
+
+    def randomize(self, data=None):
+        pass
+
+    def __call__(self, data):
+        d = dict(data)
+        c = self.R.choice(self.img_chan_indices)
+        for key in self.key_iterator(d):
+            if key == "image":
+                if _D.active() and _D.has_plan(d, key):
+                    _D.record(d, key, ("sel", int(c)))
+                else:
+                    d[key] = d[key][c].unsqueeze(0)
+            elif key == "label":
+                d[key] = d[key][self.label_idx].unsqueeze(0)
+        return d

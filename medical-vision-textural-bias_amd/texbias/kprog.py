@@ -22,7 +22,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from ._abi import (TB_OP_DISK, TB_OP_GIBBS, TB_OP_LAYER, TB_OP_SPIKE, TB_OP_WRAP, TB_OP_ZF, TbOp)
+from ._abi import (TB_MAX_OPS, TB_OP_DISK, TB_OP_GIBBS, TB_OP_LAYER, TB_OP_SPIKE, TB_OP_WRAP, TB_OP_ZF, TbOp)
 
 
 @dataclass(frozen=True)
@@ -209,3 +209,60 @@ def spike_op(idx_shifted: Sequence[int], geo: Geometry, log_intensity: float,
 
 
 Program = List[TbOp]
+
+
+def _copy(op: TbOp) -> TbOp:
+    c = TbOp()
+    C_ = type(op)
+    for name, _ in C_._fields_:
+        v = getattr(op, name)
+        setattr(c, name, v if not hasattr(v, "_length_") else type(v)(*v))
+    return c
+
+
+def _touch(a: TbOp, b: TbOp, hwd: Sequence[int]) -> bool:
+    """Spikes ``a`` and ``b`` reach the same stored coefficient (equal or conjugate frequencies,
+    overlapping channels)."""
+    if a.kind != TB_OP_SPIKE or b.kind != TB_OP_SPIKE:
+        return True
+    if a.chan != -1 and b.chan != -1 and a.chan != b.chan:
+        return False
+    fa = tuple(int(v) for v in a.i)
+    fb = tuple(int(v) for v in b.i)
+    conj = tuple((n - v) % n for v, n in zip(fb, hwd))
+    return fa == fb or fa == conj
+
+
+def split_program(prog: Sequence[TbOp], hwd: Sequence[int], max_ops: int = TB_MAX_OPS) -> List[List[TbOp]]:
+    """Cut a program longer than one launch holds (``TB_MAX_OPS``) into passes run one after the
+    other, each FFT -> ops -> inverse FFT (.real), at points where that is exact:
+
+    * between two reference calls (ops not joined by ``reserved``): the reference itself takes
+      ``.real`` after every call (SURVEY G4), which a separate pass reproduces;
+    * inside one call's group of spikes (KSpaceSpikeNoise with many locations, channel-wise
+      draws): a later part reads the spectrum after the earlier part's pass, which differs from the
+      pre-call spectrum only at the earlier part's own frequencies and their conjugates -- so the cut
+      is exact when no spike of the later part touches those (same or conjugate frequency in an
+      overlapping channel); otherwise ValueError.
+    The first op of every later pass starts a new group."""
+    if len(prog) <= max_ops:
+        return [list(prog)]
+    chunks: List[List[TbOp]] = [[]]
+    group: List[Tuple[int, TbOp]] = []   # the current call's spikes so far, with their pass index
+    for op in prog:
+        cut = len(chunks[-1]) == max_ops
+        if cut:
+            chunks.append([])
+        k = len(chunks) - 1
+        if not op.reserved:
+            group = []
+        elif any(ki < k and _touch(g, op, hwd) for ki, g in group):
+            raise ValueError("cannot split this spike group exactly: two of its spikes share a frequency "
+                             "(or its conjugate) in one channel")
+        o = op
+        if cut and op.reserved:
+            o = _copy(op)
+            o.reserved = 0
+        chunks[-1].append(o)
+        group.append((k, op))
+    return chunks

@@ -31,10 +31,22 @@ _REC = C.sizeof(TbSampleOps)
 
 
 def pack_programs(programs: Sequence[Sequence]) -> torch.Tensor:
-    """list (per sample) of op lists -> uint8 CPU tensor [B, sizeof(tb_sample_ops)]."""
+    """list (per sample) of op lists -> uint8 CPU tensor [B, sizeof(tb_sample_ops)]; with a program
+    longer than TB_MAX_OPS, [passes, B, sizeof(tb_sample_ops)] (cut by ``kprog.split_program``:
+    needs the op's frequency geometry, so such programs go through ``pack_programs_split``)."""
     arr = programs_array(programs)
     buf = np.frombuffer(C.string_at(C.addressof(arr), C.sizeof(arr)), dtype=np.uint8).copy()
     return torch.from_numpy(buf).reshape(len(programs), _REC)
+
+
+def pack_programs_split(programs: Sequence[Sequence], hwd: Sequence[int]) -> torch.Tensor:
+    """``pack_programs`` for programs of any length: [passes, B, REC] when one exceeds TB_MAX_OPS."""
+    from ._abi import TB_MAX_OPS
+    if all(len(p) <= TB_MAX_OPS for p in programs):
+        return pack_programs(programs)
+    parts = [K.split_program(list(p), hwd) for p in programs]
+    npass = max(len(c) for c in parts)
+    return torch.stack([pack_programs([c[i] if i < len(c) else [] for c in parts]) for i in range(npass)])
 
 
 def unpack_programs(t: torch.Tensor) -> List[TbSampleOps]:
@@ -54,16 +66,20 @@ def kspace_filter(x: torch.Tensor, n_dims: int, programs: torch.Tensor, channels
     """y = Re(IFFT(program_b(FFT(x)))) over the trailing ``n_dims`` axes of [B*channels..., *spatial]
     (last axis padded by ``pad`` zero columns); also the per-sample (min, max) order-preserving keys
     (int32 [B, 2]) that salt-and-pepper uses."""
-    progs = _as_prog_lists(unpack_programs(programs))
+    passes = [programs] if programs.dim() == 2 else list(programs)   # [passes, B, REC]: split programs
+    progs = _as_prog_lists(unpack_programs(passes[0]))
     mm = torch.empty((len(progs), 2), dtype=torch.int32, device=x.device)
-    y = rt.kspace_filter(x, n_dims, progs, channels, pad=pad, minmax=mm)
+    y = rt._kspace_filter_pass(x, n_dims, progs, channels, pad=pad, minmax=mm)
+    view = y[..., : x.shape[-1]] if pad else y
+    for p in passes[1:]:
+        rt._kspace_filter_pass(view, n_dims, _as_prog_lists(unpack_programs(p)), channels, out=view, minmax=mm)
     return y, mm
 
 
 @kspace_filter.register_fake
 def _kspace_filter_fake(x, n_dims, programs, channels, pad=0):
     shape = tuple(x.shape[:-1]) + (x.shape[-1] + pad,)
-    return x.new_empty(shape), x.new_empty((programs.shape[0], 2), dtype=torch.int32)
+    return x.new_empty(shape), x.new_empty((programs.shape[-2], 2), dtype=torch.int32)
 
 
 @torch.library.custom_op("texbias::salt_and_pepper_", mutates_args=("x",))

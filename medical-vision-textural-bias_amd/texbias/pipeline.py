@@ -31,17 +31,54 @@ def _kind(t) -> str:
 
 
 KSPACE = {"RandFourierDiskMaskd", "RandPlaneWaves_ellipsoid", "WrapArtifactd", "WrapArtifact", "GibbsNoise",
-          "RandGibbsNoise", "RandGibbsNoised", "KSpaceSpikeNoise"}
+          "RandGibbsNoise", "RandGibbsNoised", "KSpaceSpikeNoise", "RandKSpaceSpikeNoise", "RandKSpaceSpikeNoised"}
 POINTWISE = {"SaltAndPepper"}
+CHANNEL = {"SelectChanneld", "MultimodalSlicesd"}
+
+
+def select_channel_index(t, key: str, keys_present: Sequence[str]) -> Optional[int]:
+    """The channel SelectChanneld (filters_and_operators.py:25-58) keeps for ``key`` given the keys
+    present in the sample, or None when it does not touch ``key``."""
+    order = [k for k in t.keys if k in keys_present]
+    if key not in order:
+        return None
+    cn = t.chan_num
+    if isinstance(cn, Sequence) and not isinstance(cn, (str, bytes)):
+        if len(cn) > 1:
+            i = order.index(key)
+            return int(cn[i]) if i < len(cn) else None
+        return int(cn[0])
+    return int(cn)
+
+
+def spike_program(t, c_cur: int, spatial) -> List:
+    """RandKSpaceSpikeNoise's draws for one [c_cur, *spatial] image (filters_and_operators.py:
+    1047-1103) and the KSpaceSpikeNoise program they call (:906-983)."""
+    import filters_and_operators as F
+    if t.intensity_range is None:
+        raise ValueError("FusedChain needs RandKSpaceSpikeNoise's intensity_range (the default range is data "
+                         "dependent: 2.5 * mean log |k| of the sample)")
+    if isinstance(t.intensity_range[0], Sequence) and len(t.intensity_range) != c_cur:
+        raise AssertionError("If intensity_range is a sequence of sequences, then there must be one (low, high) "
+                             "tuple for each channel.")
+    meta = torch.empty((c_cur,) + tuple(spatial), device="meta")
+    t.sampled_k_intensity = []
+    t.sampled_locs = []
+    t._randomize(meta, t._make_sequence(meta))
+    if not t.sampled_locs:
+        return []
+    return F.KSpaceSpikeNoise(t.sampled_locs, t.sampled_k_intensity).program(meta)
 
 
 class FusedChain:
     """Compile ``transforms`` (instances from filters_and_operators) for batched device execution.
 
     ``__call__(x, pad=0)``: x [B, C, *spatial] float32 on a HIP device (spatial = 3 axes);
-    returns [B, C, *spatial[:-1], spatial[-1] + pad].  The same transform objects draw for every
-    sample in turn, exactly like a per-sample Compose (per-rank streams: seed the transforms per
-    rank with ``set_random_state``).
+    returns [B, C', *spatial[:-1], spatial[-1] + pad] (C' = 1 after a channel selection).  The
+    same transform objects draw for every sample in turn, exactly like a per-sample Compose
+    (per-rank streams: seed the transforms per rank with ``set_random_state``).  ``apply(data)``
+    takes a collated dict ({"image", "label"}) and also applies the channel selections to the
+    label (``SelectChanneld`` / ``MultimodalSlicesd``).
 
     Parity hooks (the reference's draws that a device run cannot reproduce):
     ``phases`` -- per sample, the per-channel phase of the plane-wave spike coefficient as the
@@ -53,13 +90,14 @@ class FusedChain:
 
     def __init__(self, transforms: Sequence, key: str = "image"):
         for t in transforms:
-            if _kind(t) not in KSPACE | POINTWISE:
+            if _kind(t) not in KSPACE | POINTWISE | CHANNEL:
                 raise TypeError(f"{_kind(t)} is not a fusable texbias transform")
         self.transforms = list(transforms)
         self.key = key
         self._mm: Optional[torch.Tensor] = None
         self._mm_b = 0
         self._last_mm: Optional[torch.Tensor] = None
+        self._label_sel: List[Optional[int]] = []
 
     @property
     def last_minmax(self) -> Optional[np.ndarray]:
@@ -68,11 +106,22 @@ class FusedChain:
         return rt.keys_to_float(self._last_mm) if self._mm_b else None
 
     # --- host side: one sample's draws, in Compose order --------------------------------
-    def _sample_plan(self, spatial, phase: Optional[Sequence[float]] = None) -> List:
-        """Returns a list of stages: ('k', program) or ('sap', p) for one sample."""
+    def _sample_plan(self, spatial, channels: int = 4, phase: Optional[Sequence[float]] = None,
+                     keys_present: Sequence[str] = ("image",)) -> List:
+        """Returns a list of stages for one sample: ('k', program), ('sap', p or None) or
+        ('sel', channel); records the label channel a selection keeps in ``self._label_sel``."""
         stages: List = []
         prog: List = []
         seg = False   # the current segment holds a k-space transform (structure, not draws)
+        c_cur = channels
+        lsel: Optional[int] = None
+
+        def close():
+            nonlocal prog, seg
+            if seg:
+                stages.append(("k", prog))
+            prog, seg = [], False
+
         for t in self.transforms:
             k = _kind(t)
             seg = seg or k in KSPACE
@@ -100,21 +149,50 @@ class FusedChain:
             elif k == "KSpaceSpikeNoise":
                 if t.k_intensity is None:
                     raise ValueError("FusedChain needs explicit k_intensity (the default is data dependent)")
-                prog += t.program(torch.empty((1,) + tuple(spatial), device="meta"))
+                prog += t.program(torch.empty((c_cur,) + tuple(spatial), device="meta"))
+            elif k == "RandKSpaceSpikeNoise":
+                prog += spike_program(t, c_cur, spatial)
+            elif k == "RandKSpaceSpikeNoised":
+                t.randomize(None)                   # the global probability (:1218)
+                if t.common_sampling:
+                    for kk in t.keys:
+                        t.transforms[kk].set_random_state(t.common_seed)
+                if self.key in t.keys and t._do_transform:
+                    prog += spike_program(t.transforms[self.key], c_cur, spatial)
             elif k == "SaltAndPepper":
                 t.randomize(None)
-                if seg:
-                    stages.append(("k", prog))
-                    prog, seg = [], False
+                close()
                 stages.append(("sap", t.p if t._do_transform else None))
-        if seg:
-            stages.append(("k", prog))
+            elif k == "SelectChanneld":
+                close()
+                c = select_channel_index(t, self.key, keys_present)
+                if c is not None:
+                    if not 0 <= c < c_cur:
+                        raise AssertionError(f"Provided channel index {c} larger than max channel index for key = "
+                                             f"{self.key}")
+                    stages.append(("sel", c))
+                    c_cur = 1
+                if "label" in keys_present:
+                    lsel = select_channel_index(t, "label", keys_present)
+            elif k == "MultimodalSlicesd":
+                close()
+                c = int(t.R.choice(t.img_chan_indices))   # one draw per call (…3modalities.py:99)
+                if self.key in t.keys:
+                    stages.append(("sel", c))
+                    c_cur = 1
+                if "label" in t.keys and "label" in keys_present:
+                    lsel = int(t.label_idx)
+        close()
+        self._label_sel.append(lsel)
         return stages
 
-    def plan(self, B: int, spatial, phases: Optional[Sequence[Sequence[float]]] = None) -> List[List]:
+    def plan(self, B: int, spatial, phases: Optional[Sequence[Sequence[float]]] = None, channels: int = 4,
+             keys_present: Sequence[str] = ("image",)) -> List[List]:
         if phases is not None and len(phases) != B:
             raise ValueError("one phase list per sample")
-        return [self._sample_plan(spatial, None if phases is None else phases[b]) for b in range(B)]
+        self._label_sel = []
+        return [self._sample_plan(spatial, channels, None if phases is None else phases[b], keys_present)
+                for b in range(B)]
 
     # --- device side --------------------------------------------------------------------
     def __call__(self, x: torch.Tensor, pad: int = 0, plans: Optional[List[List]] = None,
@@ -127,11 +205,36 @@ class FusedChain:
         if x.dim() != 5:
             raise ValueError("FusedChain expects [B, C, H, W, D]")
         B, C = x.shape[:2]
+        plans = plans if plans is not None else self.plan(B, tuple(x.shape[2:]), phases, C)
+        return self.execute(x, plans, pad=pad, u=u, cls=cls, seed=seed)
+
+    def apply(self, data: dict, pad: int = 0, **kw) -> dict:
+        """Dictionary form: ``data[self.key]`` through the chain; a "label" entry gets the channel
+        selections (SelectChanneld / MultimodalSlicesd) the draws made for it."""
+        d = dict(data)
+        x = d[self.key]
+        keys = [k for k in d]
+        plans = self.plan(x.shape[0], tuple(x.shape[2:]), kw.pop("phases", None), x.shape[1], keys)
+        d[self.key] = self.__call__(x, pad=pad, plans=plans, **kw)
+        if "label" in d and any(s is not None for s in self._label_sel):
+            lab = d["label"]
+            idx = torch.tensor([s if s is not None else 0 for s in self._label_sel], device=lab.device)
+            d["label"] = lab[torch.arange(lab.shape[0], device=lab.device), idx][:, None]
+        return d
+
+    def execute(self, x: torch.Tensor, plans: List[List], pad: int = 0, u: Optional[torch.Tensor] = None,
+                cls: Optional[torch.Tensor] = None, seed: Optional[int] = None) -> torch.Tensor:
+        """Run per-sample stage lists (``plan`` or deferred plans) over the batch x [B, C, *spatial]."""
+        rt.require_hip(x, "FusedChain")
+        if x.dim() != 5:
+            raise ValueError("FusedChain expects [B, C, H, W, D]")
+        B = x.shape[0]
         spatial = tuple(x.shape[2:])
         for t, nm in ((u, "u"), (cls, "cls")):
             if t is not None and tuple(t.shape) != tuple(x.shape):
                 raise ValueError(f"{nm} must have the input's shape {tuple(x.shape)}")
-        plans = plans if plans is not None else self.plan(B, spatial, phases)
+        if len(plans) != B:
+            raise ValueError(f"{len(plans)} plans for a batch of {B}")
         nst = len(plans[0])
         if any(len(p) != nst or [s[0] for s in p] != [s[0] for s in plans[0]] for p in plans):
             raise ValueError("all samples of a batch must share the stage structure")
@@ -145,6 +248,7 @@ class FusedChain:
         mm_valid = False
         for si in range(nst):
             kind = plans[0][si][0]
+            C = cur.shape[1]
             if kind == "k":
                 progs = [p[si][1] for p in plans]
                 if not any(progs):
@@ -154,11 +258,21 @@ class FusedChain:
                     view = cur[..., : spatial[-1]]
                     rt.kspace_filter(view, 3, progs, C, out=view, minmax=mm)
                 else:   # the functional custom op (torch.compile / graph-capture friendly)
-                    cur, mm = torch.ops.texbias.kspace_filter(cur, 3, tbops.pack_programs(progs), C, out_pad)
+                    cur, mm = torch.ops.texbias.kspace_filter(cur, 3, tbops.pack_programs_split(progs, K.geometry(spatial).hwd), C,
+                                                              out_pad)
                     padded = out_pad > 0
                 mm_valid = True
+            elif kind == "sel":
+                chans = [int(p[si][1]) for p in plans]
+                cur = cur[torch.arange(B, device=cur.device), torch.tensor(chans, device=cur.device)][:, None]
+                if u is not None:
+                    u = u[torch.arange(B, device=u.device), torch.tensor(chans, device=u.device)][:, None]
+                if cls is not None:
+                    raise ValueError("the cls hook is not supported across a channel selection")
+                mm_valid = False   # the per-sample min/max was over the unselected channels
             else:
                 ps = [p[si][1] for p in plans]
+                seeds = [p[si][2] if len(p[si]) > 2 else None for p in plans]
                 if all(v is None for v in ps):
                     continue
                 if cur is x:
@@ -168,7 +282,14 @@ class FusedChain:
                 if not mm_valid:
                     rt.minmax_keys(view, 4, out=mm)
                 thr = [((np.float32(p / 2), np.float32(p)) if p is not None else (-1.0, -1.0)) for p in ps]
-                if u is None and cls is None:
+                if any(sd is not None for sd in seeds):
+                    # deferred samples: each its own Philox key, drawn in its worker (the eager stream)
+                    for b in range(B):
+                        if ps[b] is not None:
+                            torch.ops.texbias.salt_and_pepper_(view[b:b + 1], mm[b:b + 1],
+                                                               torch.tensor([thr[b]], dtype=torch.float32),
+                                                               int(seeds[b]), 0, 4)
+                elif u is None and cls is None:
                     sd = seed if seed is not None else int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
                     torch.ops.texbias.salt_and_pepper_(view, mm, torch.tensor(thr, dtype=torch.float32), sd, 0, 4)
                 else:

@@ -14,9 +14,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._abi import TB_MAX_BATCH, programs_array
+from ._abi import TB_MAX_BATCH, TB_MAX_OPS, programs_array
 from ._lib import TexbiasError, check, lib
-from .kprog import Geometry, geometry
+from .kprog import Geometry, geometry, split_program
 
 _plans: Dict[Tuple[int, int, int, int], "Plan"] = {}
 _ws: Dict[int, torch.Tensor] = {}
@@ -140,9 +140,28 @@ def kspace_filter(x: torch.Tensor, n_dims: int, programs: Sequence[Sequence], ch
     ``x``: [*lead, *spatial] float32 on a HIP device, lead = (B, C) flattened to B*C with
     ``channels`` = C; ``programs``: B lists of TbOp.  ``pad`` appends zero columns to the
     last axis of the output (U-Net padding).  ``minmax``: optional int32 [B, 2] device
-    tensor receiving the per-sample (min, max) keys of the output.
+    tensor receiving the per-sample (min, max) keys of the output.  Programs longer than one
+    launch holds (TB_MAX_OPS) run as several passes cut where that is exact
+    (``kprog.split_program``); the later passes filter the output in place.
     """
     require_hip(x, "kspace_filter")
+    if all(len(p) <= TB_MAX_OPS for p in programs):
+        return _kspace_filter_pass(x, n_dims, programs, channels, out, pad, minmax)
+    hwd = geometry(x.shape[x.dim() - n_dims:]).hwd
+    parts = [split_program(list(p), hwd) for p in programs]
+    npass = max(len(c) for c in parts)
+    passes = [[c[i] if i < len(c) else [] for c in parts] for i in range(npass)]
+    y = _kspace_filter_pass(x, n_dims, passes[0], channels, out, pad, minmax)
+    view = y[..., : x.shape[-1]] if pad else y
+    for prog in passes[1:]:
+        _kspace_filter_pass(view, n_dims, prog, channels, view, 0, minmax)
+    return y
+
+
+def _kspace_filter_pass(x: torch.Tensor, n_dims: int, programs: Sequence[Sequence], channels: int,
+                        out: Optional[torch.Tensor] = None, pad: int = 0,
+                        minmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One launch group of ``kspace_filter`` (every program at most TB_MAX_OPS ops)."""
     geo = geometry(x.shape[x.dim() - n_dims:])
     H, W, D = geo.hwd
     v = _bc_view(x, n_dims)
