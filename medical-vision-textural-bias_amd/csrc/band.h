@@ -92,7 +92,7 @@ struct BandFwdArgs {
 
 struct BandMidArgs {
   tb_plan_dev pl;
-  const cf* P;
+  cf* P;            // pass A' partial sums; pass B' writes Z over each slab's first slot
   float4* AB;       // [bc][KH + 1][ncol]: (Q'(kh) + Q'(-kh), Q'(kh) - Q'(-kh))
   cf* pts;          // [bc][BAND_MAX_PTS]
   float* M2F;       // [bc][H][VT][KV][64]: pass C''s V-product A fragments (written by B2')
@@ -189,6 +189,13 @@ TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W) {
   c.pkw = band_al16(c.frag + BAND_SLOTS16 * band_vt(g) * band_kv(g) * 64 * 4);
   c.total = band_al16(c.pkw + BAND_SLOTS16 * BAND_MAX_PTS * 4);
   return c;
+}
+
+// Pass B' (k_band_hcol): BAND_HC_CB box columns per workgroup; LDS = their (A, B) rows, the
+// columns' partial sums for every slab, the H twiddles.
+constexpr int BAND_HC_CB = 16;
+TB_HD size_t band_hc_lds(int H, int KH) {
+  return (size_t)H * BAND_HC_CB * 8 + (size_t)H * 8 + (size_t)(KH + 1) * BAND_HC_CB * 16;
 }
 
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels

@@ -354,108 +354,102 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
 }
 
 // ----------------------------------------------------------------------------- pass B'
-constexpr int BAND_MID_MAXH = 1024;  // slabs per bc whose twiddles / partial counts pass B' tabulates in LDS
-constexpr int BAND_MID_KG = 4;       // kh per pass-B' workgroup
-constexpr int BAND_MID_NW = 8;       // waves per pass-B' workgroup (they split h)
-constexpr int BAND_MID_NT = 64 * BAND_MID_NW;
-
-// One workgroup per (bc, 64 box columns, BAND_MID_KG consecutive kh): the slabs' pass-A' partials
-// are read once per kh group, the four waves split h, each lane holds Q(kh) of its column for the
-// group: Ac(kh) = sum_h P_h cos(2 pi kh h / H), As(kh) = sum_h P_h sin(..).  Then the waves' sums
-// meet in LDS and wave w finishes kh = kh0 + w: the sample's op program on Q(kh) and Q(-kh),
-// stored as their sum and difference AB[bc][kh][col].
-__global__ __launch_bounds__(BAND_MID_NT) void k_band_mid(BandMidArgs) {
+// One workgroup per (bc, BAND_HC_CB box columns): the slabs' pass-A' partial sums of the block
+// (segments added) are staged in LDS once, then
+//   forward  Q(kh) = sum_h P_h e^{-2 pi i kh h / H} for kh in [-KH, KH]   (threads: (kh, column))
+//   program  the sample's op program (apply_ops, the code of pass B) on Q(kh) and Q(-kh), kept as
+//            A = Q'(kh) + Q'(-kh), B = Q'(kh) - Q'(-kh)
+//   inverse  Z_h = A_0 + sum_{kh >= 1} (A cos + i B sin), theta = 2 pi kh h / H (threads: (h, column))
+// and Z is written over the block's first partial-sum slot (the block's own columns only; every
+// read of them happened before, in this workgroup).  Each partial sum is read once; pass B2' then
+// needs only the slab's Z row.
+__global__ __launch_bounds__(BAND_NT) void k_band_hcol(BandMidArgs) {
   const BandMidArgs& a = kargs<BandMidArgs>();
-  constexpr int KG = BAND_MID_KG, NW = BAND_MID_NW;
-  __shared__ float4 red[NW][KG][64];
-  __shared__ float2 twl[BAND_MID_MAXH];         // (cos, -sin)(2 pi t / H)
-  __shared__ unsigned char nsg[BAND_MID_MAXH];  // pass-A' partials per slab
-  const int tid = (int)threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = (int)threadIdx.x;
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
   const int NDk = a.g.NDk, KW = a.g.KW, KH = a.g.KH, ncol = a.g.ncol;
-  const int kh0 = (int)blockIdx.y * KG, bcl = (int)blockIdx.z, bc = a.bc0 + bcl;
-  const int col = (int)blockIdx.x * 64 + lane;
-  const bool live = col < ncol;
-  const cf* Pc = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol + (live ? col : 0);
-  const bool tab = H <= BAND_MID_MAXH;
-  if (tab)
-    for (int hh = tid; hh < H; hh += BAND_MID_NT) {
-      twl[hh] = ld2(a.pl.tw[0] + hh);
-      nsg[hh] = (unsigned char)fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
-    }
-  __syncthreads();
-  float4 acc[KG];  // (Ac.re, Ac.im, As.re, As.im) of kh0 + k
+  const int bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int c0 = (int)blockIdx.x * BAND_HC_CB;
+  float4* ABs = reinterpret_cast<float4*>(smem);                                  // [KH + 1][CB] (A, B)
+  float2* Pb = reinterpret_cast<float2*>(smem + (size_t)(KH + 1) * BAND_HC_CB * 16);  // [H][CB]
+  float2* tw = Pb + (size_t)H * BAND_HC_CB;                                       // (cos, -sin)(2 pi t / H)
+  cf* P = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol;
+  for (int hh = tid; hh < H; hh += BAND_NT) tw[hh] = ld2(a.pl.tw[0] + hh);
+  for (int e = tid; e < H * BAND_HC_CB; e += 4 * BAND_NT) {  // 4 slabs' loads in flight per thread
+    float2 v[4][3];
+    int nseg[4];
 #pragma unroll
-  for (int k = 0; k < KG; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int U = 6;  // slabs whose loads are in flight together (3 partials each)
-  for (int h0 = wv; h0 < H; h0 += NW * U) {
-    float2 p[U];
+    for (int u = 0; u < 4; ++u) {
+      const int ee = e + u * BAND_NT, hh = ee / BAND_HC_CB, col = c0 + (ee - hh * BAND_HC_CB);
+      const bool ok = ee < H * BAND_HC_CB && col < ncol;
+      nseg[u] = ok ? fwd_nseg(a.split, (uint32_t)(bcl * H + hh)) : 0;
+      const cf* ph = P + (int64_t)(ok ? hh : 0) * BAND_FWD_SEGS * ncol + (ok ? col : 0);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int hh = h0 + NW * u < H ? h0 + NW * u : H - 1;
-      const int nseg = tab ? (int)nsg[hh] : fwd_nseg(a.split, (uint32_t)(bcl * H + hh));
-      const cf* ph = Pc + (int64_t)hh * BAND_FWD_SEGS * ncol;
-      // only the slab's live partial slots are read (nseg is wave-uniform: no divergence)
-      const float2 p0 = ld2(ph);
-      const float2 p1 = nseg > 1 ? ld2(ph + ncol) : make_float2(0.f, 0.f);
-      const float2 p2 = nseg > 2 ? ld2(ph + 2 * ncol) : make_float2(0.f, 0.f);
-      p[u].x = p0.x + p1.x + p2.x;
-      p[u].y = p0.y + p1.y + p2.y;
-      if (h0 + NW * u >= H) p[u] = make_float2(0.f, 0.f);
+      for (int sg = 0; sg < 3; ++sg) v[u][sg] = sg < nseg[u] ? ld2(ph + sg * ncol) : make_float2(0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int hh = h0 + NW * u < H ? h0 + NW * u : 0;
-      int t = (int)(((int64_t)kh0 * hh) % H);
-#pragma unroll
-      for (int k = 0; k < KG; ++k) {  // slots past KH accumulate too (never stored): no branches
-        const float2 tw = tab ? twl[t] : ld2(a.pl.tw[0] + t);  // (cos, -sin)(2 pi (kh0 + k) hh / H)
-        acc[k].x = fmaf(p[u].x, tw.x, acc[k].x);
-        acc[k].y = fmaf(p[u].y, tw.x, acc[k].y);
-        acc[k].z = fmaf(p[u].x, -tw.y, acc[k].z);
-        acc[k].w = fmaf(p[u].y, -tw.y, acc[k].w);
-        t += hh;
-        t = t >= H ? t - H : t;
-      }
+    for (int u = 0; u < 4; ++u) {
+      const int ee = e + u * BAND_NT;
+      if (ee < H * BAND_HC_CB) Pb[ee] = make_float2(v[u][0].x + v[u][1].x + v[u][2].x, v[u][0].y + v[u][1].y + v[u][2].y);
     }
   }
-#pragma unroll
-  for (int k = 0; k < KG; ++k) red[wv][k][lane] = acc[k];
   __syncthreads();
   const int lb = a.cofs + bcl, s = lb / a.C, chan = lb - s * a.C;
   const tb_sample_ops& so = a.ops.s[s];
-  if (live) {
-    const int jw = col / NDk, kd = col - jw * NDk;
-    const int kw = (jw - KW + W) % W;
-    const FreqCol fc = freq_col(kw, kd, W, D);
-    for (int k = wv; k < KG && kh0 + k <= KH; k += NW) {
-      const int kh = kh0 + k;
-      float4 q = red[0][k][lane];
-      for (int w_ = 1; w_ < NW; ++w_) {
-        const float4 r = red[w_][k][lane];
-        q.x += r.x; q.y += r.y; q.z += r.z; q.w += r.w;
+  for (int it = tid; it < (KH + 1) * BAND_HC_CB; it += BAND_NT) {
+    const int kh = it / BAND_HC_CB, c = it - kh * BAND_HC_CB, col = c0 + c;
+    float4 ab = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < ncol) {
+      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);  // (Ac.re, Ac.im, As.re, As.im)
+      int t = 0;
+      for (int hh = 0; hh < H; ++hh) {
+        const float2 p = Pb[hh * BAND_HC_CB + c], w = tw[t];
+        q.x = fmaf(p.x, w.x, q.x);
+        q.y = fmaf(p.y, w.x, q.y);
+        q.z = fmaf(p.x, -w.y, q.z);
+        q.w = fmaf(p.y, -w.y, q.w);
+        t += kh;
+        t = t >= H ? t - H : t;
       }
-      cf qp = apply_ops(so, chan, mk(q.x + q.w, q.y - q.z), fc, kh, H);
-      float4 o;
+      const int jw = col / NDk, kd = col - jw * NDk;
+      const FreqCol fc = freq_col((jw - KW + W) % W, kd, W, D);
+      const cf qp = apply_ops(so, chan, mk(q.x + q.w, q.y - q.z), fc, kh, H);
       if (kh == 0) {
-        o = make_float4(qp.x, qp.y, 0.f, 0.f);
+        ab = make_float4(qp.x, qp.y, 0.f, 0.f);
       } else {
         const cf qm = apply_ops(so, chan, mk(q.x - q.w, q.y + q.z), fc, H - kh, H);
-        o = make_float4(qp.x + qm.x, qp.y + qm.y, qp.x - qm.x, qp.y - qm.y);
+        ab = make_float4(qp.x + qm.x, qp.y + qm.y, qp.x - qm.x, qp.y - qm.y);
       }
-      a.AB[((int64_t)bc * (KH + 1) + kh) * ncol + col] = o;
     }
+    ABs[it] = ab;
+  }
+  __syncthreads();
+  for (int e = tid; e < H * BAND_HC_CB; e += BAND_NT) {
+    const int hh = e / BAND_HC_CB, c = e - hh * BAND_HC_CB, col = c0 + c;
+    if (col >= ncol) continue;
+    const float4 a0 = ABs[c];
+    float zx = a0.x, zy = a0.y;
+    int t = 0;
+    for (int kh = 1; kh <= KH; ++kh) {
+      t += hh;
+      t = t >= H ? t - H : t;
+      const float2 w = tw[t];  // (cos, -sin)
+      const float4 ab = ABs[kh * BAND_HC_CB + c];
+      zx = fmaf(ab.x, w.x, fmaf(ab.w, w.y, zx));   // A.re cos - B.im sin
+      zy = fmaf(ab.y, w.x, fmaf(-ab.z, w.y, zy));  // A.im cos + B.re sin
+    }
+    P[(int64_t)hh * BAND_FWD_SEGS * ncol + col] = mk(zx, zy);
   }
   // the out-of-box spike points: the program applied to a coefficient the low-pass zeroed
-  if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0 && lane < BAND_MAX_PTS) {
+  if (blockIdx.x == 0 && tid < BAND_MAX_PTS) {
     const BandSamplePts& sp = a.sp[s];
     cf c = mk(0.f, 0.f);
-    if (lane < sp.n) {
-      const BandPt p = sp.p[lane];
+    if (tid < sp.n) {
+      const BandPt p = sp.p[tid];
       c = apply_ops(so, chan, mk(0.f, 0.f), freq_col(p.kw, p.kd, W, D), p.kh, H);
     }
-    a.pts[(int64_t)bc * BAND_MAX_PTS + lane] = c;
+    a.pts[(int64_t)bc * BAND_MAX_PTS + tid] = c;
   }
 }
 
@@ -481,28 +475,9 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
   if (u >= H * a.nbc) return;
   const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
   const int s = (a.cofs + bcl) / a.C;
-  const float4* ABb = a.AB + (int64_t)bc * (KH + 1) * ncol;
-  for (int col = lane; col < ncol; col += 64) {
-    const float4 a0 = ABb[col];
-    float zx = a0.x, zy = a0.y;
-    int t = 0;
-    for (int k0 = 1; k0 <= KH; k0 += 4) {
-      float4 ab[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (k0 + q <= KH) ab[q] = ABb[(int64_t)(k0 + q) * ncol + col];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (k0 + q > KH) break;
-        t += h;
-        t = t >= H ? t - H : t;
-        const cf tw = a.pl.tw[0][t];  // (cos, -sin), wave-uniform
-        zx = fmaf(ab[q].x, tw.x, fmaf(ab[q].w, tw.y, zx));   // - B.y sin
-        zy = fmaf(ab[q].y, tw.x, fmaf(-ab[q].z, tw.y, zy));  // + B.x sin
-      }
-    }
-    zs[wv][col] = make_float2(zx, zy);
-  }
+  (void)KH;
+  const cf* Zr = a.P + ((int64_t)bc * H + h) * BAND_FWD_SEGS * ncol;  // Z_h (pass B', first slot)
+  for (int col = lane; col < ncol; col += 64) zs[wv][col] = ld2(Zr + col);
   const BandSamplePts& sp = a.sp[s];
   if (lane < BAND_MAX_PTS) {
     float2 v = make_float2(0.f, 0.f);
@@ -1299,9 +1274,10 @@ hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
 }
 
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
-  const dim3 grid((a.g.ncol + 63) / 64, (a.g.KH + BAND_MID_KG) / BAND_MID_KG, a.nbc);
-  hipLaunchKernelGGL(k_band_mid, grid, dim3(BAND_MID_NT), 0, st, a);
-  hipError_t e;
+  const size_t lds = band_hc_lds(a.pl.H, a.g.KH);
+  hipError_t e = allow_lds(k_band_hcol, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_band_hcol, dim3((a.g.ncol + BAND_HC_CB - 1) / BAND_HC_CB, a.nbc), dim3(BAND_NT), lds, st, a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4), dim3(BAND_NT), 0, st, a);

@@ -620,7 +620,7 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   g.PT = g.cat ? ptot : 0;
   g.NTD = (D + y_pad + 31) / 32;
   if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || KW >= 32 || KH > BAND_MAX_KH) return false;
-  if (g.ncol > BAND_MAX_ZCOL || W > 1024) return false;
+  if (g.ncol > BAND_MAX_ZCOL || W > 1024 || band_hc_lds(H, KH) > 160000) return false;
   if (2 * g.KS > 64 || g.KS > 32) return false;  // pass C' holds V in at most two 32-row MFMA tiles
   // worth it only when the box is a small part of the half spectrum
   if ((double)(2 * KH + 1) * g.ncol * 4.0 > (double)H * W * (D / 2 + 1)) return false;
@@ -707,7 +707,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     split = fa.split;
   }
   {
-    Timer t(1, st, pbytes + abytes, "k_band_mid");
+    Timer t(1, st, pbytes + abytes, "k_band_hcol");
     BandMidArgs ma;
     std::memset(&ma, 0, sizeof(ma));
     ma.pl = p->dev;

@@ -189,7 +189,7 @@ def test_band_c3_kernels_and_bytes(rt):
     rt.kspace_filter(x, 3, [prog, prog], 4, pad=5)
     ms, cnt, nbytes, names = rt.pass_stats()
     rt.set_pass_timing(False)
-    assert names[:3] == ["k_band_fwd", "k_band_mid", "k_band_inv16"]
+    assert names[:3] == ["k_band_fwd", "k_band_hcol", "k_band_inv16"]
     img = 8 * 240 * 240 * 155 * 4
     assert img < nbytes[0] < 1.05 * img
     assert 8 * 240 * 240 * 160 * 4 < nbytes[2] < 1.05 * 8 * 240 * 240 * 160 * 4
