@@ -102,6 +102,7 @@ struct BandMidArgs {
   FwdSplit split;   // pass A''s strip division (how many partial sums each slab has)
   BandSamplePts sp[TB_MAX_BATCH];
   int p0[TB_MAX_BATCH];  // g.cat: the first V point row (pair) of each sample of the launch
+  int16_t pkd[TB_MAX_BATCH * BAND_MAX_PTS];  // g.cat: kd of the launch's points in row order
   void* T16;        // g.cat: synthesis-table fragments for pass C' (written by k_band_tab16)
   const float* tds; // g.cat: [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   BatchOps ops;
@@ -191,11 +192,12 @@ TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W) {
   return c;
 }
 
-// Pass B' (k_band_hcol): BAND_HC_CB box columns per workgroup; LDS = their (A, B) rows, the
-// columns' partial sums for every slab, the H twiddles.
-constexpr int BAND_HC_CB = 16;
+// Pass B' (k_band_hcol): 16 box columns per workgroup; LDS = their partial sums for every slab (+1
+// zero row), the H twiddles, the [C; S] product tiles, the G rows of the inverse.
 TB_HD size_t band_hc_lds(int H, int KH) {
-  return (size_t)H * BAND_HC_CB * 8 + (size_t)H * 8 + (size_t)(KH + 1) * BAND_HC_CB * 16;
+  const int mt = KH + 1 <= 16 ? 1 : 2;
+  return (size_t)(H + 1) * 16 * 8 + (size_t)H * 8 + (size_t)mt * 1024 * 4 + (size_t)2 * (KH + 1) * 32 * 4 +
+         (size_t)4 * mt * 1024 * 4;  // + the 4 waves' forward sums
 }
 
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels

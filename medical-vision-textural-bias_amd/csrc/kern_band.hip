@@ -22,6 +22,9 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// row of register s of a 32x32 MFMA accumulator (lane half 0; +4 for lanes 32-63)
+__device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
+
 __device__ __forceinline__ float2 ld2(const cf* p) {
   const cf v = *p;
   return make_float2(v.x, v.y);
@@ -354,106 +357,185 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
 }
 
 // ----------------------------------------------------------------------------- pass B'
-// One workgroup per (bc, BAND_HC_CB box columns): the slabs' pass-A' partial sums of the block
-// (segments added) are staged in LDS once, then
-//   forward  Q(kh) = sum_h P_h e^{-2 pi i kh h / H} for kh in [-KH, KH]   (threads: (kh, column))
-//   program  the sample's op program (apply_ops, the code of pass B) on Q(kh) and Q(-kh), kept as
-//            A = Q'(kh) + Q'(-kh), B = Q'(kh) - Q'(-kh)
-//   inverse  Z_h = A_0 + sum_{kh >= 1} (A cos + i B sin), theta = 2 pi kh h / H (threads: (h, column))
-// and Z is written over the block's first partial-sum slot (the block's own columns only; every
-// read of them happened before, in this workgroup).  Each partial sum is read once; pass B2' then
-// needs only the slab's Z row.
-__global__ __launch_bounds__(BAND_NT) void k_band_hcol(BandMidArgs) {
+// One workgroup (2 waves) per (bc, 16 box columns); the H transforms are f32 MFMA products
+// (v_mfma_f32_32x32x2f32: exact f32 products and sums):
+//   stage    the columns' pass-A' partial sums for every slab, segments added, into LDS (each
+//            partial sum read once, ~30 loads in flight per lane);
+//   forward  [C; S](kh, h) . [P.re P.im](h, col) over h -- rows 16 kh cosines then their 16 sines
+//            per 32-row tile, columns (col, re/im); the waves take a quarter of h each (operands of
+//            6 steps read from LDS ahead of their MFMAs) and meet in LDS: (Ac.re, Ac.im, As.re,
+//            As.im) = the sums of pass B;
+//   program  the sample's op program (apply_ops, the code of pass B) on Q(kh) = Ac - i As and
+//            Q(-kh) = Ac + i As, kept as G rows (A.re, A.im | -B.im, B.re), A / B = Q'(kh) +/- Q'(-kh);
+//   inverse  Z(h, col) = [cos sin](h, (kh, t)) . G((kh, t), col) per 32-slab tile, the tiles dealt
+//            to the waves, written over the slab's first partial-sum slot (own columns only).
+constexpr int BAND_HC_CB = 16;  // box columns per workgroup
+constexpr int BAND_HC_NW = 4;   // waves per workgroup (they split h)
+template <int MT>               // 32-row tiles of [C; S]: KH + 1 <= 16 MT
+__global__ __launch_bounds__(64 * BAND_HC_NW) void k_band_hcol(BandMidArgs) {
   const BandMidArgs& a = kargs<BandMidArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = (int)threadIdx.x;
+  const int tid = (int)threadIdx.x, lane = tid & 63, hl = lane >> 5, l31 = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, W = a.pl.W, D = a.pl.D;
   const int NDk = a.g.NDk, KW = a.g.KW, KH = a.g.KH, ncol = a.g.ncol;
   const int bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
   const int c0 = (int)blockIdx.x * BAND_HC_CB;
-  float4* ABs = reinterpret_cast<float4*>(smem);                                  // [KH + 1][CB] (A, B)
-  float2* Pb = reinterpret_cast<float2*>(smem + (size_t)(KH + 1) * BAND_HC_CB * 16);  // [H][CB]
-  float2* tw = Pb + (size_t)H * BAND_HC_CB;                                       // (cos, -sin)(2 pi t / H)
+  float2* Pb = reinterpret_cast<float2*>(smem);                     // [H + 1][16] (row H: zeros)
+  float2* tw = Pb + (size_t)(H + 1) * BAND_HC_CB;                   // (cos, -sin)(2 pi t / H)
+  float* Qs = reinterpret_cast<float*>(tw + H);                     // [MT][32][32]
+  float* G = Qs + MT * 1024;                                        // [2 (KH + 1)][32]
   cf* P = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol;
-  for (int hh = tid; hh < H; hh += BAND_NT) tw[hh] = ld2(a.pl.tw[0] + hh);
-  for (int e = tid; e < H * BAND_HC_CB; e += 4 * BAND_NT) {  // 4 slabs' loads in flight per thread
-    float2 v[4][3];
-    int nseg[4];
+  constexpr int NT = 64 * BAND_HC_NW;
+  for (int hh = tid; hh < H; hh += NT) tw[hh] = ld2(a.pl.tw[0] + hh);
+  if (tid < BAND_HC_CB) Pb[H * BAND_HC_CB + tid] = make_float2(0.f, 0.f);
+  {  // stage: lane -> (h offset tid >> 4, column tid & 15); UR slab rows x 3 slots in flight
+    const int c = tid & 15, col = c0 + c;
+    const bool ok = col < ncol;
+    constexpr int UR = 8, RS = NT / 16;
+    for (int hb = tid >> 4; hb < H; hb += RS * UR) {
+      float2 v[UR][3];
+      int ns[UR];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ee = e + u * BAND_NT, hh = ee / BAND_HC_CB, col = c0 + (ee - hh * BAND_HC_CB);
-      const bool ok = ee < H * BAND_HC_CB && col < ncol;
-      nseg[u] = ok ? fwd_nseg(a.split, (uint32_t)(bcl * H + hh)) : 0;
-      const cf* ph = P + (int64_t)(ok ? hh : 0) * BAND_FWD_SEGS * ncol + (ok ? col : 0);
+      for (int u = 0; u < UR; ++u) {
+        const int hh = hb + RS * u < H ? hb + RS * u : H - 1;
+        ns[u] = (ok && hb + RS * u < H) ? fwd_nseg(a.split, (uint32_t)(bcl * H + hh)) : 0;
+        const cf* ph = P + (int64_t)hh * BAND_FWD_SEGS * ncol + (ok ? col : 0);
 #pragma unroll
-      for (int sg = 0; sg < 3; ++sg) v[u][sg] = sg < nseg[u] ? ld2(ph + sg * ncol) : make_float2(0.f, 0.f);
+        for (int sg = 0; sg < 3; ++sg) v[u][sg] = ld2(ph + sg * ncol);
+      }
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        if (hb + RS * u >= H) break;
+        float2 z = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int sg = 0; sg < 3; ++sg) {
+          z.x += sg < ns[u] ? v[u][sg].x : 0.f;
+          z.y += sg < ns[u] ? v[u][sg].y : 0.f;
+        }
+        Pb[(hb + RS * u) * BAND_HC_CB + c] = z;
+      }
     }
+  }
+  __syncthreads();
+  // forward: this wave's quarter of the h pairs, 6 steps' operands read ahead of their MFMAs
+  f32x16 acc[MT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ee = e + u * BAND_NT;
-      if (ee < H * BAND_HC_CB) Pb[ee] = make_float2(v[u][0].x + v[u][1].x + v[u][2].x, v[u][0].y + v[u][1].y + v[u][2].y);
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[mt][j] = 0.f;
+  {
+    const int nst = (H + 1) / 2, sh = (nst + BAND_HC_NW - 1) / BAND_HC_NW;
+    const int s0 = wv * sh, s1 = s0 + sh < nst ? s0 + sh : nst;
+    const int bcol = l31 >> 1, bcomp = l31 & 1;
+    int tA[MT], dA[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int kh = 16 * mt + (l31 & 15);
+      tA[mt] = (int)(((int64_t)kh * (2 * s0 + hl)) % H);
+      dA[mt] = (2 * kh) % H;
     }
+    constexpr int US = 6;
+    for (int st = s0; st < s1; st += US) {
+      float bv[US], av[US][MT];
+#pragma unroll
+      for (int u = 0; u < US; ++u) {
+        const int h = 2 * (st + u) + hl;  // past this wave's steps / h == H: the zero row
+        const float2 pv = Pb[(st + u < s1 && h < H ? h : H) * BAND_HC_CB + bcol];
+        bv[u] = bcomp ? pv.y : pv.x;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const float2 w = tw[tA[mt]];
+          av[u][mt] = (l31 < 16) ? w.x : -w.y;  // cos rows, then sin rows
+          tA[mt] += dA[mt];
+          tA[mt] = tA[mt] >= H ? tA[mt] - H : tA[mt];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < US; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][mt], bv[u], acc[mt], 0, 0, 0);
+    }
+  }
+  // the waves' sums meet in LDS: [wave][MT 32 x 32], then summed per element
+  float* red = G + 2 * (KH + 1) * 32;  // [NW][MT][32][32]
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[((wv * MT + mt) * 32 + acc_row(r) + 4 * hl) * 32 + l31] = acc[mt][r];
+  __syncthreads();
+  for (int e = tid; e < MT * 1024; e += NT) {
+    float q = red[e];
+#pragma unroll
+    for (int w_ = 1; w_ < BAND_HC_NW; ++w_) q += red[w_ * MT * 1024 + e];
+    Qs[e] = q;
   }
   __syncthreads();
   const int lb = a.cofs + bcl, s = lb / a.C, chan = lb - s * a.C;
   const tb_sample_ops& so = a.ops.s[s];
-  for (int it = tid; it < (KH + 1) * BAND_HC_CB; it += BAND_NT) {
-    const int kh = it / BAND_HC_CB, c = it - kh * BAND_HC_CB, col = c0 + c;
+  for (int it = tid; it < (KH + 1) * BAND_HC_CB; it += NT) {  // the op program, once per (kh, column)
+    const int k = it / BAND_HC_CB, c = it - k * BAND_HC_CB, cl = c0 + c;
+    const float* q = Qs + (k >> 4) * 1024 + (k & 15) * 32 + 2 * c;  // C rows; S rows 16 below
+    const float acr = q[0], aci = q[1], asr = q[512], asi = q[513];
     float4 ab = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < ncol) {
-      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);  // (Ac.re, Ac.im, As.re, As.im)
-      int t = 0;
-      for (int hh = 0; hh < H; ++hh) {
-        const float2 p = Pb[hh * BAND_HC_CB + c], w = tw[t];
-        q.x = fmaf(p.x, w.x, q.x);
-        q.y = fmaf(p.y, w.x, q.y);
-        q.z = fmaf(p.x, -w.y, q.z);
-        q.w = fmaf(p.y, -w.y, q.w);
-        t += kh;
-        t = t >= H ? t - H : t;
-      }
-      const int jw = col / NDk, kd = col - jw * NDk;
+    if (cl < ncol) {
+      const int jw = cl / NDk, kd = cl - jw * NDk;
       const FreqCol fc = freq_col((jw - KW + W) % W, kd, W, D);
-      const cf qp = apply_ops(so, chan, mk(q.x + q.w, q.y - q.z), fc, kh, H);
-      if (kh == 0) {
-        ab = make_float4(qp.x, qp.y, 0.f, 0.f);
-      } else {
-        const cf qm = apply_ops(so, chan, mk(q.x - q.w, q.y + q.z), fc, H - kh, H);
-        ab = make_float4(qp.x + qm.x, qp.y + qm.y, qp.x - qm.x, qp.y - qm.y);
-      }
+      const cf qp = apply_ops(so, chan, mk(acr + asi, aci - asr), fc, k, H);
+      const cf qm = k == 0 ? mk(0.f, 0.f) : apply_ops(so, chan, mk(acr - asi, aci + asr), fc, H - k, H);
+      ab = k == 0 ? make_float4(qp.x, qp.y, 0.f, 0.f) : make_float4(qp.x + qm.x, qp.y + qm.y, qp.x - qm.x, qp.y - qm.y);
     }
-    ABs[it] = ab;
+    G[(2 * k) * 32 + 2 * c] = ab.x;           // cos row: (A.re, A.im)
+    G[(2 * k) * 32 + 2 * c + 1] = ab.y;
+    G[(2 * k + 1) * 32 + 2 * c] = -ab.w;      // sin row: (-B.im, B.re)
+    G[(2 * k + 1) * 32 + 2 * c + 1] = ab.z;
   }
   __syncthreads();
-  for (int e = tid; e < H * BAND_HC_CB; e += BAND_NT) {
-    const int hh = e / BAND_HC_CB, c = e - hh * BAND_HC_CB, col = c0 + c;
-    if (col >= ncol) continue;
-    const float4 a0 = ABs[c];
-    float zx = a0.x, zy = a0.y;
+  // inverse: 32-slab tiles dealt to the waves, 4 steps' operands read ahead of their MFMAs
+  float* Pf = reinterpret_cast<float*>(P);
+  const int col = c0 + (l31 >> 1);
+  for (int ht = wv; ht * 32 < H; ht += BAND_HC_NW) {
+    f32x16 z;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) z[j] = 0.f;
+    const int h = 32 * ht + l31;
+    const int hm = h < H ? h : 0;
     int t = 0;
-    for (int kh = 1; kh <= KH; ++kh) {
-      t += hh;
-      t = t >= H ? t - H : t;
-      const float2 w = tw[t];  // (cos, -sin)
-      const float4 ab = ABs[kh * BAND_HC_CB + c];
-      zx = fmaf(ab.x, w.x, fmaf(ab.w, w.y, zx));   // A.re cos - B.im sin
-      zy = fmaf(ab.y, w.x, fmaf(-ab.z, w.y, zy));  // A.im cos + B.re sin
+    for (int k0 = 0; k0 <= KH; k0 += 4) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = k0 + u <= KH;
+        const float2 w = tw[t];
+        av[u] = ok ? (hl ? -w.y : w.x) : 0.f;  // k-slot (k, cos) on lanes 0-31, (k, sin) on 32-63
+        bv[u] = ok ? G[(2 * (k0 + u) + hl) * 32 + l31] : 0.f;
+        t += hm;
+        t = t >= H ? t - H : t;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) z = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], z, 0, 0, 0);
     }
-    P[(int64_t)hh * BAND_FWD_SEGS * ncol + col] = mk(zx, zy);
+    if (col < ncol)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int hh = 32 * ht + acc_row(r) + 4 * hl;
+        if (hh < H) Pf[((int64_t)hh * BAND_FWD_SEGS * ncol + col) * 2 + (l31 & 1)] = z[r];
+      }
   }
   // the out-of-box spike points: the program applied to a coefficient the low-pass zeroed
   if (blockIdx.x == 0 && tid < BAND_MAX_PTS) {
     const BandSamplePts& sp = a.sp[s];
     cf c = mk(0.f, 0.f);
     if (tid < sp.n) {
-      const BandPt p = sp.p[tid];
-      c = apply_ops(so, chan, mk(0.f, 0.f), freq_col(p.kw, p.kd, W, D), p.kh, H);
+      const BandPt pt = sp.p[tid];
+      c = apply_ops(so, chan, mk(0.f, 0.f), freq_col(pt.kw, pt.kd, W, D), pt.kh, H);
     }
     a.pts[(int64_t)bc * BAND_MAX_PTS + tid] = c;
   }
 }
 
 // ----------------------------------------------------------------------------- pass B2'
+__device__ void band_tab16(const BandMidArgs& a, int t);  // pass C''s split-f16 table (below)
 // Z_h(col) = A_0 + sum_kh>=1 (A cos + i B sin), theta = 2 pi kh h / H, for every slab h: lanes =
 // columns (AB loaded once per lane), waves = slabs (twiddles wave-uniform).  Written over P.
 __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
@@ -471,6 +553,11 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.pl.H, D = a.pl.D, KH = a.g.KH, KW = a.g.KW, NDk = a.g.NDk, ncol = a.g.ncol;
   const int npm = a.g.KS - NDk, KV = KW + 1 + npm, VT = band_vt(a.g);
+  const int nzb = (H * a.nbc + 3) / 4;  // blocks past these build the split-f16 synthesis table
+  if ((int)blockIdx.x >= nzb) {
+    band_tab16(a, ((int)blockIdx.x - nzb) * BAND_NT + tid);
+    return;
+  }
   const int u = (int)blockIdx.x * 4 + wv;
   if (u >= H * a.nbc) return;
   const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
@@ -533,7 +620,6 @@ __global__ __launch_bounds__(BAND_NT) void k_band_zh(BandMidArgs) {
 //                imaginary parts when odd -- so it is the B operand of one k-step as it stands
 //   y[w][d] = E - O,  y[w][D - d] = E + O   for d in [0, D/2]  (the C2R folded over d <-> D - d)
 // Each lane ends with 4 consecutive columns of one image row for both halves: 16-B stores.
-__device__ __forceinline__ int acc_row(int s) { return (s & 3) + 8 * (s >> 2); }  // rho(s)
 #ifndef TB_INV_PRIO
 #define TB_INV_PRIO 2  // 2: store phases at raised wave priority (C3 -2 %, C2 -5 %); 1: MFMA phases; 0: off
 #endif
@@ -834,7 +920,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
 //   Y^T(w, d) = sum_v V^T(w, v) T(v, d),   T(2 kd, d) = cos(2 pi kd d / D), T(2 kd + 1, d) = -sin(..)
 // for every output column d < D + pad (T = 0 past D: the U-Net's zero padding comes out of the
 // MFMA).  V^T is the V-product accumulator tile used as the A operand as it stands (its rows are
-// the k index); T is the launch's fragment image (k_band_tab16) in LDS.  Split precision:
+// the k index); T is the launch's fragment image (band_tab16, built by pass B2''s extra blocks) in LDS.  Split precision:
 // V = Vh + Vl (scaled by a power of two per unit so that max |V| < 2^15), T = Th + Tl (scaled by
 // 2^8), Y = (Vh Th + Vh Tl + Vl Th) / scale -- 22 bits per operand, the dropped Vl Tl term
 // 2^-22 relative, so Y matches the f32 synthesis to a few 1e-7 of max |y|.  The accumulator has
@@ -852,10 +938,8 @@ __device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
 // to match the accumulator-as-A-operand order of V^T (element j of lane half h is V row
 // 16 c + 8 (j >> 2) + 4 h + (j & 3)); rows 2 kd + (re, im), the band columns first, then every
 // sample's out-of-box points in launch order.
-__global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
-  const BandMidArgs& a = kargs<BandMidArgs>();
+__device__ void band_tab16(const BandMidArgs& a, int t) {
   const int nch = band_nch(a.g), ntd = a.g.NTD, NCOL = a.g.NCOL, NDk = a.g.NDk, D = a.pl.D, Dh = D / 2 + 1;
-  const int t = (int)(blockIdx.x * 256 + threadIdx.x);
   if (t >= ntd * nch * 64) return;
   const int lane = t & 63, cc = t >> 6, c = cc % nch, nt = cc / nch;
   const int d = 32 * nt + (lane & 31), hl = lane >> 5;
@@ -867,14 +951,7 @@ __global__ __launch_bounds__(256) void k_band_tab16(BandMidArgs) {
   for (int j = 0; j < 8; ++j) {
     const int v = 16 * c + 8 * (j >> 2) + 4 * hl + (j & 3);
     const int pr = v >> 1, im = v & 1;
-    int kd = -1;
-    if (pr < NDk) {
-      kd = pr;
-    } else {
-      const int gp = pr - NDk;
-      for (int s = 0; s < TB_MAX_BATCH && kd < 0; ++s)
-        if (gp >= a.p0[s] && gp < a.p0[s] + a.sp[s].n) kd = a.sp[s].p[gp - a.p0[s]].kd;
-    }
+    const int kd = pr < NDk ? pr : (pr - NDk < a.g.PT ? (int)a.pkd[pr - NDk] : -1);
     float tv = 0.f;
     if (kd >= 0 && in) {
       tv = a.tds[(2 * kd + im) * NCOL + dd];
@@ -924,6 +1001,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int ntw = (W + 31) / 32;
   const int nslab = H * a.nbc;
   const int ncolo = D + a.ypad;        // stored columns of a row
+  if (a.diag & 128) tb4 = 0;           // measurement: no table loads (results invalid)
   const int diag = a.diag;             // measurement only (TEXBIAS_BAND_DIAG >> 8): skipped stages
   if (diag & 64) return;
   const int nunit = nslab * ntw;
@@ -937,7 +1015,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
     const int nb = s1 - s0 + 1;
     __syncthreads();
     {  // [tables,] the batch's V-product fragments: rounds of loads in flight
-      const int nf4 = nb * fsz / 4;
+      const int nf4 = (a.diag & 256) ? 0 : nb * fsz / 4;
       const int ntot = tb4 + nf4;
       const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
       for (int base = 0; base < ntot; base += 9 * BAND_NT) {
@@ -1273,18 +1351,21 @@ hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
   return k1 ? launch_fwd_t<2, 1, 0>(a, lds, ncu, st) : launch_fwd_t<2, 2, 0>(a, lds, ncu, st);
 }
 
-hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
+template <int MT>
+hipError_t launch_hcol_t(const BandMidArgs& a, hipStream_t st) {
   const size_t lds = band_hc_lds(a.pl.H, a.g.KH);
-  hipError_t e = allow_lds(k_band_hcol, lds);
+  auto kern = k_band_hcol<MT>;
+  hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_band_hcol, dim3((a.g.ncol + BAND_HC_CB - 1) / BAND_HC_CB, a.nbc), dim3(BAND_NT), lds, st, a);
-  e = hipGetLastError();
+  hipLaunchKernelGGL(kern, dim3((a.g.ncol + BAND_HC_CB - 1) / BAND_HC_CB, a.nbc), dim3(64 * BAND_HC_NW), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
+  hipError_t e = a.g.KH + 1 <= 16 ? launch_hcol_t<1>(a, st) : launch_hcol_t<2>(a, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4), dim3(BAND_NT), 0, st, a);
-  e = hipGetLastError();
-  if (e != hipSuccess || !a.g.cat) return e;
-  const int nth = a.g.NTD * band_nch(a.g) * 64;
-  hipLaunchKernelGGL(k_band_tab16, dim3((nth + 255) / 256), dim3(256), 0, st, a);
+  const int ntab = a.g.cat ? (a.g.NTD * band_nch(a.g) * 64 + BAND_NT - 1) / BAND_NT : 0;
+  hipLaunchKernelGGL(k_band_zh, dim3((a.pl.H * a.nbc + 3) / 4 + ntab), dim3(BAND_NT), 0, st, a);
   return hipGetLastError();
 }
 

@@ -727,6 +727,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
       ma.sp[i] = sp[i];
       ma.ops.s[i] = ops[b0 + i];
       ma.p0[i] = p0;
+      for (int j = 0; j < sp[i].n; ++j) ma.pkd[p0 + j] = sp[i].p[j].kd;
       p0 += sp[i].n;
     }
     ma.T16 = ws + wl.off_t16;
@@ -758,7 +759,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.tds = p->tds;
     ia.T16 = ws + wl.off_t16;
     ia.g = g;
-    ia.diag = (g_band_diag >> 8) & 0xff;
+    ia.diag = (g_band_diag >> 8) & 0xffff;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
     TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
   }

@@ -6,6 +6,8 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-r3p}; shift
 O=gpurun_out/$T
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --tb=short --timeout 200 --timeout-method thread -m gpu tests/test_gpu_band.py > $O/tests_band.log 2>&1
+rc=$?; grep -cE "PASSED" $O/tests_band.log; [ $rc = 0 ] || { grep -E "Error|assert" $O/tests_band.log | head -30 | cut -c1-300; exit $rc; }
 for fl in 1024 0; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_f$fl -o run -- python3 scripts/pass_bench.py --config c3 --iters 20 --flush-mb $fl > $O/prof_c3_f$fl.out 2> $O/prof_c3_f$fl.err || { echo prof $fl failed; tail -5 $O/prof_c3_f$fl.err; exit 1; }
   f=$(find $O/prof_c3_f$fl -name '*kernel_stats.csv' | head -1)
