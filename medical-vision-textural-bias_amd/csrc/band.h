@@ -177,18 +177,20 @@ TB_HD BandInvCarve band_inv_carve(const BandGeo& g, int W, int D) {
 #define TB_BAND_SLOTS16 3
 #endif
 constexpr int BAND_SLOTS16 = TB_BAND_SLOTS16;
+// slab slots of a workgroup of nw waves (16 waves: one workgroup per CU takes ~4x the units)
+TB_HD constexpr int band_slots16(int nw) { return nw <= 4 ? BAND_SLOTS16 : 12; }
 TB_HD int band_nch(const BandGeo& g) { return (band_rows(g) + 15) / 16; }
 TB_HD int band_t16_bytes(const BandGeo& g) { return g.NTD * band_nch(g) * 2 * 64 * 16; }
 struct BandInv16Carve {
   int tab, tww, frag, pkw, total;
 };
-TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W) {
+TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W, int slots = BAND_SLOTS16) {
   BandInv16Carve c;
   c.tab = 0;
   c.tww = band_al16(band_t16_bytes(g));
   c.frag = band_al16(c.tww + W * 8);
-  c.pkw = band_al16(c.frag + BAND_SLOTS16 * band_vt(g) * band_kv(g) * 64 * 4);
-  c.total = band_al16(c.pkw + BAND_SLOTS16 * BAND_MAX_PTS * 4);
+  c.pkw = band_al16(c.frag + slots * band_vt(g) * band_kv(g) * 64 * 4);
+  c.total = band_al16(c.pkw + slots * BAND_MAX_PTS * 4);
   return c;
 }
 

@@ -970,8 +970,14 @@ __device__ void band_tab16(const BandMidArgs& a, int t) {
 #ifndef TB_INV16_WPE
 #define TB_INV16_WPE 4  // waves per SIMD the VT = 1 split-f16 kernel is compiled for (register budget)
 #endif
-template <int VT>  // 32-row tiles of V
-__global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1 ? TB_INV16_WPE : 3, 8))) void k_band_inv16(BandInvArgs) {
+#ifndef TB_INV16_NW
+#define TB_INV16_NW 16  // waves per split-f16 pass-C' workgroup: 16 = one workgroup per CU (C3 80 -> 72 us vs 4)
+#endif
+#ifndef TB_INV16_TR
+#define TB_INV16_TR 1   // 1: tile rows = image columns where row strides allow (see k_band_inv16); 0: never
+#endif
+template <int VT, int NW, bool TR>  // 32-row tiles of V; waves per workgroup; tile rows = image columns
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1 ? TB_INV16_WPE : 3, 8))) void k_band_inv16(BandInvArgs) {
   // Same unit structure as k_band_inv: (slab, 32-row tile) units dealt to a persistent grid, each
   // workgroup's slabs in batches whose V-product fragments are loaded to LDS first (the unit loop
   // then issues no vector-memory loads), per-unit min/max partials.
@@ -986,7 +992,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int nch = band_nch(a.g);       // 16-row chunks of V in use
   const int ntd = a.g.NTD;             // 32-column tiles of the output row (D + pad)
   const int fsz = VT * KV * 64;
-  const BandInv16Carve cv = band_inv16_carve(a.g, W);
+  constexpr int NT = 64 * NW, SLOTS = band_slots16(NW);
+  const BandInv16Carve cv = band_inv16_carve(a.g, W, SLOTS);
   const h16x8* Tab = reinterpret_cast<const h16x8*>(smem + cv.tab);  // [nt][c][hi/lo][64]
   float2* twW = reinterpret_cast<float2*>(smem + cv.tww);
   float* Fs = reinterpret_cast<float*>(smem + cv.frag);
@@ -994,7 +1001,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int ntab4 = band_t16_bytes(a.g) / 16;
   const bool twv = !(W & 1) && (reinterpret_cast<uintptr_t>(a.pl.tw[1]) & 15) == 0;
   const int ntw4 = twv ? W / 2 : 0;
-  if (!twv) lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  if (!twv)
+    for (int i = tid; i < W; i += NT) twW[i] = reinterpret_cast<const float2*>(a.pl.tw[1])[i];
   const float4* Tsrc = reinterpret_cast<const float4*>(a.T16);
   const float4* Wsrc = reinterpret_cast<const float4*>(a.pl.tw[1]);
   int tb4 = ntab4 + ntw4;
@@ -1003,6 +1011,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int ncolo = D + a.ypad;        // stored columns of a row
   if (a.diag & 128) tb4 = 0;           // measurement: no table loads (results invalid)
   const int diag = a.diag;             // measurement only (TEXBIAS_BAND_DIAG >> 8): skipped stages
+  constexpr bool tr = TR;
   if (diag & 64) return;
   const int nunit = nslab * ntw;
   const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -1010,7 +1019,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
   for (int c0 = ub; c0 < ue;) {
     const int s0 = c0 / ntw;
     const int slast = (ue - 1) / ntw;
-    const int s1 = slast < s0 + BAND_SLOTS16 - 1 ? slast : s0 + BAND_SLOTS16 - 1;
+    const int s1 = slast < s0 + SLOTS - 1 ? slast : s0 + SLOTS - 1;
     const int c1 = (s1 + 1) * ntw < ue ? (s1 + 1) * ntw : ue;
     const int nb = s1 - s0 + 1;
     __syncthreads();
@@ -1018,11 +1027,11 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
       const int nf4 = (a.diag & 256) ? 0 : nb * fsz / 4;
       const int ntot = tb4 + nf4;
       const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
-      for (int base = 0; base < ntot; base += 9 * BAND_NT) {
+      for (int base = 0; base < ntot; base += 9 * NT) {
         float4 v[9];
 #pragma unroll
         for (int u = 0; u < 9; ++u) {
-          const int e = base + u * BAND_NT + tid;
+          const int e = base + u * NT + tid;
           const int q = e - tb4;
           if (e < tb4)
             v[u] = e < ntab4 ? Tsrc[e] : Wsrc[e - ntab4];
@@ -1031,7 +1040,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
         }
 #pragma unroll
         for (int u = 0; u < 9; ++u) {
-          const int e = base + u * BAND_NT + tid;
+          const int e = base + u * NT + tid;
           const int q = e - tb4;
           if (e < tb4) {
             if (e < ntab4)
@@ -1052,7 +1061,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
     }
     __syncthreads();
     if (diag & 32) return;
-    for (int un = c0 + ((wv - ((c0 - ub) & 3)) & 3); un < c1; un += 4) {
+    for (int un = c0 + ((wv - ((c0 - ub) % NW) + NW) % NW); un < c1; un += NW) {  // (un - ub) % NW == wave
       const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
       const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
       const float* F = Fs + slot * fsz + lane;
@@ -1134,9 +1143,15 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
           if (c >= nch || (diag & 8)) break;
           const h16x8* tp = Tab + ((nt * nch + c) * 2) * 64 + lane;
           const h16x8 th = tp[0], tl = tp[64];
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], th, acc, 0, 0, 0);
+          if (tr) {  // Y(d, w) = T(d, v) . V(v, w): the table as the A operand, the V tile as B
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, al[c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, ah[c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ah[c], acc, 0, 0, 0);
+          } else {   // Y^T(w, d) = V^T(w, v) . T(v, d)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], th, acc, 0, 0, 0);
+          }
         }
         const int col = 32 * nt + l31;
         if (diag & 16) {  // no stores: keep the results live
@@ -1144,6 +1159,34 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
 #pragma unroll
           for (int r = 0; r < 16; ++r) z += acc[r];
           lo = fminf(lo, z);
+          continue;
+        }
+        if (tr) {  // lane (w, half): columns 32 nt + 8 g + 4 half + 0..3 in registers 4 g .. 4 g + 3: 16-B stores
+          const int wr = 32 * tw_ + l31;
+          if (wr < W) {
+            float* yr = yb + (int64_t)wr * a.sw;
+            const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int d0 = 32 * nt + 8 * g + 4 * hl;
+              f32x4 v;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = acc[4 * g + q] * inv;  // exactly 0 past D (T = 0 there)
+              if (vec && d0 + 4 <= ncolo) {
+                *reinterpret_cast<f32x4*>(yr + d0) = v;
+              } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (d0 + q < ncolo) yr[d0 + q] = v[q];
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (d0 + q < D) {
+                  lo = fminf(lo, v[q]);
+                  hi = fmaxf(hi, v[q]);
+                }
+            }
+          }
           continue;
         }
         if (col < ncolo) {
@@ -1308,13 +1351,17 @@ hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int VT>
+template <int VT, int NW>
 hipError_t launch_inv16_t(const BandInvArgs& a, int ncu, hipStream_t st) {
-  const size_t lds = band_inv16_carve(a.g, a.pl.W).total;
-  auto kern = k_band_inv16<VT>;
+  const size_t lds = band_inv16_carve(a.g, a.pl.W, band_slots16(NW)).total;
+  // output orientation: tile rows = image columns (16-B row stores) unless rows are 512-B strided
+  // (a power-of-two row stride piles one store's 32 rows onto one memory channel): then image rows
+  auto kern = (TB_INV16_TR && ((a.sw * 4) % 512) != 0) ? k_band_inv16<VT, NW, true> : k_band_inv16<VT, NW, false>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(band_grid(kern, a.pl.H * a.nbc, lds, ncu, 8)), dim3(BAND_NT), lds, st, a);
+  const int per_cu = band_occupancy(kern, lds, 64 * NW, 8);
+  const int units = a.pl.H * a.nbc, g = ncu * per_cu;
+  hipLaunchKernelGGL(kern, dim3(units < g ? units : g), dim3(64 * NW), lds, st, a);
   return hipGetLastError();
 }
 
@@ -1372,7 +1419,11 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
 
 
 hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
-  if (a.g.cat) return band_vt(a.g) == 1 ? launch_inv16_t<1>(a, ncu, st) : launch_inv16_t<2>(a, ncu, st);
+  if (a.g.cat) {
+    if (TB_INV16_NW == 16 && band_inv16_carve(a.g, a.pl.W, band_slots16(16)).total <= 160000)
+      return band_vt(a.g) == 1 ? launch_inv16_t<1, 16>(a, ncu, st) : launch_inv16_t<2, 16>(a, ncu, st);
+    return band_vt(a.g) == 1 ? launch_inv16_t<1, 4>(a, ncu, st) : launch_inv16_t<2, 4>(a, ncu, st);
+  }
   return band_vt(a.g) == 1 ? launch_inv_t<1>(a, ncu, st) : launch_inv_t<2>(a, ncu, st);
 }
 
