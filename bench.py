@@ -29,6 +29,15 @@ for p in (PKG, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# MIOpen's find-db / perf-db (seeded in the tree: miopen_db/, gfx950 + this image's MIOpen) and its
+# compiled-kernel cache: MIOpen's Find (cudnn.benchmark) then runs once per cache, not once per process
+# and rank (first step 12.9 s cold -> 0.8 s seeded; texbias/__init__ also keeps MIOpen's naive solvers out
+# of Find, which was 140 s).  Set before torch initialises MIOpen; TEXBIAS_MIOPEN_DIR overrides, an
+# existing MIOPEN_* setting wins.
+_MIOPEN_DIR = os.environ.get("TEXBIAS_MIOPEN_DIR", os.path.join(ROOT, "miopen_db"))
+os.environ.setdefault("MIOPEN_USER_DB_PATH", _MIOPEN_DIR)
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_MIOPEN_DIR, "kcache"))
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -75,7 +84,7 @@ def parse():
     return a
 
 
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r2")  # traffic_<config>.json (scripts/make_traffic.py)
+TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r3")  # traffic_<config>.json (scripts/make_traffic.py)
 
 
 def pmc_traffic(kernel: str, launch_bytes: int, config: str = "c3"):
@@ -268,7 +277,7 @@ def main():
             "roofline": {"kernel": passes[dom]["kernel"], "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(passes[dom]["kernel"], dom_bytes, args.config),
-                         "traffic_unit": f"bytes per launch (rocprofv3 PMC, profiles/r2/traffic_{args.config}.json)",
+                         "traffic_unit": f"bytes per launch (rocprofv3 PMC, profiles/r3/traffic_{args.config}.json)",
                          "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),

@@ -9,4 +9,14 @@ Layering (DESIGN.md):
   unet / losses      MONAI-equivalent 3-D residual U-Net and DiceLoss (PyTorch-ROCm)
   train              train step, DDP over RCCL
 """
+import os as _os
+
 __version__ = "0.1.0"
+
+# MIOpen's naive direct-convolution solvers are reference kernels: on this U-Net's full-volume layers
+# one trial of them takes up to 9 s, and MIOpen's Find (cudnn.benchmark) times every applicable
+# solver on first use -- ~120 s of the first train step in every process (round-2 profile).  The
+# implicit-GEMM / GEMM solvers cover every layer, so the naive ones are left out of the search.
+# Set before MIOpen reads them (first convolution); an explicit setting wins.
+for _d in ("FWD", "BWD", "WRW"):
+    _os.environ.setdefault(f"MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_{_d}", "0")

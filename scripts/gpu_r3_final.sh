@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 3 perf record: bench C3 (with CPU baseline), C2, C5; filter-only C3 + PMC FETCH/WRITE passes for
+# roofline.traffic; rocprofv3 kernel trace of the C3 train step (steady-state window).  Usage: TAG
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/${1:-r3f}; mkdir -p $O
+run() { local n=$1; shift; timeout -k 10 600 python3 -u bench.py "$@" > $O/$n.json 2> $O/$n.err || { echo "$n failed"; tail -5 $O/$n.err; exit 1; }; cut -c1-220 $O/$n.json; }
+run bench_c3
+run bench_c2 --config c2 --no-cpu-baseline
+run bench_c5 --config c5 --no-cpu-baseline
+run filter_c3 --filter-only --steps 20 --warmup 3 --no-cpu-baseline
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --filter-only --steps 5 --warmup 2 --no-cpu-baseline > /dev/null 2> $O/pmc_fetch.err || { echo fetch failed; tail -3 $O/pmc_fetch.err; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 bench.py --filter-only --steps 5 --warmup 2 --no-cpu-baseline > /dev/null 2> $O/pmc_write.err || { echo write failed; tail -3 $O/pmc_write.err; exit 1; }
+python3 scripts/make_traffic.py $O/pmc_fetch $O/pmc_write $O/filter_c3.json $O/traffic_c3.json "--filter-only --steps 5 --warmup 2" > /dev/null || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof_c3.json 2> $O/prof_c3.err || { echo prof failed; tail -5 $O/prof_c3.err; exit 1; }
+f=$(find $O/prof_c3 -name '*kernel_trace.csv' | head -1)
+python3 scripts/steady_stats.py $f --steps 20 --marker k_band_fwd --top 30 > $O/steady_c3.txt && head -14 $O/steady_c3.txt
+rm -f $f
+echo done
