@@ -60,6 +60,14 @@ def parse():
     ap.add_argument("--shape", type=str, default=None, help="c3: 240,240,155; c2: 128,128,128")
     ap.add_argument("--pad-to", type=int, default=None, help="U-Net D extent (c3: 160, G10: 155 is not /16)")
     ap.add_argument("--random-filters", action="store_true")
+    ap.add_argument("--chain", choices=("ref", "planes", "wrap", "gibbs-aug", "spikes-aug"), default="ref",
+                    help="c3: which of the reference's chains runs -- ref: disk -> planes -> wrap -> S&P "
+                         "(127_.../..._3modalities.py:171-174); planes: RandPlaneWaves_ellipsoid alone "
+                         "(30_plane_waves_filters/stylized_planes15.py:133); wrap: WrapArtifactd(0.5) alone "
+                         "(50_wraparound/stylized_wrap0__test.py); gibbs-aug: RandGibbsNoised(alpha=(0, 0.4)) "
+                         "(300_.../30_augmentation/baseline_domain_augment_alpha0p4.py:118); spikes-aug: "
+                         "RandKSpaceSpikeNoised(intensity_ranges=(10, 11)) (..._spikes10-11.py:120); the two "
+                         "augmentations at prob 1 (the drivers' 0.1 would time mostly identity copies)")
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--no-cudnn-benchmark", action="store_true",
                     help="skip MIOpen Find (its exhaustive solver search makes the first step slow, the rest fast)")
@@ -78,6 +86,8 @@ def parse():
     if c5:
         a.no_cpu_baseline = True  # the reference trains its DCGAN on the GPU; no CPU path to time
         a.channels_last = True    # NHWC: 4.89k vs 4.60k slices/s at batch 64 (profiles/r2/bench/c5_variants.txt)
+    if a.chain != "ref":
+        a.no_cpu_baseline = True  # the CPU restatement times the reference chain only
     a.cpu_sample_vols = a.cpu_sample_vols or (8 if c2 else 1)
     if c2:
         a.filter_only = True  # config 2 is the filter kernel alone
@@ -174,6 +184,20 @@ def main():
         chain = FusedChain([disk])
     elif args.config == "c5":  # 2-D slices [B, 1, 1, 128, 128]: the plane-wave shell does not fit
         chain = FusedChain([disk, wrap, sap])
+    if args.config == "c3" and args.chain != "ref":
+        import filters_and_operators as F
+        if args.chain == "planes":
+            chain = FusedChain([planes])
+        elif args.chain == "wrap":
+            chain = FusedChain([wrap])
+        elif args.chain == "gibbs-aug":
+            g = F.RandGibbsNoised("image", prob=1.0, alpha=(0.0, 0.4))
+            g.set_random_state(100 + rank)
+            chain = FusedChain([g])
+        else:
+            g = F.RandKSpaceSpikeNoised("image", global_prob=1.0, prob=1.0, intensity_ranges={"image": (10.0, 11.0)})
+            g.set_random_state(100 + rank)
+            chain = FusedChain([g])
     prs = np.random.RandomState(12345 + rank)
 
     def randomize_filters():
@@ -265,6 +289,7 @@ def main():
                 "workload": (("C3 full filter chain (disk 12.5 -> plane wave (55,55,30) I=15 -> wrap 0.5 -> S&P 0.05) "
                               "+ 3D U-Net(4->3, 16..256, 2 res units) fwd/bwd/Adam(amsgrad), DiceLoss")
                              + (" [random per-batch filter params, config 4]" if args.random_filters else "")
+                             + (f" [CHAIN {args.chain}: see bench.py --help]" if args.chain != "ref" else "")
                              + (" [FILTER ONLY diagnostic]" if args.filter_only else ""))
                             if args.config == "c3" else
                             "C2 Gibbs truncation: RandFourierDiskMaskd(r=12.5) low-pass alone, batched 4x128^3 volumes",

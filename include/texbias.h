@@ -109,8 +109,8 @@ int tb_kspace_filter_f32(const tb_plan* plan, const float* x, const int64_t* xs,
  *   y = cls==1 ? min_b/2 : cls==2 ? max_b/2 : x     (min_b/max_b from minmax keys)
  * u_in != NULL (parity mode): u is the caller's field, one value per voxel (the reference's
  *   torch.rand), classified exactly as above.
- * u_in == NULL: the device stream -- per segment of 1024 voxels, Philox4x32-10 (key seed, counter
- *   from sample / segment / draw, stream `offset`) drives a geometric-gap walk over the changed
+ * u_in == NULL: the device stream -- per segment of 256 voxels (TB_SAP_SEG), Philox4x32-10 (key seed,
+ *   counter (sample << 44) ^ (segment << 20) | draw, stream `offset`) drives a geometric-gap walk over the changed
  *   voxels (gap = floor(log u / log(1 - thr[b][1]))) and each changed voxel's class (MIN with
  *   probability thr[b][0] / thr[b][1]): the same Bernoulli field at ~p of the RNG work.
  *   In place (x == y) only the changed voxels are stored; out of place y is a copy plus them.
@@ -288,6 +288,15 @@ const char* tb_pass_kernel(int slot);
  * copied through unchanged (bit-identical, as the reference returns them untouched).
  */
 int tb_set_band_plans(int enable);
+
+/*
+ * Spike-only programs (RandPlaneWaves_ellipsoid, KSpaceSpikeNoise: filters_and_operators.py:370-393,
+ * 966-983) whose spikes do not touch (no two at equal or conjugate frequencies in a shared channel) run
+ * in closed form, y = x + Re(sum_j Delta_j e^{2 pi i f_j.n/N}) / N with Delta_j = target_j(K(f_j)) - K(f_j):
+ * one pass computing the coefficients K(f_j), one streaming add (12 B per voxel instead of a spectrum
+ * round trip).  Same results to rounding.  Default on; TEXBIAS_POINT=0 in the environment turns it off.
+ */
+int tb_set_point_plans(int enable);
 
 /*
  * Pass C' of the band-limited plans synthesises the image on the f16 matrix cores in split

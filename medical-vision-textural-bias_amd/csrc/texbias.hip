@@ -22,6 +22,7 @@
 #include "band.h"
 #include "fft_core.h"
 #include "kernels.h"
+#include "point.h"
 #include "plan_host.h"
 #include "sap_core.h"
 
@@ -507,6 +508,12 @@ static bool g_band = [] {
   const char* e = std::getenv("TEXBIAS_BAND");
   return !(e && e[0] == '0');
 }();
+// Spike-only programs (plane waves, k-space spikes) in closed form (point.h); TEXBIAS_POINT=0 or
+// tb_set_point_plans(0): the full-spectrum passes.
+static bool g_point = [] {
+  const char* e = std::getenv("TEXBIAS_POINT");
+  return !(e && e[0] == '0');
+}();
 // Pass C' synthesis in split f16 on the matrix cores (k_band_inv16) when the launch's V rows fit
 // (band columns + every sample's points <= 64); TEXBIAS_INV16=0 or tb_set_band_inv16(0): the f32 kernel.
 static bool g_inv16 = [] {
@@ -635,7 +642,7 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   return true;
 }
 
-enum { RUN_COPY = 0, RUN_FULL = 1, RUN_BAND = 2 };
+enum { RUN_COPY = 0, RUN_FULL = 1, RUN_BAND = 2, RUN_POINT = 3 };
 
 template <int RA, int RB>
 static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad, cf* S,
@@ -780,6 +787,36 @@ static int run_generic(const tb_plan* p, const float* x, const int64_t* xs, floa
   return TB_OK;
 }
 
+static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
+                     char* ws, int bcn_total, int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax,
+                     hipStream_t st) {
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  const int nbc = nb * C;
+  tb::PointArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.H = H, a.W = W, a.D = D;
+  a.x = x, a.xsbc = xs[0], a.xsh = xs[1], a.xsw = xs[2];
+  a.y = y, a.ysbc = ys[0], a.ysh = ys[1], a.ysw = ys[2];
+  a.ypad = y_pad, a.bc0 = b0 * C, a.C = C, a.nbc = nbc, a.mm = minmax;
+  a.part = reinterpret_cast<double*>(ws);
+  a.delta = reinterpret_cast<float*>(ws + (((size_t)bcn_total * H * TB_MAX_OPS * 2 * sizeof(double) + 255) & ~(size_t)255));
+  for (int i = 0; i < nb; ++i) a.ops.s[i] = ops[b0 + i];
+  const double vox = (double)nbc * H * W * D;
+  {
+    Timer t(0, st, vox * 4.0, "k_point_dft");
+    TB_HIP(tb::launch_point(a, st, 0));
+  }
+  {
+    Timer t(1, st, (double)nbc * H * TB_MAX_OPS * 16.0, "k_point_delta");
+    TB_HIP(tb::launch_point(a, st, 1));
+  }
+  {
+    Timer t(2, st, vox * 4.0 + (double)nbc * H * W * (D + y_pad) * 4.0, "k_point_apply");
+    TB_HIP(tb::launch_point(a, st, 2));
+  }
+  return TB_OK;
+}
+
 static int run_copy(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad, int b0,
                     int nb, int C, uint32_t* minmax, hipStream_t st) {
   const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
@@ -822,6 +859,11 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
       while (j < nb && route(b0 + j) == run.route) ++j;
       run.s0 = b0 + i;
       run.s1 = b0 + j;
+      if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_workspace_bytes(p->dev.H, B * C)) {
+        bool pt = true;
+        for (int s = run.s0; s < run.s1 && pt; ++s) pt = tb::point_program(ops[s], p->dev.H, p->dev.W, p->dev.D);
+        if (pt) run.route = RUN_POINT;
+      }
       if (run.route == RUN_FULL && g_band && band_plan(p, ops, run.s0, run.s1, y_pad, ws_bytes, B * C, run.g, run.sp))
         run.route = RUN_BAND;
       atomic_keys |= run.route != RUN_BAND;
@@ -838,6 +880,8 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     int rc = TB_OK;
     if (run.route == RUN_COPY)
       rc = run_copy(p, x, xs, y, ys, y_pad, run.s0, nb, C, minmax, st);
+    else if (run.route == RUN_POINT)
+      rc = run_point(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, run.s0, nb, C, ops, minmax, st);
     else if (run.route == RUN_BAND)
       rc = run_band(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, run.s0, nb, C, ops, run.g, run.sp, minmax,
                     st);
@@ -1006,6 +1050,11 @@ int tb_set_compiled_plans(int enable) {
 
 int tb_set_band_plans(int enable) {
   g_band = enable != 0;
+  return TB_OK;
+}
+
+int tb_set_point_plans(int enable) {
+  g_point = enable != 0;
   return TB_OK;
 }
 

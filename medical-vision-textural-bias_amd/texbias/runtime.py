@@ -349,6 +349,12 @@ def set_band_plans(enable: bool) -> None:
     check(lib().tb_set_band_plans(1 if enable else 0))
 
 
+def set_point_plans(enable: bool) -> None:
+    """Spike-only programs (plane waves, k-space spikes) in closed form when True (default), else
+    on the full-spectrum passes (tb_set_point_plans)."""
+    check(lib().tb_set_point_plans(1 if enable else 0))
+
+
 def set_band_inv16(enable: bool) -> None:
     """Pass C' synthesis in split f16 on the matrix cores when True (default, where the launch's
     V rows fit), else the f32 MFMA synthesis (tb_set_band_inv16)."""
