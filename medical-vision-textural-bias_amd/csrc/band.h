@@ -106,6 +106,7 @@ struct BandMidArgs {
   void* T16;        // g.cat: synthesis-table fragments for pass C' (written by k_band_tab16)
   const float* tds; // g.cat: [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   BatchOps ops;
+  uint32_t* cnt;    // pass C''s arrival counter, zeroed here (B' runs before every C')
 };
 
 struct BandInvArgs {
@@ -124,6 +125,7 @@ struct BandInvArgs {
   int diag;
   const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   const void* T16;  // g.cat: split-f16 synthesis-table fragments (k_band_tab16)
+  uint32_t* cnt;    // g.cat: arrival counter (zeroed by pass B'); the last workgroup writes the keys
 };
 
 // Pass A': LDS row pitch of a staged strip.  Odd D: D (the strip is one contiguous run, 16-B
@@ -204,7 +206,7 @@ TB_HD size_t band_hc_lds(int H, int KH) {
 
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels
 struct BandWs {
-  size_t off_P, off_AB, off_pts, off_mmp, off_m2f, off_t16, total;
+  size_t off_P, off_AB, off_pts, off_mmp, off_m2f, off_t16, off_cnt, total;
 };
 TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   BandWs w;
@@ -217,7 +219,8 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
   w.off_m2f = (w.off_m2f + 255) & ~(size_t)255;
   w.off_t16 = w.off_m2f + (size_t)bcn * H * band_vt(g) * band_kv(g) * 64 * 4;
   w.off_t16 = (w.off_t16 + 255) & ~(size_t)255;
-  w.total = w.off_t16 + (size_t)band_t16_bytes(g);
+  w.off_cnt = (w.off_t16 + (size_t)band_t16_bytes(g) + 255) & ~(size_t)255;  // pass C' arrival counter
+  w.total = w.off_cnt + 256;
   return w;
 }
 

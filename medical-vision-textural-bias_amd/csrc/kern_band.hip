@@ -387,6 +387,7 @@ __global__ __launch_bounds__(64 * BAND_HC_NW) void k_band_hcol(BandMidArgs) {
   float* G = Qs + MT * 1024;                                        // [2 (KH + 1)][32]
   cf* P = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol;
   constexpr int NT = 64 * BAND_HC_NW;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && a.cnt) *a.cnt = 0u;
   for (int hh = tid; hh < H; hh += NT) tw[hh] = ld2(a.pl.tw[0] + hh);
   if (tid < BAND_HC_CB) Pb[H * BAND_HC_CB + tid] = make_float2(0.f, 0.f);
   {  // stage: lane -> (h offset tid >> 4, column tid & 15); UR slab rows x 3 slots in flight
@@ -967,6 +968,52 @@ __device__ void band_tab16(const BandMidArgs& a, int t) {
   T[(cc * 2 + 1) * 64 + lane] = fl;
 }
 
+// Per-sample min/max keys without a launch of their own: every workgroup of pass C' counts itself
+// in after its partials are stored (release fence); the last one to arrive (acquire fence, loads at
+// device scope so no stale L1 line is read) reduces the launch's partials as k_band_minmax does.
+template <int NT>
+__device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float* red = reinterpret_cast<float*>(smem);
+  const int ntw = (a.pl.W + 31) / 32, nb = a.nbc / a.C;
+  const int64_t n = (int64_t)a.C * a.pl.H * ntw;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int b = 0; b < nb; ++b) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(a.mmp + (int64_t)b * n);
+    float lo = 3.402823466e38f, hi = -3.402823466e38f;
+    for (int64_t i = threadIdx.x; i < n; i += NT) {
+      const uint64_t v = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lo = fminf(lo, __uint_as_float((uint32_t)v));
+      hi = fmaxf(hi, __uint_as_float((uint32_t)(v >> 32)));
+    }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (lane == 0) {
+      red[wid] = lo;
+      red[NT / 64 + wid] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < NT / 64; ++w) {
+        lo = fminf(lo, red[w]);
+        hi = fmaxf(hi, red[NT / 64 + w]);
+      }
+      const int sb = a.bc0 / a.C + b;
+      a.mm[2 * sb] = f2key(lo);
+      a.mm[2 * sb + 1] = f2key(hi);
+    }
+    __syncthreads();
+  }
+}
+
 #ifndef TB_INV16_WPE
 #define TB_INV16_WPE 4  // waves per SIMD the VT = 1 split-f16 kernel is compiled for (register budget)
 #endif
@@ -1027,29 +1074,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
       const int nf4 = (a.diag & 256) ? 0 : nb * fsz / 4;
       const int ntot = tb4 + nf4;
       const float4* F4 = reinterpret_cast<const float4*>(a.M2F + (int64_t)s0 * fsz);
+      // source and LDS destination chosen by selects, every load unconditional (a clamped index):
+      // branches around the loads made the compiler keep v[] in scratch and wait on each load
       for (int base = 0; base < ntot; base += 9 * NT) {
         float4 v[9];
 #pragma unroll
         for (int u = 0; u < 9; ++u) {
           const int e = base + u * NT + tid;
           const int q = e - tb4;
-          if (e < tb4)
-            v[u] = e < ntab4 ? Tsrc[e] : Wsrc[e - ntab4];
-          else
-            v[u] = F4[(q < nf4 && q >= 0) ? q : 0];
+          const float4* src = e < tb4 ? (e < ntab4 ? Tsrc + e : Wsrc + (e - ntab4)) : F4 + (q < nf4 ? q : 0);
+          v[u] = *src;
         }
 #pragma unroll
         for (int u = 0; u < 9; ++u) {
           const int e = base + u * NT + tid;
           const int q = e - tb4;
-          if (e < tb4) {
-            if (e < ntab4)
-              reinterpret_cast<float4*>(smem + cv.tab)[e] = v[u];
-            else
-              reinterpret_cast<float4*>(twW)[e - ntab4] = v[u];
-          } else if (q < nf4) {
-            reinterpret_cast<float4*>(Fs)[q] = v[u];
-          }
+          const int dst = e < tb4 ? (e < ntab4 ? cv.tab + 16 * e : cv.tww + 16 * (e - ntab4)) : cv.frag + 16 * q;
+          if (e < tb4 || q < nf4) *reinterpret_cast<float4*>(smem + dst) = v[u];
         }
       }
       tb4 = 0;
@@ -1214,6 +1255,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
     }
     c0 = c1;
   }
+  if (a.mm && a.cnt) band_minmax_last_t<NT>(a, smem);
 }
 
 // per-sample keys of the slab partials: one workgroup per sample

@@ -17,8 +17,6 @@ namespace tb {
 
 namespace {
 
-constexpr int PT_RB = 4;  // rows a wave keeps in flight
-
 // The spikes of (sample, channel) bcl, as LDS ints: n, then per spike (kh, kw, kd, op slot).  Filled
 // by one thread (the op program lives in the kernarg segment; a per-thread copy with dynamic
 // indexing would sit in scratch).
@@ -51,75 +49,100 @@ __device__ __forceinline__ float2 cis_f(int m, int n, float sgn) {
 
 __device__ __forceinline__ int mulmod(int a, int b, int n) { return (int)(((int64_t)a * b) % n); }
 
-__device__ __forceinline__ float wave_sum(float v) {
-  return wave_reduce(v, [](float x, float y) { return x + y; });
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
 }
 
 }  // namespace
 
+// Work item = a quad: 4 consecutive columns d0 .. d0 + 3 of one row w of the slab; consecutive lanes
+// take consecutive quads (coalesced), each thread PT_QU quads per round with all their loads issued
+// first (a wave per row kept ~4 loads in flight: 230 us at C3 against ~40 for the bytes).
+constexpr int PT_QU = 4;
+// Workgroups per slab: each takes a quarter of the slab's quads, so a C3 launch is 7,680 small
+// workgroups rather than 1,920 slabs (one full round of resident workgroups plus a 7 % second round
+// took twice one round's time).
+constexpr int PT_PARTS = 4;
+
+__device__ __forceinline__ void load_quad(const float* row, int d0, int D, bool vec, float (&v)[4]) {
+  if (vec && d0 + 4 <= D) {
+    const float4 q = *reinterpret_cast<const float4*>(row + d0);
+    v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = d0 + j < D ? row[d0 + j] : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
   const PointArgs& a = kargs<PointArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int h = (int)blockIdx.x, bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int h = (int)blockIdx.x / PT_PARTS, part = (int)blockIdx.x - h * PT_PARTS, bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
   const int H = a.H, W = a.W, D = a.D, tid = (int)threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   __shared__ int act[PT_ACT];
   point_active(a, bcl, act);
   const int na = __builtin_amdgcn_readfirstlane(act[0]);
   if (na == 0) return;
-  float2* tD = reinterpret_cast<float2*>(smem);       // [na][D]  e^{-2 pi i kd d / D}
-  float2* tW = tD + TB_MAX_OPS * D;                    // [na][W]  e^{-2 pi i kw w / W}
-  double* red = reinterpret_cast<double*>(tW + TB_MAX_OPS * W);  // [4 waves][na][2]
-  for (int t = tid; t < na * D; t += POINT_NT) {
-    const int k = t / D, d = t - k * D;
-    tD[k * D + d] = cis_f(mulmod(act[3 + 4 * k], d, D), D, -1.f);
+  float2* tD = reinterpret_cast<float2*>(smem);       // [na][D + 3]  e^{-2 pi i kd d / D}, 0 past D
+  float2* tW = tD + TB_MAX_OPS * (D + 3);              // [na][W]  e^{-2 pi i kw w / W}
+  double* red = reinterpret_cast<double*>(tW + TB_MAX_OPS * W);  // [4 waves][TB_MAX_OPS][2]
+  const int Dp = D + 3;
+  for (int t = tid; t < na * Dp; t += POINT_NT) {
+    const int k = t / Dp, d = t - k * Dp;
+    tD[t] = d < D ? cis_f(mulmod(act[3 + 4 * k], d, D), D, -1.f) : make_float2(0.f, 0.f);
   }
   for (int t = tid; t < na * W; t += POINT_NT) {
     const int k = t / W, w = t - k * W;
-    tW[k * W + w] = cis_f(mulmod(act[2 + 4 * k], w, W), W, -1.f);
+    tW[t] = cis_f(mulmod(act[2 + 4 * k], w, W), W, -1.f);
   }
   __syncthreads();
   const float* xs = a.x + (int64_t)bc * a.xsbc + (int64_t)h * a.xsh;
-  float accr[TB_MAX_OPS], acci[TB_MAX_OPS];
+  const bool vec = (a.xsw & 3) == 0 && (reinterpret_cast<uintptr_t>(xs) & 15) == 0;
+  const int nq = (D + 3) / 4, nall = W * nq;
+  const int qb = (int)((int64_t)nall * part / PT_PARTS), nquad = (int)((int64_t)nall * (part + 1) / PT_PARTS);
+  const FastDiv fq = FastDiv::make(nq);
+  // float64 sums: the coefficient of a bin whose value is cancellation noise (the DC of a zero-mean
+  // channel) keeps the sign of the exact sum, as the reference's FFT mostly does
+  double accr[TB_MAX_OPS], acci[TB_MAX_OPS];
 #pragma unroll
-  for (int k = 0; k < TB_MAX_OPS; ++k) accr[k] = acci[k] = 0.f;
-  for (int w0 = wv * PT_RB; w0 < W; w0 += 4 * PT_RB) {
-    float sr[PT_RB][TB_MAX_OPS], si[PT_RB][TB_MAX_OPS];
+  for (int k = 0; k < TB_MAX_OPS; ++k) accr[k] = acci[k] = 0.0;
+  for (int q0 = qb + tid; q0 < nquad; q0 += PT_QU * POINT_NT) {
+    float v[PT_QU][4];
+    int ww[PT_QU], dd[PT_QU];
 #pragma unroll
-    for (int r = 0; r < PT_RB; ++r)
-#pragma unroll
-      for (int k = 0; k < TB_MAX_OPS; ++k) sr[r][k] = si[r][k] = 0.f;
-    for (int d = lane; d < D; d += 64) {
-      float xv[PT_RB];
-#pragma unroll
-      for (int r = 0; r < PT_RB; ++r) xv[r] = w0 + r < W ? xs[(int64_t)(w0 + r) * a.xsw + d] : 0.f;
-#pragma unroll
-      for (int k = 0; k < TB_MAX_OPS; ++k) {
-        if (k >= na) break;
-        const float2 t = tD[k * D + d];
-#pragma unroll
-        for (int r = 0; r < PT_RB; ++r) {
-          sr[r][k] = fmaf(xv[r], t.x, sr[r][k]);
-          si[r][k] = fmaf(xv[r], t.y, si[r][k]);
-        }
-      }
+    for (int u = 0; u < PT_QU; ++u) {
+      const int q = q0 + u * POINT_NT;
+      const int w = fq.div(q < nquad ? q : qb);
+      ww[u] = q < nquad ? w : -1;
+      dd[u] = 4 * ((q < nquad ? q : qb) - w * nq);
+      load_quad(xs + (int64_t)w * a.xsw, dd[u], q < nquad ? D : 0, vec, v[u]);
     }
 #pragma unroll
-    for (int r = 0; r < PT_RB; ++r) {
-      if (w0 + r >= W) break;
+    for (int u = 0; u < PT_QU; ++u) {
+      if (ww[u] < 0) break;
 #pragma unroll
       for (int k = 0; k < TB_MAX_OPS; ++k) {
         if (k >= na) break;
-        const float2 t = tW[k * W + w0 + r];
-        accr[k] += sr[r][k] * t.x - si[r][k] * t.y;
-        acci[k] += sr[r][k] * t.y + si[r][k] * t.x;
+        const float2* t = tD + k * Dp + dd[u];
+        double sr = 0.0, si = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float2 tj = t[j];
+          sr = fma((double)v[u][j], (double)tj.x, sr);
+          si = fma((double)v[u][j], (double)tj.y, si);
+        }
+        const float2 r = tW[k * W + ww[u]];
+        accr[k] += sr * (double)r.x - si * (double)r.y;
+        acci[k] += sr * (double)r.y + si * (double)r.x;
       }
     }
   }
 #pragma unroll
   for (int k = 0; k < TB_MAX_OPS; ++k) {
     if (k >= na) break;
-    const float vr = wave_sum(accr[k]), vi = wave_sum(acci[k]);
+    const double vr = wave_sum(accr[k]), vi = wave_sum(acci[k]);
     if (lane == 0) {
       red[(wv * TB_MAX_OPS + k) * 2] = vr;
       red[(wv * TB_MAX_OPS + k) * 2 + 1] = vi;
@@ -135,7 +158,7 @@ __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
     }
     double s, c;
     sincospi(2.0 * (double)mulmod(act[1 + 4 * k], h, H) / (double)H, &s, &c);  // e^{-2 pi i kh h / H}
-    double* o = a.part + ((int64_t)(bcl * H + h) * TB_MAX_OPS + act[4 + 4 * k]) * 2;
+    double* o = a.part + ((int64_t)(bcl * H * PT_PARTS + blockIdx.x) * TB_MAX_OPS + act[4 + 4 * k]) * 2;
     o[0] = vr * c + vi * s;
     o[1] = vi * c - vr * s;
   }
@@ -152,8 +175,8 @@ __global__ __launch_bounds__(64) void k_point_delta(PointArgs) {
     float2 dl = make_float2(0.f, 0.f);
     if (on) {
       double kr = 0.0, ki = 0.0;
-      for (int h = lane; h < a.H; h += 64) {
-        const double* p = a.part + ((int64_t)(bcl * a.H + h) * TB_MAX_OPS + o) * 2;
+      for (int h = lane; h < a.H * PT_PARTS; h += 64) {
+        const double* p = a.part + ((int64_t)(bcl * a.H * PT_PARTS + h) * TB_MAX_OPS + o) * 2;
         kr += p[0];
         ki += p[1];
       }
@@ -182,18 +205,18 @@ __global__ __launch_bounds__(64) void k_point_delta(PointArgs) {
 __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
   const PointArgs& a = kargs<PointArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int h = (int)blockIdx.x, bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
-  const int H = a.H, W = a.W, D = a.D, tid = (int)threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = (int)blockIdx.x / PT_PARTS, part = (int)blockIdx.x - h * PT_PARTS, bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int H = a.H, W = a.W, D = a.D, tid = (int)threadIdx.x;
   __shared__ int act[PT_ACT];
   point_active(a, bcl, act);
   const int na = __builtin_amdgcn_readfirstlane(act[0]);
-  float2* tD = reinterpret_cast<float2*>(smem);   // [na][D]  e^{+2 pi i kd d / D}
-  float2* R = tD + TB_MAX_OPS * D;                 // [na][W]  Delta / N e^{2 pi i (kh h / H + kw w / W)}
+  const int Dp = D + 3;
+  float2* tD = reinterpret_cast<float2*>(smem);   // [na][D + 3]  e^{+2 pi i kd d / D}, 0 past D
+  float2* R = tD + TB_MAX_OPS * Dp;                // [na][W]  Delta / N e^{2 pi i (kh h / H + kw w / W)}
   float* red = reinterpret_cast<float*>(R + TB_MAX_OPS * W);
-  for (int t = tid; t < na * D; t += POINT_NT) {
-    const int k = t / D, d = t - k * D;
-    tD[k * D + d] = cis_f(mulmod(act[3 + 4 * k], d, D), D, 1.f);
+  for (int t = tid; t < na * Dp; t += POINT_NT) {
+    const int k = t / Dp, d = t - k * Dp;
+    tD[t] = d < D ? cis_f(mulmod(act[3 + 4 * k], d, D), D, 1.f) : make_float2(0.f, 0.f);
   }
   for (int t = tid; t < na * W; t += POINT_NT) {
     const int k = t / W, w = t - k * W;
@@ -203,49 +226,65 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
                         ((int64_t)H * W);
     double s, c;
     sincospi(2.0 * (double)num / ((double)H * (double)W), &s, &c);
-    R[k * W + w] = make_float2((float)(dl.x * c - dl.y * s), (float)(dl.x * s + dl.y * c));
+    R[t] = make_float2((float)(dl.x * c - dl.y * s), (float)(dl.x * s + dl.y * c));
   }
   __syncthreads();
   const float* xs = a.x + (int64_t)bc * a.xsbc + (int64_t)h * a.xsh;
   float* ys = a.y + (int64_t)bc * a.ysbc + (int64_t)h * a.ysh;
   const int ncol = D + a.ypad;
+  const bool vin = (a.xsw & 3) == 0 && (reinterpret_cast<uintptr_t>(xs) & 15) == 0;
+  const bool vout = (a.ysw & 3) == 0 && (reinterpret_cast<uintptr_t>(ys) & 15) == 0;
+  const int nq = (ncol + 3) / 4, nall = W * nq;  // quads of output columns
+  const int qb = (int)((int64_t)nall * part / PT_PARTS), nquad = (int)((int64_t)nall * (part + 1) / PT_PARTS);
+  const FastDiv fq = FastDiv::make(nq);
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  for (int w0 = wv * PT_RB; w0 < W; w0 += 4 * PT_RB) {
-    for (int d = lane; d < ncol; d += 64) {
-      float v[PT_RB];
-      const bool img = d < D;
+  for (int q0 = qb + tid; q0 < nquad; q0 += PT_QU * POINT_NT) {
+    float v[PT_QU][4];
+    int ww[PT_QU], dd[PT_QU];
 #pragma unroll
-      for (int r = 0; r < PT_RB; ++r) v[r] = (img && w0 + r < W) ? xs[(int64_t)(w0 + r) * a.xsw + d] : 0.f;
-      if (img) {
+    for (int u = 0; u < PT_QU; ++u) {
+      const int q = q0 + u * POINT_NT;
+      const int w = fq.div(q < nquad ? q : qb);
+      ww[u] = q < nquad ? w : -1;
+      dd[u] = 4 * ((q < nquad ? q : qb) - w * nq);
+      load_quad(xs + (int64_t)w * a.xsw, dd[u], q < nquad ? D : 0, vin, v[u]);
+    }
 #pragma unroll
-        for (int k = 0; k < TB_MAX_OPS; ++k) {
-          if (k >= na) break;
-          const float2 t = tD[k * D + d];
+    for (int u = 0; u < PT_QU; ++u) {
+      if (ww[u] < 0) break;
+      const int d0 = dd[u];
 #pragma unroll
-          for (int r = 0; r < PT_RB; ++r) {
-            if (w0 + r < W) {
-              const float2 q = R[k * W + w0 + r];
-              v[r] += q.x * t.x - q.y * t.y;
-            }
-          }
+      for (int k = 0; k < TB_MAX_OPS; ++k) {
+        if (k >= na) break;
+        const float2 r = R[k * W + ww[u]];
+        const float2* t = tD + k * Dp + (d0 < D ? d0 : 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float2 tj = t[j];
+          v[u][j] += d0 < D ? r.x * tj.x - r.y * tj.y : 0.f;
         }
-#pragma unroll
-        for (int r = 0; r < PT_RB; ++r)
-          if (w0 + r < W) {
-            lo = fminf(lo, v[r]);
-            hi = fmaxf(hi, v[r]);
-          }
       }
 #pragma unroll
-      for (int r = 0; r < PT_RB; ++r)
-        if (w0 + r < W) ys[(int64_t)(w0 + r) * a.ysw + d] = v[r];
+      for (int j = 0; j < 4; ++j)
+        if (d0 + j < D) {
+          lo = fminf(lo, v[u][j]);
+          hi = fmaxf(hi, v[u][j]);
+        }
+      float* yr = ys + (int64_t)ww[u] * a.ysw;
+      if (vout && d0 + 4 <= ncol) {
+        *reinterpret_cast<float4*>(yr + d0) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (d0 + j < ncol) yr[d0 + j] = v[u][j];
+      }
     }
   }
   if (a.mm) block_minmax_atomic<POINT_NT>(lo, hi, red, a.mm + 2 * (bc / a.C));
 }
 
 bool point_program(const tb_sample_ops& s, int H, int W, int D) {
-  if (s.n < 1 || (size_t)TB_MAX_OPS * (W + D) * sizeof(float2) > 65536) return false;
+  if (s.n < 1 || (size_t)TB_MAX_OPS * (W + D + 3) * sizeof(float2) > 65536) return false;
   for (int o = 0; o < s.n; ++o)
     if (s.op[o].kind != TB_OP_SPIKE) return false;
   const int n[3] = {H, W, D};
@@ -264,17 +303,17 @@ bool point_program(const tb_sample_ops& s, int H, int W, int D) {
 }
 
 size_t point_workspace_bytes(int H, int bc) {
-  return (size_t)bc * H * TB_MAX_OPS * 2 * sizeof(double) + (size_t)bc * TB_MAX_OPS * 2 * sizeof(float) + 256;
+  return (size_t)bc * H * PT_PARTS * TB_MAX_OPS * 2 * sizeof(double) + (size_t)bc * TB_MAX_OPS * 2 * sizeof(float) + 512;
 }
 
 hipError_t launch_point(const PointArgs& a, hipStream_t st, int stage) {
-  const size_t tabs = (size_t)TB_MAX_OPS * (a.D + a.W) * sizeof(float2);
+  const size_t tabs = (size_t)TB_MAX_OPS * (a.D + 3 + a.W) * sizeof(float2);
   if (stage == 0) {
-    hipLaunchKernelGGL(k_point_dft, dim3(a.H, a.nbc), dim3(POINT_NT), tabs + 4 * TB_MAX_OPS * 2 * sizeof(double), st, a);
+    hipLaunchKernelGGL(k_point_dft, dim3(a.H * PT_PARTS, a.nbc), dim3(POINT_NT), tabs + 4 * TB_MAX_OPS * 2 * sizeof(double), st, a);
   } else if (stage == 1) {
     hipLaunchKernelGGL(k_point_delta, dim3(a.nbc), dim3(64), 0, st, a);
   } else {
-    hipLaunchKernelGGL(k_point_apply, dim3(a.H, a.nbc), dim3(POINT_NT), tabs + 2 * POINT_NT / 64 * sizeof(float), st, a);
+    hipLaunchKernelGGL(k_point_apply, dim3(a.H * PT_PARTS, a.nbc), dim3(POINT_NT), tabs + 2 * POINT_NT / 64 * sizeof(float), st, a);
   }
   return hipGetLastError();
 }

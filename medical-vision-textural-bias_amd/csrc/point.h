@@ -25,7 +25,7 @@ struct PointArgs {
   int64_t ysbc, ysh, ysw;
   int ypad, bc0, C, nbc;  // bc0 = first sample * C (absolute); ops.s[i] = the run's i-th sample
   uint32_t* mm;           // per-sample min/max keys (atomic; reset by the caller) or null
-  double* part;           // [nbc][H][TB_MAX_OPS][2] per-slab coefficient sums
+  double* part;           // [nbc][H * parts][TB_MAX_OPS][2] per-workgroup coefficient sums
   float* delta;           // [nbc][TB_MAX_OPS][2] Delta_j / N (zero for ops that skip the channel)
   BatchOps ops;
 };

@@ -739,11 +739,12 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     }
     ma.T16 = ws + wl.off_t16;
     ma.tds = p->tds;
+    ma.cnt = reinterpret_cast<uint32_t*>(ws + wl.off_cnt);
     TB_HIP(tb::launch_band_mid(ma, st));
   }
   {
-    // the events bracket k_band_inv alone (the per-sample min/max reduction after it runs untimed),
-    // so the pass time is that kernel's duration, as rocprofv3 reports it
+    // the events bracket k_band_inv16 (with the per-sample min/max keys from its last workgroup) or
+    // k_band_inv alone (k_band_minmax after it runs untimed): the kernel's duration, as rocprofv3 reports it
     Timer t(2, st, abytes + (double)nbc * H * W * (D + y_pad) * 4.0, g.cat ? "k_band_inv16" : "k_band_inv");
     BandInvArgs ia;
     std::memset(&ia, 0, sizeof(ia));
@@ -767,10 +768,12 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.T16 = ws + wl.off_t16;
     ia.g = g;
     ia.diag = (g_band_diag >> 8) & 0xffff;
+    ia.cnt = g.cat ? reinterpret_cast<uint32_t*>(ws + wl.off_cnt) : nullptr;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
     TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
   }
-  if (minmax) TB_HIP(tb::launch_band_minmax(reinterpret_cast<float2*>(ws + wl.off_mmp), minmax, b0 * C, C, nbc, H, W, st));
+  // the split-f16 C' writes the keys from its last workgroup; the f32 C' leaves them to k_band_minmax
+  if (minmax && !g.cat) TB_HIP(tb::launch_band_minmax(reinterpret_cast<float2*>(ws + wl.off_mmp), minmax, b0 * C, C, nbc, H, W, st));
   return TB_OK;
 }
 
@@ -799,7 +802,7 @@ static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float*
   a.y = y, a.ysbc = ys[0], a.ysh = ys[1], a.ysw = ys[2];
   a.ypad = y_pad, a.bc0 = b0 * C, a.C = C, a.nbc = nbc, a.mm = minmax;
   a.part = reinterpret_cast<double*>(ws);
-  a.delta = reinterpret_cast<float*>(ws + (((size_t)bcn_total * H * TB_MAX_OPS * 2 * sizeof(double) + 255) & ~(size_t)255));
+  a.delta = reinterpret_cast<float*>(ws + ((tb::point_workspace_bytes(H, bcn_total) - (size_t)bcn_total * TB_MAX_OPS * 8 - 256) & ~(size_t)255));
   for (int i = 0; i < nb; ++i) a.ops.s[i] = ops[b0 + i];
   const double vox = (double)nbc * H * W * D;
   {

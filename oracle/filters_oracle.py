@@ -111,6 +111,18 @@ def plane_waves(x: np.ndarray, idx: Sequence[int], intensity: float,
     return inv_shift_fourier(k2, 3)
 
 
+def polar_roundtrip(x: np.ndarray) -> np.ndarray:
+    """The reference's float32 polar round trip of every coefficient with nothing changed
+    (filters_and_operators.py:383-391: log|k|, angle, exp(log) * exp(i angle), inverse `.real`): its
+    distance from x is the rounding floor of any plane-wave / spike output of that path (1.4e-5 of
+    max|x| for a raw 240x240x155 volume; after a low-pass almost every coefficient is exactly 0)."""
+    k = shift_fourier(x, 3)
+    with np.errstate(divide="ignore"):
+        la = np.log(np.abs(k)).astype(np.float32)
+    ph = np.angle(k).astype(np.float32)
+    return inv_shift_fourier((np.exp(la) * np.exp(1j * ph)).astype(np.complex64), 3)
+
+
 # filters_and_operators.py:503-515 (WrapArtifact.__call__): odd shifted indices scaled by alpha per axis
 def wrap_artifact(x: np.ndarray, alpha: float) -> np.ndarray:
     k = shift_fourier(x, 3)

@@ -2,8 +2,11 @@
 (RandPlaneWaves_ellipsoid, filters_and_operators.py:370-393) and KSpaceSpikeNoise spikes (:906-983)
 against the full-spectrum passes (same program, tb_set_point_plans(0)) and the numpy oracle.
 
-Tolerances: closed form vs full passes max|d| / max|y| <= 2e-6; vs oracle <= 1e-5 (north_star);
-zero padding and min/max keys bit-exact against the output.
+Tolerances: closed form vs full passes max|d| / max|y| <= 2e-6; vs oracle <= 1e-5 (north_star), or
+1.5x the reference's own polar round-trip floor where that is larger (its float32 log / angle / exp of
+EVERY coefficient moves a raw 240x240x155 volume by 1.4e-5 of max|x| against float64 -- no exact
+method can be closer to it than that; ``O.polar_roundtrip``); zero padding and min/max keys
+bit-exact against the output.
 """
 import numpy as np
 import pytest
@@ -72,8 +75,10 @@ def test_planes_closed_form(rt, shape):
     assert (yp - yf).abs().max().item() / yf.abs().max().item() < 2e-6
     check_keys(rt, yp, mmp, sp[-1])
     for b in range(shape[0]):
-        ref = O.plane_waves(x[b].cpu().numpy(), idxs[b % 2], 12.0 + b)
-        assert relerr(yp[b, ..., : sp[-1]].cpu().numpy(), ref) < 1e-5
+        xb = x[b].cpu().numpy()
+        ref = O.plane_waves(xb, idxs[b % 2], 12.0 + b)
+        tol = max(1e-5, 1.5 * relerr(O.polar_roundtrip(xb), xb))
+        assert relerr(yp[b, ..., : sp[-1]].cpu().numpy(), ref) < tol
 
 
 @pytest.mark.parametrize("where", ["dc", "nyquist", "kd0", "override"])
@@ -150,3 +155,4 @@ def test_planes_in_place_strided(rt):
     torch.cuda.synchronize()
     ref = O.plane_waves(x0[1].cpu().numpy(), (4, 6, 7), 10.0)
     assert relerr(view[1].cpu().numpy(), ref) < 1e-5
+
