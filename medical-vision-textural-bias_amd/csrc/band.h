@@ -126,6 +126,7 @@ struct BandInvArgs {
   const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   const void* T16;  // g.cat: split-f16 synthesis-table fragments (k_band_tab16)
   uint32_t* cnt;    // g.cat: arrival counter (zeroed by pass B'); the last workgroup writes the keys
+  int stagger;      // g.cat: start offset of wave w, (w / 4) * stagger * 512 cycles (TEXBIAS_INV16_STAGGER)
 };
 
 // Pass A': LDS row pitch of a staged strip.  Odd D: D (the strip is one contiguous run, 16-B

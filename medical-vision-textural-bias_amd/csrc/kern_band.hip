@@ -969,30 +969,31 @@ __device__ void band_tab16(const BandMidArgs& a, int t) {
 }
 
 // Per-sample min/max keys without a launch of their own: every workgroup of pass C' counts itself
-// in after its partials are stored (release fence); the last one to arrive (acquire fence, loads at
-// device scope so no stale L1 line is read) reduces the launch's partials as k_band_minmax does.
+// in after its partials are stored (store_partial / arrive_last, kernels.h); the last one to arrive
+// reduces the launch's partials as k_band_minmax does.
 template <int NT>
 __device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
   __shared__ int last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(a.cnt, 1u) == gridDim.x - 1;
-  }
+  __syncthreads();  // every wave's partials issued (store_partial)
+  if (threadIdx.x == 0) last = arrive_last(a.cnt, gridDim.x);
   __syncthreads();
   if (!last) return;
-  __threadfence();
   float* red = reinterpret_cast<float*>(smem);
   const int ntw = (a.pl.W + 31) / 32, nb = a.nbc / a.C;
   const int64_t n = (int64_t)a.C * a.pl.H * ntw;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int b = 0; b < nb; ++b) {
-    const uint64_t* p = reinterpret_cast<const uint64_t*>(a.mmp + (int64_t)b * n);
+    const float2* p = a.mmp + (int64_t)b * n;
     float lo = 3.402823466e38f, hi = -3.402823466e38f;
-    for (int64_t i = threadIdx.x; i < n; i += NT) {
-      const uint64_t v = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lo = fminf(lo, __uint_as_float((uint32_t)v));
-      hi = fmaxf(hi, __uint_as_float((uint32_t)(v >> 32)));
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * NT) {
+      float2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i0 + u * NT < n ? load_partial(p + i0 + u * NT) : make_float2(lo, hi);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        lo = fminf(lo, v[u].x);
+        hi = fmaxf(hi, v[u].y);
+      }
     }
     lo = wave_min(lo);
     hi = wave_max(hi);
@@ -1102,6 +1103,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
     }
     __syncthreads();
     if (diag & 32) return;
+    if (c0 == ub)
+      for (int i = (wv >> 2) * a.stagger; i > 0; --i) __builtin_amdgcn_s_sleep(8);
     for (int un = c0 + ((wv - ((c0 - ub) % NW) + NW) % NW); un < c1; un += NW) {  // (un - ub) % NW == wave
       const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
       const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
@@ -1250,7 +1253,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
       if (a.mm) {
         lo = wave_min(lo);
         hi = wave_max(hi);
-        if (lane == 0) a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
+        if (lane == 0) {
+          if (a.cnt)
+            store_partial(a.mmp + (int64_t)slab * ntw + tw_, make_float2(lo, hi));
+          else
+            a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
+        }
       }
     }
     c0 = c1;

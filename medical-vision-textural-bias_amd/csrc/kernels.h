@@ -154,6 +154,26 @@ __device__ __forceinline__ void block_minmax_atomic(float lo, float hi, float* r
   }
 }
 
+// Last-arriver hand-off between the workgroups of one launch (they may sit on different XCDs, whose
+// L2s are not coherent) without __threadfence(): its agent-scope release writes back the XCD's whole
+// L2 (buffer_wbl2) from every workgroup -- 12 us at the end of pass C', 100+ us over the 2,048
+// workgroups of the closed-form apply.  Instead the partial goes out as a device-scope atomic store,
+// the workgroup waits for it (workgroup-scope release: s_waitcnt only) and counts itself in with a
+// device-scope atomic; the last one reads the partials with device-scope atomic loads.
+__device__ __forceinline__ void store_partial(float2* p, float2 v) {
+  const uint64_t u = ((uint64_t)__float_as_uint(v.y) << 32) | (uint64_t)__float_as_uint(v.x);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 load_partial(const float2* p) {
+  const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float2(__uint_as_float((uint32_t)u), __uint_as_float((uint32_t)(u >> 32)));
+}
+// count the calling thread's workgroup in after its store_partial calls; true for the last of `total`
+__device__ __forceinline__ bool arrive_last(uint32_t* cnt, uint32_t total) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+}
+
 // Raise a kernel's dynamic-LDS limit to `bytes` (the launch's dynamic LDS) once per kernel: the
 // kernels share one function type, so the cache is keyed by the kernel's address.  The request is
 // the launch's own size -- 160 KiB plus a kernel's static LDS would be refused.

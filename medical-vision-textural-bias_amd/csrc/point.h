@@ -16,6 +16,7 @@
 namespace tb {
 
 constexpr int POINT_NT = 256;
+constexpr int POINT_WG = 2048;  // most workgroups a launch uses (8 per CU)
 
 struct PointArgs {
   int H, W, D;
@@ -24,15 +25,36 @@ struct PointArgs {
   float* y;
   int64_t ysbc, ysh, ysw;
   int ypad, bc0, C, nbc;  // bc0 = first sample * C (absolute); ops.s[i] = the run's i-th sample
-  uint32_t* mm;           // per-sample min/max keys (atomic; reset by the caller) or null
-  double* part;           // [nbc][H * parts][TB_MAX_OPS][2] per-workgroup coefficient sums
+  int parts;              // workgroups per volume-channel (each a contiguous range of the volume's quads)
+  int parts_apply;        // the same for k_point_apply (its own occupancy)
+  int namax;              // most spikes any volume-channel of the launch has (twiddle-table stride)
+  uint32_t* mm;           // per-sample min/max keys (written by the last apply workgroup) or null
+  double* part;           // [nbc][parts][TB_MAX_OPS][2] per-workgroup coefficient sums
   float* delta;           // [nbc][TB_MAX_OPS][2] Delta_j / N (zero for ops that skip the channel)
+  float2* mmp;            // [nbc][parts] per-workgroup (min, max) of the output
+  uint32_t* cnt;          // arrival counter of the apply workgroups (zeroed by k_point_delta)
   BatchOps ops;
 };
 
+// workspace carve for nbc volume-channels
+struct PointWs {
+  size_t part, delta, mmp, cnt, total;
+};
+inline PointWs point_ws(int nbc) {
+  PointWs w;
+  w.part = 0;  // nbc * parts <= POINT_WG + nbc: regions sized for that, so the carve grows with nbc
+  w.delta = ((size_t)(POINT_WG + nbc) * TB_MAX_OPS * 16 + 255) & ~(size_t)255;
+  w.mmp = (w.delta + (size_t)nbc * TB_MAX_OPS * 8 + 255) & ~(size_t)255;
+  w.cnt = (w.mmp + (size_t)(POINT_WG + nbc) * 8 + 255) & ~(size_t)255;
+  w.total = w.cnt + 256;
+  return w;
+}
+
 // Every op is a spike and no two touch (same or conjugate frequency in an overlapping channel).
 bool point_program(const tb_sample_ops& s, int H, int W, int D);
-size_t point_workspace_bytes(int H, int bc);
+// Sets a.parts / a.parts_apply: one round of resident workgroups per launch (ncu x occupancy, at most
+// POINT_WG), split evenly over the launch's volume-channels.
+void point_grid(PointArgs& a, int ncu);
 hipError_t launch_point(const PointArgs& a, hipStream_t st, int stage);  // stage 0: K, 1: Delta, 2: apply
 
 }  // namespace tb

@@ -520,6 +520,13 @@ static bool g_inv16 = [] {
   const char* e = std::getenv("TEXBIAS_INV16");
   return !(e && e[0] == '0');
 }();
+// Pass C' (split f16): the 4 waves a SIMD holds start their first unit this many 512-cycle sleeps
+// apart (wave w: (w / 4) * stagger), so their compute and store phases interleave instead of running
+// in lockstep after the prologue barrier.  TEXBIAS_INV16_STAGGER overrides.
+static int g_inv16_stagger = [] {
+  const char* e = std::getenv("TEXBIAS_INV16_STAGGER");
+  return e ? (int)std::strtol(e, nullptr, 0) : 0;
+}();
 // measurement only: TEXBIAS_BAND_DIAG=0xIIFF skips stages of A' (FF) / C' (II); results invalid
 static int g_band_diag = [] {
   const char* e = std::getenv("TEXBIAS_BAND_DIAG");
@@ -768,6 +775,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.T16 = ws + wl.off_t16;
     ia.g = g;
     ia.diag = (g_band_diag >> 8) & 0xffff;
+    ia.stagger = g_inv16_stagger;
     ia.cnt = g.cat ? reinterpret_cast<uint32_t*>(ws + wl.off_cnt) : nullptr;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
     TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
@@ -791,7 +799,7 @@ static int run_generic(const tb_plan* p, const float* x, const int64_t* xs, floa
 }
 
 static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
-                     char* ws, int bcn_total, int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax,
+                     char* ws, int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax,
                      hipStream_t st) {
   const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
   const int nbc = nb * C;
@@ -801,16 +809,28 @@ static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float*
   a.x = x, a.xsbc = xs[0], a.xsh = xs[1], a.xsw = xs[2];
   a.y = y, a.ysbc = ys[0], a.ysh = ys[1], a.ysw = ys[2];
   a.ypad = y_pad, a.bc0 = b0 * C, a.C = C, a.nbc = nbc, a.mm = minmax;
-  a.part = reinterpret_cast<double*>(ws);
-  a.delta = reinterpret_cast<float*>(ws + ((tb::point_workspace_bytes(H, bcn_total) - (size_t)bcn_total * TB_MAX_OPS * 8 - 256) & ~(size_t)255));
-  for (int i = 0; i < nb; ++i) a.ops.s[i] = ops[b0 + i];
+  const tb::PointWs wl = tb::point_ws(nbc);
+  a.part = reinterpret_cast<double*>(ws + wl.part);
+  a.delta = reinterpret_cast<float*>(ws + wl.delta);
+  a.mmp = reinterpret_cast<float2*>(ws + wl.mmp);
+  a.cnt = reinterpret_cast<uint32_t*>(ws + wl.cnt);
+  a.namax = 1;
+  for (int i = 0; i < nb; ++i) {
+    a.ops.s[i] = ops[b0 + i];
+    for (int c = 0; c < C; ++c) {
+      int n = 0;
+      for (int o = 0; o < ops[b0 + i].n; ++o) n += ops[b0 + i].op[o].chan < 0 || ops[b0 + i].op[o].chan == c;
+      a.namax = n > a.namax ? n : a.namax;
+    }
+  }
+  tb::point_grid(a, p->ncu);
   const double vox = (double)nbc * H * W * D;
   {
     Timer t(0, st, vox * 4.0, "k_point_dft");
     TB_HIP(tb::launch_point(a, st, 0));
   }
   {
-    Timer t(1, st, (double)nbc * H * TB_MAX_OPS * 16.0, "k_point_delta");
+    Timer t(1, st, (double)nbc * a.parts * TB_MAX_OPS * 16.0, "k_point_delta");
     TB_HIP(tb::launch_point(a, st, 1));
   }
   {
@@ -862,7 +882,7 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
       while (j < nb && route(b0 + j) == run.route) ++j;
       run.s0 = b0 + i;
       run.s1 = b0 + j;
-      if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_workspace_bytes(p->dev.H, B * C)) {
+      if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_ws(B * C).total) {
         bool pt = true;
         for (int s = run.s0; s < run.s1 && pt; ++s) pt = tb::point_program(ops[s], p->dev.H, p->dev.W, p->dev.D);
         if (pt) run.route = RUN_POINT;
@@ -884,7 +904,7 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     if (run.route == RUN_COPY)
       rc = run_copy(p, x, xs, y, ys, y_pad, run.s0, nb, C, minmax, st);
     else if (run.route == RUN_POINT)
-      rc = run_point(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, run.s0, nb, C, ops, minmax, st);
+      rc = run_point(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), run.s0, nb, C, ops, minmax, st);
     else if (run.route == RUN_BAND)
       rc = run_band(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), B * C, run.s0, nb, C, ops, run.g, run.sp, minmax,
                     st);
