@@ -1210,25 +1210,44 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
           if (wr < W) {
             float* yr = yb + (int64_t)wr * a.sw;
             const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
+            f32x4 v[4];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int d0 = 32 * nt + 8 * g + 4 * hl;
-              f32x4 v;
+            for (int g = 0; g < 4; ++g)
 #pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = acc[4 * g + q] * inv;  // exactly 0 past D (T = 0 there)
-              if (vec && d0 + 4 <= ncolo) {
-                *reinterpret_cast<f32x4*>(yr + d0) = v;
-              } else {
+              for (int q = 0; q < 4; ++q) v[g][q] = acc[4 * g + q] * inv;  // exactly 0 past D (T = 0 there)
+            if (vec && 32 * nt + 32 <= ncolo) {  // wave-uniform: the whole tile lies inside the row
+#pragma unroll
+              for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(yr + 32 * nt + 8 * g + 4 * hl) = v[g];
+            } else {
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const int d0 = 32 * nt + 8 * g + 4 * hl;
+                if (vec && d0 + 4 <= ncolo) {
+                  *reinterpret_cast<f32x4*>(yr + d0) = v[g];
+                } else {
+#pragma unroll
+                  for (int q = 0; q < 4; ++q)
+                    if (d0 + q < ncolo) yr[d0 + q] = v[g][q];
+                }
+              }
+            }
+            if (32 * nt + 32 <= D) {  // wave-uniform: every column an image column -- min3/max3 chains
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  lo = fminf(lo, v[g][q]);
+                  hi = fmaxf(hi, v[g][q]);
+                }
+            } else {
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                  if (d0 + q < ncolo) yr[d0 + q] = v[q];
-              }
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (d0 + q < D) {
-                  lo = fminf(lo, v[q]);
-                  hi = fmaxf(hi, v[q]);
-                }
+                  if (32 * nt + 8 * g + 4 * hl + q < D) {
+                    lo = fminf(lo, v[g][q]);
+                    hi = fmaxf(hi, v[g][q]);
+                  }
             }
           }
           continue;
