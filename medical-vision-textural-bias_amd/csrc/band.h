@@ -199,10 +199,15 @@ TB_HD BandInv16Carve band_inv16_carve(const BandGeo& g, int W, int slots = BAND_
 
 // Pass B' (k_band_hcol): 16 box columns per workgroup; LDS = their partial sums for every slab (+1
 // zero row), the H twiddles, the [C; S] product tiles, the G rows of the inverse.
+#ifndef TB_HC_NW
+#define TB_HC_NW 8  // waves per pass-B' workgroup (they split h): the launch is only ncol / 16 x nbc
+                    // workgroups (168 at C3), so its latency wants the waves (4: 33.7 us with B2', 8: 30.8)
+#endif
+constexpr int BAND_HC_NW = TB_HC_NW;
 TB_HD size_t band_hc_lds(int H, int KH) {
   const int mt = KH + 1 <= 16 ? 1 : 2;
   return (size_t)(H + 1) * 16 * 8 + (size_t)H * 8 + (size_t)mt * 1024 * 4 + (size_t)2 * (KH + 1) * 32 * 4 +
-         (size_t)4 * mt * 1024 * 4;  // + the 4 waves' forward sums
+         (size_t)BAND_HC_NW * mt * 1024 * 4;  // + the waves' forward sums
 }
 
 // workspace carve (bytes from the workspace base) for `bcn` volume-channels

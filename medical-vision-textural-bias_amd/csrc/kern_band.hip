@@ -370,7 +370,6 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
 //   inverse  Z(h, col) = [cos sin](h, (kh, t)) . G((kh, t), col) per 32-slab tile, the tiles dealt
 //            to the waves, written over the slab's first partial-sum slot (own columns only).
 constexpr int BAND_HC_CB = 16;  // box columns per workgroup
-constexpr int BAND_HC_NW = 4;   // waves per workgroup (they split h)
 template <int MT>               // 32-row tiles of [C; S]: KH + 1 <= 16 MT
 __global__ __launch_bounds__(64 * BAND_HC_NW) void k_band_hcol(BandMidArgs) {
   const BandMidArgs& a = kargs<BandMidArgs>();
