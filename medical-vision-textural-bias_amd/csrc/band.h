@@ -64,6 +64,9 @@ TB_HD int band_rows(const BandGeo& g) { return 2 * (g.cat ? g.NDk + g.PT : g.KS)
 // strips [w T / G, (w + 1) T / G).  G <= T / ceil(nst / 2), so a slab spans at most 3 waves.
 // (T + 1) G < 2^32 (host-checked): 32-bit arithmetic.
 constexpr int BAND_FWD_SEGS = 3;
+// Longest D a band plan takes (the passes stage D-long rows in LDS well below this); plans past it
+// build no band tables (tds, tbt: O(D^2) entries).
+constexpr int BAND_MAX_D = 4096;
 constexpr int BAND_FWD_ROWS = 16;  // rows per strip (one per lane of a 16x16x4 MFMA row)
 struct FwdSplit {
   uint32_t T, G, nst;
@@ -80,8 +83,6 @@ struct BandFwdArgs {
   const float* x;
   int64_t sbc, sh, sw;
   cf* P;            // [bc][H][BAND_FWD_SEGS][ncol] partial sums (bc absolute)
-  const float2* tdf;  // [d][NKP] = (cos, sin)(2 pi kd d / D), d in [0, D/2]
-  int NKP;
   int bc0, nbc;
   BandGeo g;
   int diag;         // measurement only (TEXBIAS_BAND_DIAG): skip stages, results invalid

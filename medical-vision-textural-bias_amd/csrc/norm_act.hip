@@ -243,14 +243,18 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_stats(const float* __restri
                                                            double* __restrict__ acc_a, int64_t S, int vec) {
   const Chunk c = chunk_of(S);
   const float mean = mean_in[blockIdx.y], rstd = rstd_in[blockIdx.y], a = *aw;
-  float s1 = 0.f, s2 = 0.f, sa = 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  // the PReLU weight gradient is one scalar over every voxel of the layer whose terms cancel to
+  // 1e-6..1e-8 of their magnitude: its per-thread sum runs in float64, so this kernel adds nothing to
+  // the float32 noise its input gradient already carries (tests/test_gpu_train_prod.py)
+  double sa = 0.0;
   auto visit = [&](float xv, float gv) {
     const float z = (xv - mean) * rstd;
     const bool pos = z > 0.f;
     const float g = pos ? gv : a * gv;
     s1 += g;
     s2 += g * z;
-    sa += pos ? 0.f : gv * z;
+    sa += pos ? 0.0 : (double)gv * (double)z;
   };
   if (vec) {
     const float4* px = reinterpret_cast<const float4*>(x + c.base + c.begin);
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_stats(const float* __restri
   } else {
     for (int64_t i = c.begin + threadIdx.x; i < c.end; i += NT) visit(x[c.base + i], dy[c.base + i]);
   }
-  double r[3] = {(double)s1, (double)s2, (double)sa};
+  double r[3] = {(double)s1, (double)s2, sa};
   __shared__ double red[3][NT / 64];
 #pragma unroll
   for (int k = 0; k < 3; ++k) r[k] = wave_sum(r[k]);

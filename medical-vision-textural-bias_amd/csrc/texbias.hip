@@ -259,8 +259,6 @@ struct tb_plan {
   int ncu = 256;         // compute units (grid of the persistent compiled-plan slab kernels)
   bool ct_slab = false;  // (W, D) has a compile-time slab plan (slab_ct.h)
   bool ct_tile = false;  // H has a compile-time pass-B plan (kspace_ct.h)
-  float2* tdf = nullptr; // band pass A': [D/2 + 1][NKP] (cos, sin)(2 pi kd d / D)
-  int NKP = 0;
   float* tds = nullptr;  // band pass C': [D/2 + 1][2][NCOLS] cos / sin(2 pi kd d / D), d < D/2 + 1, else 0
   float* tbt = nullptr;  // band pass A': [2][KSd][2][64] B fragments of the folded D product
   bool generic = false;  // full-spectrum route on the direct-DFT fallback (kern_generic.hip)
@@ -385,26 +383,8 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   p->dev.rev_d = reinterpret_cast<const int*>(d + off_i[0]);
   p->dev.irev_h = reinterpret_cast<const int*>(d + off_i[1]);
   p->dev.irev_w = reinterpret_cast<const int*>(d + off_i[2]);
-  {  // pruned-DFT twiddles of the band-limited pass A' (kd padded past any wave's kd group)
-    const int Ld = D / 2 + 1;
-    int nkp = Ld > 32 ? Ld : 32;
-    nkp = (nkp + 7) & ~7;
-    std::vector<float2> t((size_t)Ld * nkp);
-    for (int d = 0; d < Ld; ++d)
-      for (int k = 0; k < nkp; ++k) {
-        const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)k * d) % D) / (double)D;
-        t[(size_t)d * nkp + k] = make_float2((float)std::cos(ang), (float)std::sin(ang));
-      }
-    if (hipMalloc(reinterpret_cast<void**>(&p->tdf), t.size() * sizeof(float2)) != hipSuccess ||
-        hipMemcpy(p->tdf, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
-      if (p->tdf) (void)hipFree(p->tdf);
-      (void)hipFree(p->dmem);
-      delete p;
-      return hip_fail(hipGetLastError());
-    }
-    p->NKP = nkp;
-  }
-  {  // folded synthesis table (pass C') and the D-product B fragments (pass A'), double precision
+  if (D <= BAND_MAX_D) {  // folded synthesis table (pass C') and the D-product B fragments (pass A'),
+                         // double precision; plans no band route can take (D > BAND_MAX_D) skip them
     const int Dh = D / 2 + 1, ncols = 32 * ((Dh + 31) / 32), KSd = (Dh + 3) / 4;
     std::vector<float> ts((size_t)Dh * 2 * ncols, 0.f), tb((size_t)2 * KSd * 2 * 64, 0.f);
     for (int k = 0; k < Dh; ++k)
@@ -439,7 +419,6 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
 int tb_plan_destroy(tb_plan* plan) {
   if (!plan) return TB_OK;
   if (plan->dmem) (void)hipFree(plan->dmem);
-  if (plan->tdf) (void)hipFree(plan->tdf);
   if (plan->tds) (void)hipFree(plan->tds);
   if (plan->tbt) (void)hipFree(plan->tbt);
   delete plan;
@@ -633,7 +612,8 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   g.cat = (g_inv16 && g.NDk + ptot <= 32) ? 1 : 0;
   g.PT = g.cat ? ptot : 0;
   g.NTD = (D + y_pad + 31) / 32;
-  if (2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || KW >= 32 || KH > BAND_MAX_KH) return false;
+  if (D > BAND_MAX_D || 2 * KH + 1 > H || 2 * KW + 1 > W || g.NDk > BAND_MAX_NDK || KW >= 32 || KH > BAND_MAX_KH)
+    return false;
   if (g.ncol > BAND_MAX_ZCOL || W > 1024 || band_hc_lds(H, KH) > 160000) return false;
   if (2 * g.KS > 64 || g.KS > 32) return false;  // pass C' holds V in at most two 32-row MFMA tiles
   // worth it only when the box is a small part of the half spectrum
@@ -713,7 +693,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
   tb::FwdSplit split{};
   {
     Timer t(0, st, (double)nbc * H * W * D * 4.0 + pbytes, "k_band_fwd");
-    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, p->tdf, p->NKP, bc0, nbc, g, g_band_diag & 0xff, p->tbt};
+    BandFwdArgs fa{p->dev, x, xs[0], xs[1], xs[2], P, bc0, nbc, g, g_band_diag & 0xff, p->tbt};
     // 16-B vector strips: contiguous rows, and 16-B aligned strips where the compiled even-D staging needs them
     const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (xs[0] & 3) == 0 && (xs[1] & 3) == 0;
     fa.vec = xs[2] == D && ((D & 1) || al || !tb::band_fwd_use_ct(D, g.NDk <= 16 ? 1 : 2));

@@ -249,3 +249,41 @@ def test_band_inv16_falls_back_past_32_rows(rt):
     names = rt.pass_stats()[3]
     rt.set_pass_timing(False)
     assert names[2] == "k_band_inv", names
+
+
+@pytest.mark.parametrize("layout", ["ten_lowpass", "copy_then_band", "mixed_routes"])
+def test_band_runs_at_nonzero_offset(rt, layout):
+    """Band runs that do not start at sample 0 (bc0 != 0): a batch past TB_MAX_BATCH (second launch
+    group), a band run after an identity sample, and band / closed-form / full / copy runs
+    interleaved -- against the full-spectrum passes, with every sample's min/max keys exact."""
+    torch.manual_seed(11)
+    C, sp = 2, (24, 20, 15)
+    lp = [K.disk_op(4.5, False), K.wrap_op(0.5)]
+    if layout == "ten_lowpass":
+        progs = [[K.disk_op(4.0 + 0.25 * b, False), K.wrap_op(0.5)] for b in range(10)]
+    elif layout == "copy_then_band":
+        progs = [[], lp, lp]
+    else:
+        progs = [lp, [spike((5, 7, 3), sp, 9.0)], [K.wrap_op(0.25)], lp, [], lp]
+    B = len(progs)
+    x = torch.randn((B, C) + sp, device="cuda")
+    mm_b = torch.empty((B, 2), dtype=torch.int32, device="cuda")
+    mm_f = torch.empty((B, 2), dtype=torch.int32, device="cuda")
+    yb = rt.kspace_filter(x, 3, progs, C, pad=3, minmax=mm_b)
+    try:
+        rt.set_band_plans(False)
+        rt.set_point_plans(False)
+        yf = rt.kspace_filter(x, 3, progs, C, pad=3, minmax=mm_f)
+    finally:
+        rt.set_band_plans(True)
+        rt.set_point_plans(True)
+    torch.cuda.synchronize()
+    assert torch.all(yb[..., sp[-1]:] == 0)
+    assert (yb - yf).abs().max().item() / yf.abs().max().item() < 2e-6
+    v = yb[..., : sp[-1]].reshape(B, -1)
+    m = rt.keys_to_float(mm_b)
+    np.testing.assert_array_equal(m[:, 0], v.min(1).values.cpu().numpy())
+    np.testing.assert_array_equal(m[:, 1], v.max(1).values.cpu().numpy())
+    for b, p in enumerate(progs):
+        if not p:
+            assert torch.equal(yb[b, ..., : sp[-1]], x[b])
