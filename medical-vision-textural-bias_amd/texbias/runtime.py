@@ -19,7 +19,7 @@ from ._lib import TexbiasError, check, lib
 from .kprog import Geometry, geometry, split_program
 
 _plans: Dict[Tuple[int, int, int, int], "Plan"] = {}
-_ws: Dict[int, torch.Tensor] = {}
+_ws: Dict[Tuple[int, int], torch.Tensor] = {}
 _mm: Dict[int, torch.Tensor] = {}
 _lock = threading.Lock()
 
@@ -68,26 +68,34 @@ def plan_for(device: torch.device, H: int, W: int, D: int) -> Plan:
     return p
 
 
-def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+def _ws_key(device: torch.device) -> Tuple[int, int]:
+    """Workspaces are per (device, current stream): the launches of one stream are ordered, so they
+    share one; launches from two streams (a side stream, a second thread) get separate scratch --
+    the band passes keep their arrival counter and min/max partials in it."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    ws = _ws.get(idx)
+    return idx, torch.cuda.current_stream(torch.device("cuda", idx)).cuda_stream
+
+
+def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    key = _ws_key(device)
+    ws = _ws.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", idx))
-        _ws[idx] = ws
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", key[0]))
+        _ws[key] = ws
     return ws
 
 
-_ws_prep = {}
+_ws_prep: Dict[Tuple[int, int], torch.Tensor] = {}
 
 
 def workspace_prep(device: torch.device, nbytes: int) -> torch.Tensor:
-    """Small per-device workspace of the preprocessing statistics (kept apart from the spectrum
-    workspace so neither reallocates the other)."""
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    ws = _ws_prep.get(idx)
+    """Small per-(device, stream) workspace of the preprocessing statistics (kept apart from the
+    spectrum workspace so neither reallocates the other)."""
+    key = _ws_key(device)
+    ws = _ws_prep.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", idx))
-        _ws_prep[idx] = ws
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", key[0]))
+        _ws_prep[key] = ws
     return ws
 
 
