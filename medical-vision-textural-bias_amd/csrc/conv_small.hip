@@ -16,6 +16,8 @@
 // (every lane reads the same address: broadcast).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "texbias.h"
 
 namespace {
@@ -105,12 +107,125 @@ __global__ __launch_bounds__(NT) void k_conv3d_small(const float* __restrict__ x
   }
 }
 
+// z-marching form: block = (n, ZB consecutive output planes z, ROWS rows of h).  The input planes
+// live in a 4-slot LDS ring ([slot][ci][ROWS + 2 rows][XP]); plane z + 2 is fetched by
+// global->LDS DMA (no registers, no waits) while plane z is computed from the slots of z - 1, z,
+// z + 1, so every input row is read from memory once per block instead of three times (once per tz
+// of each output plane) and its fetch hides under the previous plane's FMAs.
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+constexpr int ZB = 8;  // output planes per block
+
+template <int CI, int CO>
+__global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__ x, const float* __restrict__ wt,
+                                                       const float* __restrict__ bias, float* __restrict__ y, int D,
+                                                       int H, int W, int XP, int nhb) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [4 slots][CI][ROWS + 2][XP], col 0 = w = -1
+  constexpr int RS = ROWS + 2, NR = CI * RS;                 // staged rows per plane
+  const int slot_f = CI * RS * XP;
+  float* ws = xs + 4 * slot_f;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < 4 * slot_f; i += NT) xs[i] = 0.f;  // halo columns stay zero (DMA writes 1 .. W)
+  for (int i = tid; i < CO * CI * 27; i += NT) ws[i] = wt[i];
+  const int hb = (int)blockIdx.x % nhb, z0 = ((int)blockIdx.x / nhb) * ZB, n = (int)blockIdx.y;
+  const int h0 = hb * ROWS;
+  const int64_t plane = (int64_t)H * W, vol = (int64_t)D * plane;
+  __syncthreads();
+  // stage input plane zi into ring slot (zi - z0 + 1) & 3: in-range rows by DMA, others zeroed
+  auto stage = [&](int zi) {
+    float* sl = xs + ((zi - z0 + 1) & 3) * slot_f;
+    for (int row = wave; row < NR; row += NT / 64) {
+      const int ci = row / RS, r = row - ci * RS, hi = h0 + r - 1;
+      float* dst = sl + row * XP + 1;
+      if (zi >= 0 && zi < D && hi >= 0 && hi < H) {
+        const float* src = x + ((int64_t)n * CI + ci) * vol + (int64_t)zi * plane + (int64_t)hi * W;
+#pragma unroll
+        for (int sg = 0; sg < kSeg; ++sg) {
+          const int c = lane + 64 * sg;
+          if (c < W) __builtin_amdgcn_global_load_lds((gptr_t)(src + c), (lptr_t)(dst + 64 * sg), 4, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int sg = 0; sg < kSeg; ++sg) {
+          const int c = lane + 64 * sg;
+          if (c < W) dst[c] = 0.f;
+        }
+      }
+    }
+  };
+  stage(z0 - 1);
+  stage(z0);
+  stage(z0 + 1);
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA landed
+  __syncthreads();
+  const int tpr = (W + WPT - 1) / WPT;
+  const int r = tid / tpr, w0 = (tid - r * tpr) * WPT;
+  const bool act = r < ROWS && h0 + r < H;
+  const int zend = z0 + ZB < D ? z0 + ZB : D;
+  for (int z = z0; z < zend; ++z) {
+    if (z + 2 < zend + 1) stage(z + 2);  // the next plane's fetch overlaps this plane's FMAs
+    if (act) {
+      float acc[CO][WPT];
+#pragma unroll
+      for (int co = 0; co < CO; ++co) {
+        const float b = bias ? bias[co] : 0.f;
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) acc[co][k] = b;
+      }
+#pragma unroll 1
+      for (int ct = 0; ct < CI * 3; ++ct) {
+        const int ci = ct / 3, tz = ct - 3 * ci;
+        const float* base = xs + ((z - z0 + tz) & 3) * slot_f + (ci * RS + r) * XP + w0;
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) {
+          const float* src = base + ty * XP;
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          const float2 v2 = *reinterpret_cast<const float2*>(src + 4);
+          const float v[WPT + 2] = {v4.x, v4.y, v4.z, v4.w, v2.x, v2.y};
+#pragma unroll
+          for (int co = 0; co < CO; ++co) {
+#pragma unroll
+            for (int tx = 0; tx < 3; ++tx) {
+              const float wv = ws[(((co * CI + ci) * 3 + tz) * 3 + ty) * 3 + tx];
+#pragma unroll
+              for (int k = 0; k < WPT; ++k) acc[co][k] = fmaf(wv, v[k + tx], acc[co][k]);
+            }
+          }
+        }
+      }
+      const int h = h0 + r;
+#pragma unroll
+      for (int co = 0; co < CO; ++co) {
+        float* dst = y + ((int64_t)n * CO + co) * vol + (int64_t)z * plane + (int64_t)h * W + w0;
+#pragma unroll
+        for (int k = 0; k < WPT; ++k)
+          if (w0 + k < W) dst[k] = acc[co][k];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // plane z + 2 landed (this wave's share)
+    __syncthreads();                // ... and every wave's; slot of z - 1 free for plane z + 3
+  }
+}
+
 template <int CI, int CO>
 int launch(const float* x, const float* w, const float* b, float* y, int N, int D, int H, int W, hipStream_t st) {
   const int XP = (W + 2 + WPT + 3) / 4 * 4;  // halo, slack for the last thread's 6-wide read, 16-B rows
   const size_t lds = sizeof(float) * ((size_t)CI * 3 * (ROWS + 2) * XP + CO * CI * 27);
   if ((W + WPT - 1) / WPT * ROWS > NT || lds > 65536 || XP > 64 * kSeg) return TB_ERR_UNSUPPORTED_SIZE;
   const int nhb = (H + ROWS - 1) / ROWS;
+  static const bool zmarch = [] {
+    const char* e = std::getenv("TEXBIAS_SMALL_CONV_Z");
+    return !(e && e[0] == '0');
+  }();
+  const size_t lds_z = sizeof(float) * ((size_t)4 * CI * (ROWS + 2) * XP + CO * CI * 27);
+  if (zmarch && lds_z <= 65536 * 2) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_small_z<CI, CO>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    if (attr != hipSuccess) return TB_ERR_HIP;
+    hipLaunchKernelGGL((k_conv3d_small_z<CI, CO>), dim3((unsigned)(nhb * ((D + ZB - 1) / ZB)), (unsigned)N), dim3(NT),
+                       lds_z, st, x, w, b, y, D, H, W, XP, nhb);
+    return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+  }
   hipLaunchKernelGGL((k_conv3d_small<CI, CO>), dim3((unsigned)(nhb * D), (unsigned)N), dim3(NT), lds, st, x, w, b, y,
                      D, H, W, XP, nhb);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
