@@ -114,7 +114,10 @@ __global__ __launch_bounds__(NT) void k_conv3d_small(const float* __restrict__ x
 // of each output plane) and its fetch hides under the previous plane's FMAs.
 typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
-constexpr int ZB = 8;  // output planes per block
+#ifndef TB_SMALL_ZB
+#define TB_SMALL_ZB 8
+#endif
+constexpr int ZB = TB_SMALL_ZB;  // output planes per block
 
 template <int CI, int CO>
 __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__ x, const float* __restrict__ wt,
