@@ -14,6 +14,8 @@ LAYERS = [  # name, G shape, X shape, stride (G = grad_out / low-res x, X = inpu
     ("L0.conv1 16->16 s1", (2, 16, 120, 120, 80), (2, 16, 120, 120, 80), 1),
     ("L0.conv0 4->16 s2", (2, 16, 120, 120, 80), (2, 4, 240, 240, 160), 2),
     ("L1.conv0 16->32 s2", (2, 32, 60, 60, 40), (2, 16, 120, 120, 80), 2),
+    ("L1.conv1 32->32 s1", (2, 32, 60, 60, 40), (2, 32, 60, 60, 40), 1),
+    ("L2.conv1 64->64 s1", (2, 64, 30, 30, 20), (2, 64, 30, 30, 20), 1),
     ("Up0.ru 3->3 s1", (2, 3, 240, 240, 160), (2, 3, 240, 240, 160), 1),
     ("Up0.convT 32->3 s2", (2, 32, 120, 120, 80), (2, 3, 240, 240, 160), 2),
 ]

@@ -23,7 +23,8 @@ def _grads(mod, x):
 
 @pytest.mark.parametrize("cin,cout,stride,shape", [(4, 16, 2, (2, 24, 20, 36)), (16, 16, 1, (2, 12, 10, 40)),
                                                     (3, 3, 1, (1, 16, 16, 33)), (20, 5, 1, (2, 10, 12, 18)),
-                                                    (32, 24, 2, (1, 16, 16, 70))])
+                                                    (32, 24, 2, (1, 16, 16, 70)), (24, 40, 1, (1, 9, 7, 130)),
+                                                    (8, 6, 1, (1, 5, 3, 250)), (16, 8, 1, (1, 17, 3, 5))])
 def test_conv3d_wgrad(conv, cin, cout, stride, shape, monkeypatch):
     monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)
     torch.manual_seed(0)
