@@ -1023,6 +1023,40 @@ __device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
 #ifndef TB_INV16_TR
 #define TB_INV16_TR 1   // 1: tile rows = image columns where row strides allow (see k_band_inv16); 0: never
 #endif
+#ifndef TB_INV16_NTS
+#define TB_INV16_NTS 0  // 1: C''s whole-line stores non-temporal
+#endif
+#ifndef TB_INV16_SWZ
+#define TB_INV16_SWZ 1  // 1: C' tiles regrouped across lanes so each 16-B store instruction writes 8 whole rows
+#endif
+// A 32 x 32 output tile in the TR layout -- lane (w = lane & 31, half = lane >> 5), register group g:
+// row w, columns 8 g + 4 half + 0..3 -- leaves each store instruction 32 rows x 32 B (128 partial
+// lines).  Two exchanges regroup it so that o[k] holds rows 8 k + (lane & 7), columns
+// 16 ((lane >> 3) & 1) + {0, 8, 4, 12}[lane >> 4] + 0..3: 8 whole 128-B rows per instruction.
+//   permlane16_swap(v[g], v[g+1]) (g = 0, 2): the odd 16-lane rows of v[g] trade with the even rows
+//   of v[g+1] -> v[g]: rows 0..15, columns 8 g + 0..15 (4 lanes a row), v[g+1]: rows 16..31;
+//   row_ror:8 inside each 16-lane row, written to one half of the banks, pairs rows r and r + 8.
+__device__ __forceinline__ void tile_rows8(const f32x4 (&v)[4], f32x4 (&o)[4]) {
+  f32x4 t[4];
+#pragma unroll
+  for (int g = 0; g < 4; g += 2)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[g][q]), __float_as_uint(v[g + 1][q]), false,
+                                                      false);
+      t[g][q] = __uint_as_float(r[0]);      // rows 0..15, columns 8 g + ..
+      t[g + 1][q] = __uint_as_float(r[1]);  // rows 16..31
+    }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)  // h = 0: rows 0..15 (t[0] columns 0..15, t[2] 16..31), h = 1: rows 16..31
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned lo = __float_as_uint(t[h][q]), hi = __float_as_uint(t[2 + h][q]);
+      o[2 * h][q] = __uint_as_float(__builtin_amdgcn_update_dpp(lo, hi, 0x128, 0xF, 0xC, false));
+      o[2 * h + 1][q] = __uint_as_float(__builtin_amdgcn_update_dpp(hi, lo, 0x128, 0xF, 0x3, false));
+    }
+}
+
 template <int VT, int NW, bool TR>  // 32-row tiles of V; waves per workgroup; tile rows = image columns
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1 ? TB_INV16_WPE : 3, 8))) void k_band_inv16(BandInvArgs) {
   // Same unit structure as k_band_inv: (slab, 32-row tile) units dealt to a persistent grid, each
@@ -1206,15 +1240,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
         }
         if (tr) {  // lane (w, half): columns 32 nt + 8 g + 4 half + 0..3 in registers 4 g .. 4 g + 3: 16-B stores
           const int wr = 32 * tw_ + l31;
+          const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
+          f32x4 v[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[g][q] = acc[4 * g + q] * inv;  // exactly 0 past D (T = 0 there)
+          const bool swz = TB_INV16_SWZ && vec && 32 * nt + 32 <= ncolo;  // wave-uniform
+          if (swz) {  // whole 128-B lines per store instruction (see tile_rows8)
+            f32x4 o[4];
+            tile_rows8(v, o);
+            const int cs = 32 * nt + 16 * ((lane >> 3) & 1) + ((0xC480 >> (4 * (lane >> 4))) & 15);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int rk = 32 * tw_ + 8 * k + (lane & 7);
+              if (rk < W) {
+                f32x4* dst = reinterpret_cast<f32x4*>(yb + (int64_t)rk * a.sw + cs);
+                if (TB_INV16_NTS) __builtin_nontemporal_store(o[k], dst);
+                else *dst = o[k];
+              }
+            }
+          }
           if (wr < W) {
             float* yr = yb + (int64_t)wr * a.sw;
-            const bool vec = ((a.sw & 3) == 0) && ((reinterpret_cast<uintptr_t>(yb) & 15) == 0);
-            f32x4 v[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[g][q] = acc[4 * g + q] * inv;  // exactly 0 past D (T = 0 there)
-            if (vec && 32 * nt + 32 <= ncolo) {  // wave-uniform: the whole tile lies inside the row
+            if (swz) {
+            } else if (vec && 32 * nt + 32 <= ncolo) {  // wave-uniform: the whole tile lies inside the row
 #pragma unroll
               for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(yr + 32 * nt + 8 * g + 4 * hl) = v[g];
             } else {
