@@ -1211,6 +1211,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
       float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
       float lo = 3.402823466e38f, hi = -3.402823466e38f;
       const int wb = 32 * tw_ + 4 * hl;  // image row of accumulator register r: wb + acc_row(r)
+      // regrouped tile (tile_rows8): lane's row 32 tw + 8 k + (lane & 7), column offset cs0 + 32 nt
+      const int r8 = 32 * tw_ + (lane & 7);
+      const int cs0 = 16 * ((lane >> 3) & 1) + ((0xC480 >> (4 * (lane >> 4))) & 15);
+      float* ys = yb + (int64_t)(r8 < W ? r8 : 0) * a.sw + cs0;
+      const int64_t s8 = 8 * a.sw;
       for (int nt = 0; nt < ntd; ++nt) {
         f32x16 acc;
 #pragma unroll
@@ -1246,25 +1251,37 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
           for (int g = 0; g < 4; ++g)
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[g][q] = acc[4 * g + q] * inv;  // exactly 0 past D (T = 0 there)
-          const bool swz = TB_INV16_SWZ && vec && 32 * nt + 32 <= ncolo;  // wave-uniform
-          if (swz) {  // whole 128-B lines per store instruction (see tile_rows8)
+          if (TB_INV16_SWZ && vec && 32 * nt + 32 <= ncolo) {  // wave-uniform: whole 128-B lines per store
             f32x4 o[4];
             tile_rows8(v, o);
-            const int cs = 32 * nt + 16 * ((lane >> 3) & 1) + ((0xC480 >> (4 * (lane >> 4))) & 15);
+            const bool img = 32 * nt + 32 <= D;  // wave-uniform: every column an image column
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const int rk = 32 * tw_ + 8 * k + (lane & 7);
-              if (rk < W) {
-                f32x4* dst = reinterpret_cast<f32x4*>(yb + (int64_t)rk * a.sw + cs);
+              if (r8 + 8 * k < W) {
+                f32x4* dst = reinterpret_cast<f32x4*>(ys + k * s8 + 32 * nt);
                 if (TB_INV16_NTS) __builtin_nontemporal_store(o[k], dst);
                 else *dst = o[k];
+                if (img) {
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) {
+                    lo = fminf(lo, o[k][q]);
+                    hi = fmaxf(hi, o[k][q]);
+                  }
+                } else {
+#pragma unroll
+                  for (int q = 0; q < 4; ++q)
+                    if (32 * nt + cs0 + q < D) {
+                      lo = fminf(lo, o[k][q]);
+                      hi = fmaxf(hi, o[k][q]);
+                    }
+                }
               }
             }
+            continue;
           }
           if (wr < W) {
             float* yr = yb + (int64_t)wr * a.sw;
-            if (swz) {
-            } else if (vec && 32 * nt + 32 <= ncolo) {  // wave-uniform: the whole tile lies inside the row
+            if (vec && 32 * nt + 32 <= ncolo) {  // wave-uniform: the whole tile lies inside the row
 #pragma unroll
               for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(yr + 32 * nt + 8 * g + 4 * hl) = v[g];
             } else {
