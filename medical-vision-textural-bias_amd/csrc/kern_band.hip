@@ -1023,6 +1023,9 @@ __device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
 #ifndef TB_INV16_TR
 #define TB_INV16_TR 1   // 1: tile rows = image columns where row strides allow (see k_band_inv16); 0: never
 #endif
+#ifndef TB_INV16_ACC2
+#define TB_INV16_ACC2 0  // 1: C''s cross-term products in an accumulator chain of their own
+#endif
 #ifndef TB_INV16_NTS
 #define TB_INV16_NTS 0  // 1: C''s whole-line stores non-temporal
 #endif
@@ -1217,24 +1220,28 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
       float* ys = yb + (int64_t)(r8 < W ? r8 : 0) * a.sw + cs0;
       const int64_t s8 = 8 * a.sw;
       for (int nt = 0; nt < ntd; ++nt) {
-        f32x16 acc;
+        f32x16 acc, acl;  // hi x hi products / the two cross terms (TB_INV16_ACC2: separate chains)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+        for (int j = 0; j < 16; ++j) acc[j] = acl[j] = 0.f;
 #pragma unroll
         for (int c = 0; c < 2 * VT; ++c) {
           if (c >= nch || (diag & 8)) break;
           const h16x8* tp = Tab + ((nt * nch + c) * 2) * 64 + lane;
           const h16x8 th = tp[0], tl = tp[64];
+          f32x16& ax = TB_INV16_ACC2 ? acl : acc;
           if (tr) {  // Y(d, w) = T(d, v) . V(v, w): the table as the A operand, the V tile as B
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, al[c], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, ah[c], acc, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, al[c], ax, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, ah[c], ax, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ah[c], acc, 0, 0, 0);
           } else {   // Y^T(w, d) = V^T(w, v) . T(v, d)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, acc, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, ax, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, ax, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], th, acc, 0, 0, 0);
           }
         }
+        if (TB_INV16_ACC2)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[j] += acl[j];
         const int col = 32 * nt + l31;
         if (diag & 16) {  // no stores: keep the results live
           float z = 0.f;
