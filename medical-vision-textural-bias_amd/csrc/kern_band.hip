@@ -1021,10 +1021,7 @@ __device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
 #define TB_INV16_NW 16  // waves per split-f16 pass-C' workgroup: 16 = one workgroup per CU (C3 80 -> 72 us vs 4)
 #endif
 #ifndef TB_INV16_TR
-#define TB_INV16_TR 1   // 1: tile rows = image columns where row strides allow (see k_band_inv16); 0: never
-#endif
-#ifndef TB_INV16_ACC2
-#define TB_INV16_ACC2 0  // 1: C''s cross-term products in an accumulator chain of their own
+#define TB_INV16_TR 1   // 1: tile rows = image columns where row strides allow (see k_band_inv16); 0: never; 2: always
 #endif
 #ifndef TB_INV16_NTS
 #define TB_INV16_NTS 0  // 1: C''s whole-line stores non-temporal
@@ -1220,28 +1217,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
       float* ys = yb + (int64_t)(r8 < W ? r8 : 0) * a.sw + cs0;
       const int64_t s8 = 8 * a.sw;
       for (int nt = 0; nt < ntd; ++nt) {
-        f32x16 acc, acl;  // hi x hi products / the two cross terms (TB_INV16_ACC2: separate chains)
+        f32x16 acc;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = acl[j] = 0.f;
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
 #pragma unroll
         for (int c = 0; c < 2 * VT; ++c) {
           if (c >= nch || (diag & 8)) break;
           const h16x8* tp = Tab + ((nt * nch + c) * 2) * 64 + lane;
           const h16x8 th = tp[0], tl = tp[64];
-          f32x16& ax = TB_INV16_ACC2 ? acl : acc;
           if (tr) {  // Y(d, w) = T(d, v) . V(v, w): the table as the A operand, the V tile as B
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, al[c], ax, 0, 0, 0);
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, ah[c], ax, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, al[c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tl, ah[c], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(th, ah[c], acc, 0, 0, 0);
           } else {   // Y^T(w, d) = V^T(w, v) . T(v, d)
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, ax, 0, 0, 0);
-            ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, ax, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], th, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], tl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], th, acc, 0, 0, 0);
           }
         }
-        if (TB_INV16_ACC2)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) acc[j] += acl[j];
         const int col = 32 * nt + l31;
         if (diag & 16) {  // no stores: keep the results live
           float z = 0.f;
@@ -1496,9 +1489,13 @@ hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
 template <int VT, int NW>
 hipError_t launch_inv16_t(const BandInvArgs& a, int ncu, hipStream_t st) {
   const size_t lds = band_inv16_carve(a.g, a.pl.W, band_slots16(NW)).total;
-  // output orientation: tile rows = image columns (16-B row stores) unless rows are 512-B strided
-  // (a power-of-two row stride piles one store's 32 rows onto one memory channel): then image rows
-  auto kern = (TB_INV16_TR && ((a.sw * 4) % 512) != 0) ? k_band_inv16<VT, NW, true> : k_band_inv16<VT, NW, false>;
+  // output orientation: tile rows = image columns.  With 16-B aligned rows the tile is regrouped
+  // into whole-line stores (tile_rows8), which beat the image-row orientation at every row stride
+  // (C2, 512-B rows: 77 -> 69 us).  Without them the 32 x 32-B pieces of a store pile onto one
+  // memory channel when rows are 512-B strided: those keep image rows.
+  const bool swz_ok = TB_INV16_SWZ && (a.sw & 3) == 0 && (a.sbc & 3) == 0 && (a.sh & 3) == 0 &&
+                      (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
+  auto kern = (TB_INV16_TR == 2 || (TB_INV16_TR && (swz_ok || ((a.sw * 4) % 512) != 0))) ? k_band_inv16<VT, NW, true> : k_band_inv16<VT, NW, false>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
   const int per_cu = band_occupancy(kern, lds, 64 * NW, 8);

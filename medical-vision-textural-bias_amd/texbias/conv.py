@@ -10,6 +10,7 @@ summed over N, D, H, W -- ATen's generic reduction ran at 0.1-0.3 TB/s, ~7 ms of
 """
 from __future__ import annotations
 
+import functools
 import math
 import os
 
@@ -71,14 +72,32 @@ def custom_backward_applies(x: torch.Tensor, w: torch.Tensor) -> bool:
     return ENABLED and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32
 
 
-def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, padding, transposed: bool) -> bool:
+@functools.lru_cache(maxsize=256)
+def _wgrad_tiles(g_shape, x_shape, stride: int) -> bool:
+    """A tiling of tb_conv3d_wgrad_f32 exists for these shapes (tb_conv3d_wgrad_config, host only):
+    rows too wide for the LDS budget at the channel tile go to ATen instead of failing."""
+    import ctypes
+    cfg = (ctypes.c_int64 * 5)()
+    N, M, Do, Ho, Wo = g_shape
+    Cc, Di, Hi, Wi = x_shape[1:]
+    return lib().tb_conv3d_wgrad_config(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, 1, cfg) == 0
+
+
+def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, padding, transposed: bool,
+                       output_padding=(0, 0, 0)) -> bool:
     if not custom_backward_applies(x, w):
         return False
     if tuple(w.shape[2:]) != (3, 3, 3) or len(set(stride)) != 1 or stride[0] not in (1, 2) or padding[0] != 1 or \
             len(set(padding)) != 1:
         return False
     pos = x.shape[0] * math.prod(out_spatial if not transposed else x.shape[2:])
-    return pos >= MIN_K_PER_OUTPUT * w.shape[0] * w.shape[1] * 27 // 16
+    if pos < MIN_K_PER_OUTPUT * w.shape[0] * w.shape[1] * 27 // 16:
+        return False
+    s = stride[0]
+    if transposed:  # G = x [N, Cin, ...], X = grad of the output [N, Cout, (n - 1) s + 1 + output_padding]
+        hi = tuple((n - 1) * s + 1 + op for n, op in zip(x.shape[2:], output_padding))
+        return _wgrad_tiles(tuple(x.shape), (x.shape[0], w.shape[1]) + hi, s)
+    return _wgrad_tiles((x.shape[0], w.shape[0]) + tuple(out_spatial), tuple(x.shape), s)
 
 
 class _ConvFn(torch.autograd.Function):
@@ -176,7 +195,7 @@ class ConvTranspose3d(nn.ConvTranspose3d):
     def forward(self, x, output_size=None):
         if output_size is None and self.groups == 1 and self.dilation == (1, 1, 1) and \
                 custom_backward_applies(x, self.weight):
-            fast = fast_wgrad_applies(x, self.weight, None, self.stride, self.padding, True)
+            fast = fast_wgrad_applies(x, self.weight, None, self.stride, self.padding, True, self.output_padding)
             return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, self.output_padding, True,
                                  fast)
         return super().forward(x, output_size)

@@ -287,3 +287,31 @@ def test_band_runs_at_nonzero_offset(rt, layout):
     for b, p in enumerate(progs):
         if not p:
             assert torch.equal(yb[b, ..., : sp[-1]], x[b])
+
+
+@pytest.mark.parametrize("extra,base", [(0, 0), (0, 1), (1, 0), (4, 0), (97, 2)])
+def test_band_output_layouts(rt, extra, base):
+    """Pass C' output orientations: 16-B aligned rows take the whole-line regrouped stores
+    (tile_rows8), rows of odd stride or an unaligned base the 16-B / 4-B piecewise stores -- the same
+    values, the pad columns zero, columns past the pad untouched, min/max keys of what was written."""
+    torch.manual_seed(5)
+    C, sp, pad = 2, (40, 37, 33), 3
+    progs = [[K.disk_op(6.0, False), K.wrap_op(0.5)], [K.disk_op(9.5, False)]]
+    B = len(progs)
+    x = torch.randn((B, C) + sp, device="cuda")
+    ref = rt.kspace_filter(x, 3, progs, C, pad=pad)
+    row = sp[-1] + pad + extra
+    buf = torch.full((B * C * sp[0] * sp[1] * row + base,), float("nan"), device="cuda")
+    out = buf[base:].view(B, C, sp[0], sp[1], row)[..., : sp[-1] + pad]
+    mm = torch.empty((B, 2), dtype=torch.int32, device="cuda")
+    y = rt.kspace_filter(x, 3, progs, C, out=out, pad=pad, minmax=mm)
+    torch.cuda.synchronize()
+    assert y.data_ptr() == out.data_ptr()
+    assert torch.all(out[..., sp[-1]:] == 0)
+    assert (out - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    if extra:
+        assert torch.isnan(buf[base:].view(B, C, sp[0], sp[1], row)[..., sp[-1] + pad:]).all()
+    v = out[..., : sp[-1]].reshape(B, -1)
+    m = rt.keys_to_float(mm)
+    np.testing.assert_array_equal(m[:, 0], v.min(1).values.cpu().numpy())
+    np.testing.assert_array_equal(m[:, 1], v.max(1).values.cpu().numpy())
