@@ -110,11 +110,16 @@ __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
   const int na = __builtin_amdgcn_readfirstlane(act[0]);
   if (na == 0) return;
   const int Dp = D + 3;
-  float2* tD = reinterpret_cast<float2*>(smem);  // e^{-2 pi i f . n / N} factors, [namax][n] per axis
+  // the D factors again as float64 pairs (exact widenings of the float table: the inner product's
+  // FMAs then read them without two conversions per voxel and spike)
+  double2* tDd = reinterpret_cast<double2*>(smem);
+  float2* tD = reinterpret_cast<float2*>(tDd + a.namax * Dp);  // e^{-2 pi i f . n / N}, [namax][n] per axis
   float2* tW = tD + a.namax * Dp;
   float2* tH = tW + a.namax * W;
   double* red = reinterpret_cast<double*>(tH + a.namax * H);  // [4 waves][TB_MAX_OPS][2]
   point_tables(act, na, H, W, D, -1.f, tD, tW, tH);
+  __syncthreads();
+  for (int t = tid; t < na * Dp; t += POINT_NT) tDd[t] = make_double2((double)tD[t].x, (double)tD[t].y);
   __syncthreads();
   const float* xb = a.x + (int64_t)bc * a.xsbc;
   const bool vec = (a.xsw & 3) == 0 && (a.xsh & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
@@ -145,13 +150,13 @@ __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
 #pragma unroll
       for (int k = 0; k < TB_MAX_OPS; ++k) {
         if (k >= na) break;
-        const float2* t = tD + k * Dp + dd[u];
+        const double2* t = tDd + k * Dp + dd[u];
         double sr = 0.0, si = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float2 tj = t[j];
-          sr = fma((double)v[u][j], (double)tj.x, sr);
-          si = fma((double)v[u][j], (double)tj.y, si);
+          const double2 tj = t[j];
+          sr = fma((double)v[u][j], tj.x, sr);
+          si = fma((double)v[u][j], tj.y, si);
         }
         const float2 r = cmul(tW[k * W + ww[u]], tH[k * H + hh[u]]);
         accr[k] += sr * (double)r.x - si * (double)r.y;
@@ -347,6 +352,10 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
 
 bool point_program(const tb_sample_ops& s, int H, int W, int D) {
   if (s.n < 1 || (size_t)TB_MAX_OPS * (H + W + D + 3) * sizeof(float2) > 65536) return false;
+  // k_point_dft adds the float64 D table (and its wave sums)
+  if ((size_t)TB_MAX_OPS * ((H + W + D + 3) * sizeof(float2) + (D + 3) * sizeof(double2)) +
+          4 * TB_MAX_OPS * 2 * sizeof(double) > 163840)
+    return false;
   for (int o = 0; o < s.n; ++o)
     if (s.op[o].kind != TB_OP_SPIKE) return false;
   const int n[3] = {H, W, D};
@@ -366,7 +375,8 @@ bool point_program(const tb_sample_ops& s, int H, int W, int D) {
 
 static size_t point_lds(const PointArgs& a, int stage) {
   const size_t tabs = (size_t)a.namax * (a.D + 3 + a.W + a.H) * sizeof(float2);
-  return stage == 0 ? tabs + 4 * TB_MAX_OPS * 2 * sizeof(double) : tabs + 2 * POINT_NT / 64 * sizeof(float);
+  return stage == 0 ? (size_t)a.namax * (a.D + 3) * sizeof(double2) + tabs + 4 * TB_MAX_OPS * 2 * sizeof(double)
+                    : tabs + 2 * POINT_NT / 64 * sizeof(float);
 }
 
 template <class K>
@@ -392,18 +402,20 @@ static int point_parts(K kern, size_t lds, int nbc, int ncu) {
 }
 
 void point_grid(PointArgs& a, int ncu) {
+  (void)allow_lds(k_point_dft, point_lds(a, 0));  // occupancy is queried at the launch's LDS size
   a.parts = point_parts(k_point_dft, point_lds(a, 0), a.nbc, ncu);
   a.parts_apply = point_parts(k_point_apply, point_lds(a, 2), a.nbc, ncu);
 }
 
 hipError_t launch_point(const PointArgs& a, hipStream_t st, int stage) {
-  const size_t tabs = (size_t)a.namax * (a.D + 3 + a.W + a.H) * sizeof(float2);
   if (stage == 0) {
-    hipLaunchKernelGGL(k_point_dft, dim3(a.parts, a.nbc), dim3(POINT_NT), tabs + 4 * TB_MAX_OPS * 2 * sizeof(double), st, a);
+    const hipError_t e = allow_lds(k_point_dft, point_lds(a, 0));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_point_dft, dim3(a.parts, a.nbc), dim3(POINT_NT), point_lds(a, 0), st, a);
   } else if (stage == 1) {
     hipLaunchKernelGGL(k_point_delta, dim3(a.nbc), dim3(64), 0, st, a);
   } else {
-    hipLaunchKernelGGL(k_point_apply, dim3(a.parts_apply, a.nbc), dim3(POINT_NT), tabs + 2 * POINT_NT / 64 * sizeof(float), st, a);
+    hipLaunchKernelGGL(k_point_apply, dim3(a.parts_apply, a.nbc), dim3(POINT_NT), point_lds(a, 2), st, a);
   }
   return hipGetLastError();
 }
