@@ -299,6 +299,15 @@ int tb_set_band_plans(int enable);
 int tb_set_point_plans(int enable);
 
 /*
+ * Wrap-only programs (WrapArtifact, filters_and_operators.py:503-515) on shapes with even H and W take
+ * the separable route: the mask is a product of symmetric 1-D masks, so y = T_h T_w T_d x with 2-tap
+ * circulants on the even axes and, for odd D (D + pad <= 256), a dense D-point circulant applied as a
+ * split-f16 matrix product -- one image read and one write, no spectrum.  Same results to rounding.
+ * Default on; TEXBIAS_WRAP=0 in the environment turns it off.
+ */
+int tb_set_wrap_plans(int enable);
+
+/*
  * Pass C' of the band-limited plans synthesises the image on the f16 matrix cores in split
  * precision (table and V each as an f16 hi/lo pair, three products, f32 accumulation; agrees with
  * the f32 synthesis to a few 1e-7 of max |y|) whenever the launch's band columns plus all of its

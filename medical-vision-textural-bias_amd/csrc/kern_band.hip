@@ -973,7 +973,8 @@ __device__ void band_tab16(const BandMidArgs& a, int t) {
 template <int NT>
 __device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
   __shared__ int last;
-  __syncthreads();  // every wave's partials issued (store_partial)
+  drain_vmem();     // this wave's store_partial calls have completed ...
+  __syncthreads();  // ... for every wave before the count-in
   if (threadIdx.x == 0) last = arrive_last(a.cnt, gridDim.x);
   __syncthreads();
   if (!last) return;

@@ -168,8 +168,14 @@ __device__ __forceinline__ float2 load_partial(const float2* p) {
   const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return make_float2(__uint_as_float((uint32_t)u), __uint_as_float((uint32_t)(u >> 32)));
 }
+// Wait until every vector-memory operation this wave issued has completed.  A workgroup-scope
+// release compiles to an lgkmcnt wait only, so without this an sc1 partial can still be in flight
+// when the counter add lands.  Every wave that called store_partial runs it before the barrier
+// that precedes arrive_last (the calling wave's own stores are drained inside arrive_last).
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // count the calling thread's workgroup in after its store_partial calls; true for the last of `total`
 __device__ __forceinline__ bool arrive_last(uint32_t* cnt, uint32_t total) {
+  drain_vmem();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   return __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
 }

@@ -25,6 +25,7 @@
 #include "point.h"
 #include "plan_host.h"
 #include "sap_core.h"
+#include "wrap.h"
 
 using namespace tb;
 
@@ -262,6 +263,7 @@ struct tb_plan {
   float* tds = nullptr;  // band pass C': [D/2 + 1][2][NCOLS] cos / sin(2 pi kd d / D), d < D/2 + 1, else 0
   float* tbt = nullptr;  // band pass A': [2][KSd][2][64] B fragments of the folded D product
   bool generic = false;  // full-spectrum route on the direct-DFT fallback (kern_generic.hip)
+  double* wrapq = nullptr;  // odd D <= WRAP_MAX_COLS: the wrap route's D circulant table q[D] (wrap.h)
 };
 
 namespace {
@@ -410,6 +412,15 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
       return hip_fail(hipGetLastError());
     }
   }
+  if ((D & 1) && D <= WRAP_MAX_COLS) {  // separable wrap route's D-axis circulant (float64)
+    std::vector<double> q(D);
+    tb::wrap_q_table(D, q.data());
+    if (hipMalloc(reinterpret_cast<void**>(&p->wrapq), q.size() * 8) != hipSuccess ||
+        hipMemcpy(p->wrapq, q.data(), q.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+      tb_plan_destroy(p);
+      return hip_fail(hipGetLastError());
+    }
+  }
   p->rset_h = needs_all(p->host.ax[0]) ? RS_ALL : RS_SMALL;
   p->rset_wd = (needs_all(p->host.ax[1]) || needs_all(p->host.ax[2])) ? RS_ALL : RS_SMALL;
   *out = p;
@@ -421,6 +432,7 @@ int tb_plan_destroy(tb_plan* plan) {
   if (plan->dmem) (void)hipFree(plan->dmem);
   if (plan->tds) (void)hipFree(plan->tds);
   if (plan->tbt) (void)hipFree(plan->tbt);
+  if (plan->wrapq) (void)hipFree(plan->wrapq);
   delete plan;
   return TB_OK;
 }
@@ -491,6 +503,12 @@ static bool g_band = [] {
 // tb_set_point_plans(0): the full-spectrum passes.
 static bool g_point = [] {
   const char* e = std::getenv("TEXBIAS_POINT");
+  return !(e && e[0] == '0');
+}();
+// Wrap-only programs on the separable route (wrap.h); TEXBIAS_WRAP=0 or tb_set_wrap_plans(0): the
+// full-spectrum passes.
+static bool g_wrap = [] {
+  const char* e = std::getenv("TEXBIAS_WRAP");
   return !(e && e[0] == '0');
 }();
 // Pass C' synthesis in split f16 on the matrix cores (k_band_inv16) when the launch's V rows fit
@@ -629,7 +647,44 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
   return true;
 }
 
-enum { RUN_COPY = 0, RUN_FULL = 1, RUN_BAND = 2, RUN_POINT = 3 };
+enum { RUN_COPY = 0, RUN_FULL = 1, RUN_BAND = 2, RUN_POINT = 3, RUN_WRAP = 4 };
+
+// The run [s0, s1) takes the separable wrap route: every program wrap-only with the same alpha
+// product (one circulant table per launch), a shape the route takes, room for its partials.
+static bool wrap_run(const tb_plan* p, const tb_sample_ops* ops, int s, int y_pad, size_t ws_bytes, float* alpha) {
+  if (!g_wrap || ws_bytes < tb::wrap_ws_bytes()) return false;
+  if (!tb::wrap_shape_ok(p->dev.H, p->dev.W, p->dev.D, y_pad)) return false;
+  if ((p->dev.D & 1) && !p->wrapq) return false;
+  return tb::wrap_program(ops[s], alpha);
+}
+
+static int run_wrap(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
+                    char* ws, int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax, hipStream_t st) {
+  const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
+  tb::WrapArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.H = H, a.W = W, a.D = D;
+  a.x = x, a.xsbc = xs[0], a.xsh = xs[1], a.xsw = xs[2];
+  a.y = y, a.ysbc = ys[0], a.ysh = ys[1], a.ysw = ys[2];
+  a.ypad = y_pad, a.bc0 = b0 * C, a.C = C, a.nbc = nb * C;
+  a.q = p->wrapq;
+  a.mm = minmax;
+  a.mmp = reinterpret_cast<float2*>(ws);
+  a.cnt = reinterpret_cast<uint32_t*>(ws + (size_t)tb::WRAP_MAX_WG * TB_MAX_BATCH * 8);
+  // 16-B loads: contiguous rows and 16-B aligned role chunks (every row start of a 4-row chunk,
+  // W/2 rows apart); 16-B stores: every output row start 16-B aligned
+  const bool xal = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (xs[0] & 3) == 0 && (xs[1] & 3) == 0;
+  const bool vld = (D & 1) ? (xal && xs[2] == D && (((int64_t)(W / 2) * D) & 3) == 0)
+                           : (xal && (xs[2] & 3) == 0);
+  const bool vst = (reinterpret_cast<uintptr_t>(y) & 15) == 0 && (ys[0] & 3) == 0 && (ys[1] & 3) == 0 && (ys[2] & 3) == 0;
+  a.vec = (vld ? 1 : 0) | (vst ? 2 : 0);
+  float alpha[TB_MAX_BATCH];
+  for (int i = 0; i < nb; ++i) tb::wrap_program(ops[b0 + i], &alpha[i]);
+  const double vox = (double)nb * C * H * W;
+  Timer t(2, st, vox * (D + D + y_pad) * 4.0, (D & 1) ? "k_wrap_dgemm" : "k_wrap_even");
+  TB_HIP(tb::launch_wrap(a, alpha, nb, p->ncu, st));
+  return TB_OK;
+}
 
 template <int RA, int RB>
 static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad, cf* S,
@@ -855,11 +910,14 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
     int i = 0;
     while (i < nb) {
-      auto route = [&](int s) { return ops[s].n == 0 ? RUN_COPY : RUN_FULL; };
+      float al0 = 0.f, al = 0.f;
+      auto route = [&](int s, float* alpha) {
+        return ops[s].n == 0 ? RUN_COPY : (wrap_run(p, ops, s, y_pad, ws_bytes, alpha) ? RUN_WRAP : RUN_FULL);
+      };
       Run run;
-      run.route = route(b0 + i);
+      run.route = route(b0 + i, &al0);
       int j = i + 1;
-      while (j < nb && route(b0 + j) == run.route) ++j;
+      while (j < nb && route(b0 + j, &al) == run.route && (run.route != RUN_WRAP || al == al0)) ++j;
       run.s0 = b0 + i;
       run.s1 = b0 + j;
       if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_ws(B * C).total) {
@@ -869,7 +927,7 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
       }
       if (run.route == RUN_FULL && g_band && band_plan(p, ops, run.s0, run.s1, y_pad, ws_bytes, B * C, run.g, run.sp))
         run.route = RUN_BAND;
-      atomic_keys |= run.route != RUN_BAND;
+      atomic_keys |= run.route != RUN_BAND && run.route != RUN_WRAP;  // these two write their keys outright
       runs.push_back(run);
       i = j;
     }
@@ -883,6 +941,8 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
     int rc = TB_OK;
     if (run.route == RUN_COPY)
       rc = run_copy(p, x, xs, y, ys, y_pad, run.s0, nb, C, minmax, st);
+    else if (run.route == RUN_WRAP)
+      rc = run_wrap(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), run.s0, nb, C, ops, minmax, st);
     else if (run.route == RUN_POINT)
       rc = run_point(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), run.s0, nb, C, ops, minmax, st);
     else if (run.route == RUN_BAND)
@@ -1053,6 +1113,11 @@ int tb_set_compiled_plans(int enable) {
 
 int tb_set_band_plans(int enable) {
   g_band = enable != 0;
+  return TB_OK;
+}
+
+int tb_set_wrap_plans(int enable) {
+  g_wrap = enable != 0;
   return TB_OK;
 }
 

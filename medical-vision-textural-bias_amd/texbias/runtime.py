@@ -363,6 +363,12 @@ def set_point_plans(enable: bool) -> None:
     check(lib().tb_set_point_plans(1 if enable else 0))
 
 
+def set_wrap_plans(enable: bool) -> None:
+    """Wrap-only programs on the separable route (2-tap H/W combine + D circulant, one image read
+    and write) when True (default), else on the full-spectrum passes (tb_set_wrap_plans)."""
+    check(lib().tb_set_wrap_plans(1 if enable else 0))
+
+
 def set_band_inv16(enable: bool) -> None:
     """Pass C' synthesis in split f16 on the matrix cores when True (default, where the launch's
     V rows fit), else the f32 MFMA synthesis (tb_set_band_inv16)."""
