@@ -68,6 +68,13 @@ def parse():
                          "(300_.../30_augmentation/baseline_domain_augment_alpha0p4.py:118); spikes-aug: "
                          "RandKSpaceSpikeNoised(intensity_ranges=(10, 11)) (..._spikes10-11.py:120); the two "
                          "augmentations at prob 1 (the drivers' 0.1 would time mostly identity copies)")
+    ap.add_argument("--model", choices=("unet", "gibbs-layer", "spike-layer"), default="unet",
+                    help="c3 only.  unet: the filter chain + U-Net(4->3) train step (the headline); gibbs-layer: "
+                         "the in-model Gibbs layer drivers (350_stylized_layers/gibbs0p7_layer_domain_GD.py:252-301): "
+                         "Gibbs_UNet(1->1) with the device-resident GibbsNoiseLayer at alpha 0.7, train step + "
+                         "Gibbs_GD (2 no-grad forwards) per step; spike-layer: Spikes_UNet(I=11) + the intensity "
+                         "finite-difference step (spikes11_layer_domain_GD.py:260-300).  Layer models default to "
+                         "the drivers' 1 x 128 x 128 x 64 crops (--shape 240,240,160 for BraTS size)")
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--no-cudnn-benchmark", action="store_true",
                     help="skip MIOpen Find (its exhaustive solver search makes the first step slow, the rest fast)")
@@ -79,10 +86,15 @@ def parse():
     ap.add_argument("--filter-only", action="store_true", help="diagnostic: time the filter chain alone")
     a = ap.parse_args()
     c2, c5 = a.config == "c2", a.config == "c5"
+    layer = a.model != "unet"
+    if layer and a.config != "c3":
+        ap.error("--model gibbs-layer / spike-layer run with --config c3")
     a.batch = a.batch or (16 if c2 else 64 if c5 else 2)
-    a.shape = a.shape or ("128,128,128" if c2 else "1,128,128" if c5 else "240,240,155")
+    a.shape = a.shape or ("128,128,128" if c2 else "1,128,128" if c5 else "128,128,64" if layer else "240,240,155")
     if a.pad_to is None:
-        a.pad_to = 0 if (c2 or c5) else 160
+        a.pad_to = 0 if (c2 or c5 or layer) else 160
+    if layer:
+        a.no_cpu_baseline = True  # the layers run inside the model on the GPU in the reference too
     if c5:
         a.no_cpu_baseline = True  # the reference trains its DCGAN on the GPU; no CPU path to time
         a.channels_last = True    # NHWC: 4.89k vs 4.60k slices/s at batch 64 (profiles/r2/bench/c5_variants.txt)
@@ -169,7 +181,8 @@ def main():
         print(f"[bench] world size {world} (backend {dist.get_backend() if world > 1 else 'none'})",
               file=sys.stderr, flush=True)
     dev = torch.device("cuda", local)
-    B, C = args.batch, (1 if args.config == "c5" else 4)
+    layer_model = args.model != "unet"
+    B, C = args.batch, (1 if (args.config == "c5" or layer_model) else 4)
     pad = max(0, args.pad_to - D)
     torch.manual_seed(1000 + rank)
 
@@ -177,6 +190,8 @@ def main():
     pool = [brats_like(B, C, (H, W, D), seed=rank * 97 + i, device=dev) for i in range(2)]
     labels = [] if args.filter_only else \
         [brats_labels(B, (H, W, D), seed=rank * 97 + i, device=dev, pad_to=D + pad) for i in range(2)]
+    if layer_model:  # the layer drivers segment one class (whole tumour) from one modality
+        labels = [lab[:, :1].contiguous() for lab in labels]
 
     chain, tr = reference_c3_chain(rank)  # per-rank seeded transform streams
     disk, planes, wrap, sap = tr["disk"], tr["planes"], tr["wrap"], tr["sap"]
@@ -213,6 +228,25 @@ def main():
         torch.manual_seed(0)  # identical network init on every rank
         step_fn = DCGANStep(dev, distributed=world > 1, bf16=not args.fp32, channels_last=args.channels_last)
         torch.manual_seed(1000 + rank)
+    elif layer_model:
+        import stylization_layers as SL
+        from texbias.train import gibbs_gd, spike_gd
+        torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
+        torch.manual_seed(0)
+        if args.model == "gibbs-layer":
+            lm = SL.Gibbs_UNet()
+            lm.gibbs.alpha.fill_(0.7)  # the driver's GibbsNoiseLayer(0.7) (gibbs0p7_layer_domain_GD.py)
+        else:
+            lm = SL.Spikes_UNet(11.0)
+        torch.manual_seed(1000 + rank)
+        step_fn = TrainStep(lm, dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb)
+        gd = gibbs_gd if args.model == "gibbs-layer" else spike_gd
+        train_step = step_fn
+
+        def step_fn(x, y):  # noqa: F811 - train step, then the layer's finite-difference update
+            loss = train_step(x, y)
+            gd(x, y, train_step.model, train_step.loss_fn)
+            return loss
     elif not args.filter_only:
         torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
         step_fn = TrainStep(reference_model(C, 3), dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb,
@@ -221,6 +255,8 @@ def main():
     def one_step(i):
         if args.random_filters:
             randomize_filters()
+        if layer_model:  # the filter is the model's first layer
+            return step_fn(pool[i % 2], labels[i % 2])
         y = chain(pool[i % 2], pad=pad)
         if args.config == "c5":
             return step_fn(y.view(B, 1, W, D))
@@ -272,6 +308,21 @@ def main():
         dom = max((n for n in names[:3] if n in passes and "GB_s" in passes[n]), key=lambda n: passes[n]["avg_ms"])
         ach = passes[dom]["GB_s"]
         dom_bytes = passes[dom]["algorithmic_bytes"]
+        if layer_model:
+            workload = f"LAYER DRIVER {args.model}: " + (
+                "Gibbs_UNet(1->1) with GibbsNoiseLayer alpha 0.7 (device-resident), train step + Gibbs_GD "
+                "(2 no-grad forwards) per step (350_stylized_layers/gibbs0p7_layer_domain_GD.py:252-301)"
+                if args.model == "gibbs-layer" else
+                "Spikes_UNet(1->1, I=11), train step + intensity finite-difference step (2 no-grad forwards) "
+                "(350_stylized_layers/spikes11_layer_domain_GD.py:260-300)")
+        elif args.config == "c3":
+            workload = ("C3 full filter chain (disk 12.5 -> plane wave (55,55,30) I=15 -> wrap 0.5 -> S&P 0.05) "
+                        "+ 3D U-Net(4->3, 16..256, 2 res units) fwd/bwd/Adam(amsgrad), DiceLoss"
+                        + (" [random per-batch filter params, config 4]" if args.random_filters else "")
+                        + (f" [CHAIN {args.chain}: see bench.py --help]" if args.chain != "ref" else "")
+                        + (" [FILTER ONLY diagnostic]" if args.filter_only else ""))
+        else:
+            workload = "C2 Gibbs truncation: RandFourierDiskMaskd(r=12.5) low-pass alone, batched 4x128^3 volumes"
         line = {
             "metric": METRIC,
             "value": round(vols / elapsed, 4),
@@ -286,13 +337,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic BraTS-like z-scored 4-ch volumes resident in HBM; random-init U-Net",
             "config": {
-                "workload": (("C3 full filter chain (disk 12.5 -> plane wave (55,55,30) I=15 -> wrap 0.5 -> S&P 0.05) "
-                              "+ 3D U-Net(4->3, 16..256, 2 res units) fwd/bwd/Adam(amsgrad), DiceLoss")
-                             + (" [random per-batch filter params, config 4]" if args.random_filters else "")
-                             + (f" [CHAIN {args.chain}: see bench.py --help]" if args.chain != "ref" else "")
-                             + (" [FILTER ONLY diagnostic]" if args.filter_only else ""))
-                            if args.config == "c3" else
-                            "C2 Gibbs truncation: RandFourierDiskMaskd(r=12.5) low-pass alone, batched 4x128^3 volumes",
+                "workload": workload,
                 "volume": [C, H, W, D],
                 "unet_input": [B, C, H, W, D + pad],
                 "per_gpu_batch": B,

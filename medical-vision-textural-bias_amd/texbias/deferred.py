@@ -11,7 +11,7 @@ main process then runs the whole batch's plans on the GPU in one batched pass
 (``run_deferred``), after the default collation of everything else (``deferred_collate``).
 
 Guards (the deferred result must equal the eager one): the plan records the image's shape and an
-exact checksum of its bits when the first stage was deferred; ``run_deferred`` raises if the
+position-dependent digest of its bits when the first stage was deferred; ``run_deferred`` raises if the
 collated image differs -- i.e. if a transform that is not a texbias transform modified the image
 after a deferred filter (texbias transforms must close the Compose; ``SelectChanneld`` and
 ``MultimodalSlicesd`` defer too).  A batch holding plans cannot go through ``default_collate``
@@ -20,6 +20,7 @@ returning unfiltered images.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 from typing import Any, Dict, List, Optional
 
@@ -44,9 +45,10 @@ def active() -> bool:
 
 
 def _checksum(t: torch.Tensor) -> int:
-    """Exact, order-independent checksum of a float32 tensor's bits."""
-    x = torch.as_tensor(t).detach().to(torch.float32).contiguous()
-    return int(x.view(torch.int32).to(torch.int64).sum().item())
+    """Position-dependent digest (BLAKE2b) of a float32 tensor's bits: a transform that only moves
+    voxels (a flip, a transpose, a rot90) changes it as surely as one that changes values."""
+    x = torch.as_tensor(t).detach().to(device="cpu", dtype=torch.float32).contiguous()
+    return int.from_bytes(hashlib.blake2b(x.numpy().tobytes(), digest_size=16).digest(), "little")
 
 
 class TexbiasPlan:

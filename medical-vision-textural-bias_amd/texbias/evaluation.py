@@ -21,12 +21,17 @@ the validation Compose -- Spacingd(1.5, 1.5, 2.0) -> Orientationd(RAS) ->
 CenterSpatialCropd(128, 128, 64) -> NormalizeIntensityd(nonzero, channel_wise) -- with one named
 filter appended, one name at a time.  Here the Compose runs on the device over each collated
 batch: ``texbias.prep.BratsPrep`` (one resample gather + normalisation), then the filter as a
-``FusedChain``; the filter objects draw per sample in the same order as the reference's
-sequential, unshuffled loader.  ``ModelEvaluation`` loads ``Gibbs_UNet`` / ``Spikes_UNet``
+``FusedChain``.  Filter draws: indexed samples (the reference's ``test_ds`` read in the main
+process) draw sequentially from the filter object; batched iteration mirrors the reference's
+``DataLoader(batch_size=2, shuffle=False, num_workers=4)``, whose 4 worker processes each hold a copy of
+the transform's ``RandomState`` taken when the epoch starts and receive batches round-robin -- batch k
+draws from copy k % 4 (``loader_workers``).  Per-sample draw parity with MONAI's loader is unpinned
+(MONAI absent); the mapping restates torch's worker assignment.  ``ModelEvaluation`` loads ``Gibbs_UNet`` / ``Spikes_UNet``
 checkpoints like the reference (``gibbs_unet=`` / ``spikes_unet=``, utils.py:286-297).
 """
 from __future__ import annotations
 
+import copy
 import json
 import math
 from typing import Dict, Iterable, Optional, Tuple
@@ -194,8 +199,12 @@ class _FilteredSplit:
 
     def __iter__(self):
         ids, bs = self.owner.test_indices, self.owner.batch_size if self.batched else 1
-        for b0 in range(0, len(ids), bs):
-            d = self._run(ids[b0:b0 + bs])
+        nw = self.owner.loader_workers if self.batched else 1
+        # batched: one copy of the filter per loader worker, taken at the start of the epoch; batch k
+        # goes to worker k % nw (torch's DataLoader order with shuffle=False)
+        copies = [copy.deepcopy(self.owner.transforms[self.name]) for _ in range(nw)] if nw > 1 else None
+        for k, b0 in enumerate(range(0, len(ids), bs)):
+            d = self.owner.run(self.name, ids[b0:b0 + bs], copies[k % nw] if copies else None)
             if self.batched:
                 yield d
             else:
@@ -211,16 +220,19 @@ class BratsValIterDataset:
     reference's filter objects (e.g. ``{"sap10": SaltAndPepper(0.10)}``), each appended to the
     validation Compose in turn.  ``return_loader``: yield batched loaders (batch 2, unshuffled)
     instead of per-sample datasets.  ``split``: the ``random_split`` lengths; the test half is kept.
+    ``loader_workers``: worker copies of the filter's random state in batched iteration (the
+    reference's ``num_workers=4``; 1 = one sequential stream).
     """
 
     def __init__(self, source, transforms: Dict, return_loader: bool = False, batch_size: int = 2,
                  split: Tuple[int, int] = (48, 48), seed: int = 0, device: Optional[torch.device] = None,
-                 pixdim=VAL_PIXDIM, axcodes: str = "RAS", roi=VAL_ROI):
+                 pixdim=VAL_PIXDIM, axcodes: str = "RAS", roi=VAL_ROI, loader_workers: int = 4):
         from .prep import BratsPrep
         if len(source) != sum(split):
             raise ValueError(f"random_split lengths {split} do not sum to the dataset size {len(source)}")
         self.source, self.transforms = source, dict(transforms)
         self.return_loader, self.batch_size = return_loader, int(batch_size)
+        self.loader_workers = max(1, int(loader_workers))
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         # torch.utils.data.random_split: randperm(n, generator) then consecutive lengths
         perm = torch.randperm(sum(split), generator=torch.Generator().manual_seed(seed)).tolist()
@@ -228,15 +240,16 @@ class BratsValIterDataset:
         self.prep = BratsPrep(roi_size=roi, flip_prob=0.0, scale_prob=0.0, shift_prob=0.0, pixdim=pixdim,
                               axcodes=axcodes, center_crop=True)
 
-    def run(self, name: str, idx) -> Dict[str, torch.Tensor]:
-        """The validation Compose + filter ``name`` on the samples ``idx`` (one device batch)."""
+    def run(self, name: str, idx, transform=None) -> Dict[str, torch.Tensor]:
+        """The validation Compose + filter ``name`` (or ``transform``, a worker's copy of it) on the
+        samples ``idx`` (one device batch)."""
         from .pipeline import FusedChain
         items = [self.source[i] for i in idx]
         img = torch.stack([torch.as_tensor(it[0], dtype=torch.float32) for it in items]).to(self.device)
         lab = torch.stack([torch.as_tensor(it[1], dtype=torch.float32) for it in items]).to(self.device)
         affs = [np.asarray(it[2], dtype=float) if len(it) > 2 else np.eye(4) for it in items]
         x, y = self.prep(img, lab, affines=affs)
-        x = FusedChain([self.transforms[name]])(x)
+        x = FusedChain([transform if transform is not None else self.transforms[name]])(x)
         return {"image": x, "label": y}
 
     def __iter__(self):

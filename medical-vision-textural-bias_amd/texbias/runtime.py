@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import threading
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -19,7 +20,8 @@ from ._lib import TexbiasError, check, lib
 from .kprog import Geometry, geometry, split_program
 
 _plans: Dict[Tuple[int, int, int, int], "Plan"] = {}
-_ws: Dict[Tuple[int, int], torch.Tensor] = {}
+_ws: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
+_ws_lock = threading.Lock()
 _mm: Dict[int, torch.Tensor] = {}
 _lock = threading.Lock()
 
@@ -76,27 +78,36 @@ def _ws_key(device: torch.device) -> Tuple[int, int]:
     return idx, torch.cuda.current_stream(torch.device("cuda", idx)).cuda_stream
 
 
-def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+# Bounded LRU caches: a caller that makes a fresh stream per iteration (or per thread) would otherwise
+# keep one spectrum-sized workspace per stream it ever used.  An evicted workspace was allocated on its
+# own stream, so the caching allocator hands its memory out again only in that stream's order.
+_WS_CAP = 8
+
+
+def _cached_ws(cache: "OrderedDict[Tuple[int, int], torch.Tensor]", device: torch.device, nbytes: int) -> torch.Tensor:
     key = _ws_key(device)
-    ws = _ws.get(key)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", key[0]))
-        _ws[key] = ws
+    with _ws_lock:
+        ws = cache.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", key[0]))
+        cache[key] = ws
+        cache.move_to_end(key)
+        while len(cache) > _WS_CAP:
+            cache.popitem(last=False)
     return ws
 
 
-_ws_prep: Dict[Tuple[int, int], torch.Tensor] = {}
+def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    return _cached_ws(_ws, device, nbytes)
+
+
+_ws_prep: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
 
 
 def workspace_prep(device: torch.device, nbytes: int) -> torch.Tensor:
     """Small per-(device, stream) workspace of the preprocessing statistics (kept apart from the
     spectrum workspace so neither reallocates the other)."""
-    key = _ws_key(device)
-    ws = _ws_prep.get(key)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=torch.device("cuda", key[0]))
-        _ws_prep[key] = ws
-    return ws
+    return _cached_ws(_ws_prep, device, nbytes)
 
 
 def _stream(device: torch.device) -> int:

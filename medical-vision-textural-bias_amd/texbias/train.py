@@ -118,3 +118,27 @@ def gibbs_gd(inputs: torch.Tensor, labels: torch.Tensor, model: torch.nn.Module,
         buf /= dist.get_world_size()
     layer.alpha.copy_(old - learning_rate * buf[0].to(old.dtype))
     return buf[1], layer.alpha.clone()
+
+
+@torch.no_grad()
+def spike_gd(inputs: torch.Tensor, labels: torch.Tensor, model: torch.nn.Module, loss_fn, layer=None,
+             h: float = 0.05, learning_rate: float = 0.1) -> Tuple[torch.Tensor, float]:
+    """Finite-difference update of a spike layer's log-intensity (the spike drivers' Gibbs_GD,
+    10_scripts/300_instutional_distribution/350_stylized_layers/spikes11_layer_domain_GD.py:260-275):
+    loss at I and at I + h on the same batch (each forward draws its own spike location, as the
+    reference's fresh RandKSpaceSpikeNoise does), I <- I - learning_rate * (L_h - L_0) / h.  The layer
+    keeps I on the host (it builds the transform from ``intensity.item()``), so the update reads the
+    slope back once per step, as the reference's ``.item()`` does.  Data-parallel: the slope and L_0
+    are averaged over the ranks first (one 2-float all-reduce).  Returns (L_0 device tensor, new I)."""
+    if layer is None:
+        layer = getattr(model, "module", model).spike
+    old = layer.intensity.clone()
+    l0 = loss_fn(model(inputs), labels)
+    layer.intensity = old + h
+    lh = loss_fn(model(inputs), labels)
+    buf = torch.stack([(lh - l0) / h, l0]).to(torch.float32)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+        buf /= dist.get_world_size()
+    layer.intensity = old - learning_rate * float(buf[0].item())
+    return buf[1], float(layer.intensity.item())

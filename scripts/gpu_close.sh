@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 3 perf record: bench C3 (with CPU baseline), C2, C5; filter-only C3 + PMC FETCH/WRITE passes for
+# Closing perf record: bench C3 (with CPU baseline), C2, C5; filter-only C3 + PMC FETCH/WRITE passes for
 # roofline.traffic; rocprofv3 kernel trace of the C3 train step (steady-state window).  Usage: TAG
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/${1:-r3f}; mkdir -p $O
+O=gpurun_out/${1:-close}; mkdir -p $O
 run() { local n=$1; shift; timeout -k 10 600 python3 -u bench.py "$@" > $O/$n.json 2> $O/$n.err || { echo "$n failed"; tail -5 $O/$n.err; exit 1; }; cut -c1-220 $O/$n.json; }
 run bench_c3
 run bench_c2 --config c2 --no-cpu-baseline

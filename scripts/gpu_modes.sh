@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 3: GPU tests (optional), then filter-only bench lines of every chain mode (ref, planes, wrap,
+# GPU tests (optional), then filter-only bench lines of every chain mode (ref, planes, wrap,
 # gibbs-aug, spikes-aug) with a rocprofv3 kernel-trace summary each.  Usage (GPU box): TAG [tests|all|none]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/${1:-r3m}; mkdir -p $O
+O=gpurun_out/${1:-modes}; mkdir -p $O
 if [ "${2:-none}" = all ]; then
   timeout -k 10 800 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > $O/tests_all.log 2>&1
   rc=$?; tail -3 $O/tests_all.log; [ $rc = 0 ] || { grep -E "FAILED|Error" $O/tests_all.log | head -20 | cut -c1-300; exit $rc; }

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 3: PMC counters of the filter chain kernels (pass_bench C3, no flush), one counter group per
-# pass, plus the list of counters.  Usage (GPU box): bash scripts/gpu_r3_pmc.sh TAG
+# PMC counters of the filter chain kernels (pass_bench C3, no flush), one counter group per
+# pass, plus the list of counters.  Usage (GPU box): bash scripts/gpu_pmc.sh TAG
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-r3m}
@@ -14,8 +14,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d $O/pmc$i -o run -- python3 scripts/pass_bench.py --config c3 --iters 5 --warmup 2 --flush-mb 0 > $O/pmc$i.out 2> $O/pmc$i.err || { echo "pmc $i failed"; tail -3 $O/pmc$i.err; }
 done
 
-for v in sap64 sap128; do
-  TEXBIAS_LIB=$GRAFT_REPO_ROOT/var/$v.so timeout -k 10 120 python -u scripts/pass_bench.py --config c3 --iters 30 --flush-mb 0 --tag $v > $O/$v.json 2> $O/$v.err || { echo "$v failed"; tail -3 $O/$v.err; exit 1; }
-  cat $O/$v.json
-done
 echo done

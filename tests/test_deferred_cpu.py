@@ -68,3 +68,26 @@ def test_guard_catches_late_modification():
         set_deferred(None)
     with pytest.raises(RuntimeError, match="changed after a deferred"):
         run_deferred(batch, device=torch.device("cpu"))
+
+
+def test_guard_catches_late_flip():
+    """A transform that only rearranges voxels (a flip keeps every value, so an order-independent
+    checksum would pass it) after a deferred filter is caught too."""
+    from texbias.deferred import deferred_collate, run_deferred, set_deferred
+
+    class Flip:
+        def __call__(self, d):
+            d = dict(d)
+            d["image"] = torch.flip(torch.as_tensor(d["image"]), dims=[-1])
+            return d
+
+    import filters_and_operators as F
+    ts = [F.WrapArtifactd("image", 0.5), Flip()]
+    set_deferred(True)
+    try:
+        ds = DictSet(ts)
+        batch = deferred_collate([ds[0], ds[1]])
+    finally:
+        set_deferred(None)
+    with pytest.raises(RuntimeError, match="changed after a deferred"):
+        run_deferred(batch, device=torch.device("cpu"))
