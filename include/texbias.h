@@ -16,6 +16,8 @@
  *                          + KSpaceSpikeNoise.__call__ / _set_spike                    :906-983
  *                          + GibbsNoiseLayer.forward / _apply_mask   stylization_layers.py:79-116
  *                          (one fused forward-FFT -> op program -> inverse-FFT round trip)
+ *   tb_planes_closed_form_f32  RandPlaneWaves_ellipsoid.__call__ / KSpaceSpikeNoise._set_spike in
+ *                          closed form (spike-only programs)                    :370-393, 966-983
  *   tb_salt_pepper_f32     SaltAndPepper.salt_and_pepper             filters_and_operators.py:465-482
  *   tb_minmax_f32          the x.max()/2, x.min()/2 of SaltAndPepper                   :476
  *   tb_disk_mask_f32       disk_mask.binary_mask_2d / binary_mask_3d                   :136-197
@@ -102,6 +104,18 @@ int tb_plan_radices(const tb_plan* plan, int axis, int* radices);
 int tb_kspace_filter_f32(const tb_plan* plan, const float* x, const int64_t* xs, float* y, const int64_t* ys,
                          int y_pad, void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops,
                          uint32_t* minmax, void* stream);
+
+/*
+ * The closed-form spike route on its own (SURVEY §8b's planes entry): RandPlaneWaves_ellipsoid.__call__
+ * (filters_and_operators.py:370-393) and KSpaceSpikeNoise._set_spike (:966-983) for programs made only
+ * of spikes that do not touch (no two at equal or conjugate frequencies in a shared channel):
+ *   y = x + Re( sum_j Delta_j e^{2 pi i f_j . n / N} ) / N,   Delta_j = target_j(K(f_j)) - K(f_j)
+ * Same arguments and results as tb_kspace_filter_f32 (which routes such programs here by itself);
+ * TB_ERR_INVALID_ARG when a program is not of that form.  ws >= tb_workspace_bytes(plan, B * C).
+ */
+int tb_planes_closed_form_f32(const tb_plan* plan, const float* x, const int64_t* xs, float* y, const int64_t* ys,
+                              int y_pad, void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops,
+                              uint32_t* minmax, void* stream);
 
 /*
  * Salt and pepper over B samples of `rows` rows of `len` floats (row pitch `ld`, sample pitch `sb`):

@@ -927,7 +927,7 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
       }
       if (run.route == RUN_FULL && g_band && band_plan(p, ops, run.s0, run.s1, y_pad, ws_bytes, B * C, run.g, run.sp))
         run.route = RUN_BAND;
-      atomic_keys |= run.route != RUN_BAND && run.route != RUN_WRAP;  // these two write their keys outright
+      atomic_keys |= run.route == RUN_COPY || run.route == RUN_FULL;  // the other routes write their keys outright
       runs.push_back(run);
       i = j;
     }
@@ -1003,6 +1003,23 @@ int tb_kspace_filter_f32(const tb_plan* p, const float* x, const int64_t* xs, fl
     return p->rset_h == RS_SMALL ? kspace_filter<RS_SMALL, RS_SMALL>(TB_ARGS) : kspace_filter<RS_SMALL, RS_ALL>(TB_ARGS);
   return p->rset_h == RS_SMALL ? kspace_filter<RS_ALL, RS_SMALL>(TB_ARGS) : kspace_filter<RS_ALL, RS_ALL>(TB_ARGS);
 #undef TB_ARGS
+}
+
+int tb_planes_closed_form_f32(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys,
+                              int y_pad, void* ws, size_t ws_bytes, int B, int C, const tb_sample_ops* ops,
+                              uint32_t* minmax, void* stream) {
+  if (!p || !x || !y || !xs || !ys || !ops || B < 1 || C < 1 || y_pad < 0 || !ws) return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb::point_ws(B * C).total) return TB_ERR_WORKSPACE;
+  for (int b = 0; b < B; ++b)
+    if (ops[b].n < 1 || ops[b].n > TB_MAX_OPS || !tb::point_program(ops[b], p->dev.H, p->dev.W, p->dev.D))
+      return TB_ERR_INVALID_ARG;  // not spike-only, or two spikes touch: tb_kspace_filter_f32 takes those
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
+    const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;
+    const int rc = run_point(p, x, xs, y, ys, y_pad, static_cast<char*>(ws), b0, nb, C, ops, minmax, st);
+    if (rc) return rc;
+  }
+  return TB_OK;
 }
 
 int tb_kspace_logabs_sum_f32(const tb_plan* p, const float* x, const int64_t* xs, void* ws, size_t ws_bytes, int B,

@@ -34,6 +34,7 @@ def _proto(L):
         "tb_workspace_bytes": (SZ, [P, I]),
         "tb_plan_radices": (I, [P, I, P]),
         "tb_kspace_filter_f32": (I, [P, P, P, P, P, I, P, SZ, I, I, P, P, P]),
+        "tb_planes_closed_form_f32": (I, [P, P, P, P, P, I, P, SZ, I, I, P, P, P]),
         "tb_salt_pepper_f32": (I, [P, P, P, P, U64, U64, P, P, I, I64, I, I64, I64, P]),
         "tb_minmax_f32": (I, [P, P, I, I64, I, I64, I64, P]),
         "tb_key_to_float": (F, [C.c_uint32]),

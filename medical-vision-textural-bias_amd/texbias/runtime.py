@@ -177,9 +177,18 @@ def kspace_filter(x: torch.Tensor, n_dims: int, programs: Sequence[Sequence], ch
     return y
 
 
+def planes_closed_form(x: torch.Tensor, n_dims: int, programs: Sequence[Sequence], channels: int,
+                       out: Optional[torch.Tensor] = None, pad: int = 0,
+                       minmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The closed-form spike route alone (``tb_planes_closed_form_f32``): ``kspace_filter`` for
+    programs made only of spikes that do not touch; raises for any other program."""
+    require_hip(x, "planes_closed_form")
+    return _kspace_filter_pass(x, n_dims, programs, channels, out, pad, minmax, entry="tb_planes_closed_form_f32")
+
+
 def _kspace_filter_pass(x: torch.Tensor, n_dims: int, programs: Sequence[Sequence], channels: int,
                         out: Optional[torch.Tensor] = None, pad: int = 0,
-                        minmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        minmax: Optional[torch.Tensor] = None, entry: str = "tb_kspace_filter_f32") -> torch.Tensor:
     """One launch group of ``kspace_filter`` (every program at most TB_MAX_OPS ops)."""
     geo = geometry(x.shape[x.dim() - n_dims:])
     H, W, D = geo.hwd
@@ -219,9 +228,8 @@ def _kspace_filter_pass(x: torch.Tensor, n_dims: int, programs: Sequence[Sequenc
             if minmax.dtype != torch.int32 or minmax.numel() < 2 * B or minmax.device != x.device:
                 raise TexbiasError("minmax must be an int32 [B,2] tensor on the input's device")
             mm_ptr = minmax.data_ptr()
-        check(lib().tb_kspace_filter_f32(plan.handle, x.data_ptr(), xs, out.data_ptr(), ys, pad, ws.data_ptr(),
-                                         ws.numel(), B, channels, C.addressof(progs), mm_ptr, _stream(x.device)),
-              "tb_kspace_filter_f32")
+        check(getattr(lib(), entry)(plan.handle, x.data_ptr(), xs, out.data_ptr(), ys, pad, ws.data_ptr(),
+                                    ws.numel(), B, channels, C.addressof(progs), mm_ptr, _stream(x.device)), entry)
     return out
 
 

@@ -156,3 +156,20 @@ def test_planes_in_place_strided(rt):
     ref = O.plane_waves(x0[1].cpu().numpy(), (4, 6, 7), 10.0)
     assert relerr(view[1].cpu().numpy(), ref) < 1e-5
 
+
+
+def test_planes_closed_form_entry(rt):
+    """tb_planes_closed_form_f32 (SURVEY §8b's planes entry) == tb_kspace_filter_f32's own routing of a
+    spike-only program, bit for bit; other programs are refused."""
+    torch.manual_seed(12)
+    shape = (2, 4, 240, 240, 155)
+    x = torch.randn(shape, device="cuda")
+    progs = [[spike((55, 55, 30), shape[2:], 15.0)], [spike((3, 200, 70), shape[2:], 12.0)]]
+    mm_a = torch.empty((2, 2), dtype=torch.int32, device="cuda")
+    mm_b = torch.empty((2, 2), dtype=torch.int32, device="cuda")
+    ya = rt.planes_closed_form(x, 3, progs, 4, pad=5, minmax=mm_a)
+    yb = rt.kspace_filter(x, 3, progs, 4, pad=5, minmax=mm_b)
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb) and torch.equal(mm_a, mm_b)
+    with pytest.raises(rt.TexbiasError):
+        rt.planes_closed_form(x, 3, [[K.wrap_op(0.5)]] * 2, 4)
