@@ -69,6 +69,55 @@ __global__ __launch_bounds__(NT) void k_kspace_ct2(KspaceArgs) {
   if (tid < P::N0 / 2) ct::b_s1_pair<P>(lds, Sc, ncols, tid);
 }
 
+// Persistent paired variant: ncu x occupancy workgroups walk the (bc, tile) units u = blockIdx.x,
+// + gridDim.x, ...; each unit's stage-0 inputs are loaded into registers while the previous unit
+// runs its middle and inverse phases (one unit of HBM reads always in flight per workgroup, instead
+// of every short-lived workgroup paying the HBM latency before any of its arithmetic starts).
+template <int H, int T, int NT>
+__global__ __launch_bounds__(NT) void k_kspace_ct2p(KspaceArgs) {
+  using P = ct::TilePlan<H, T>;
+  static_assert(P::N0 / 2 <= NT && P::NM % NT == 0 && NT % T == 0, "paired items");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const KspaceArgs& a = kargs<KspaceArgs>();
+  const int tid = (int)threadIdx.x;
+  const int ncols = a.pl.W * (a.pl.D / 2 + 1);
+  const int ntile = ncols / T, units = ntile * a.nbc;
+  const bool ld = tid < P::N0 / 2;
+  for (int i = tid; i < H; i += NT) lds[P::OFF_TW + i] = ct::V(a.pl.tw[0][i].x, a.pl.tw[0][i].y);
+  auto col0 = [&](int u, int& bcl) {
+    bcl = u / ntile;
+    return (u - bcl * ntile) * T;
+  };
+  ct::f4 r[P::Q0];
+  int u = (int)blockIdx.x;
+  if (u < units && ld) {
+    int bcl;
+    const int j0 = col0(u, bcl);
+    ct::b_load_pair<P>(r, reinterpret_cast<const v2*>(a.S) + (int64_t)(a.bc0 + bcl) * H * ncols + j0, ncols, tid);
+  }
+  for (; u < units; u += (int)gridDim.x) {
+    int bcl;
+    const int j0 = col0(u, bcl);
+    v2* Sc = reinterpret_cast<v2*>(a.S) + (int64_t)(a.bc0 + bcl) * H * ncols + j0;
+    const FreqCol fc = ct::tile_col(a.pl, j0 + tid % T);
+    __syncthreads();  // the previous unit's inverse-stage reads of the tile are done (and the twiddles are in)
+    if (ld) ct::b_s0_pair_regs<P>(lds, r, tid);
+    {  // the next unit's inputs, in flight during the middle and inverse phases (clamped on the last pass)
+      const int un = u + (int)gridDim.x < units ? u + (int)gridDim.x : u;
+      int bn;
+      const int jn = col0(un, bn);
+      if (ld) ct::b_load_pair<P>(r, reinterpret_cast<const v2*>(a.S) + (int64_t)(a.bc0 + bn) * H * ncols + jn, ncols, tid);
+    }
+    __syncthreads();
+    const int sl = a.cofs + bcl;
+#pragma unroll 1
+    for (int s = 0; s < P::NM / NT; ++s) ct::b_mid_lds<P>(lds, a.ops.s[sl / a.C], sl % a.C, fc, tid + s * NT);
+    __syncthreads();
+    if (ld) ct::b_s1_pair<P>(lds, Sc, ncols, tid);
+  }
+}
+
 }  // namespace
 
 bool kspace_ct_supported(int H) {
@@ -99,8 +148,45 @@ static int pair_tile() {
 
 int kspace_ct_tile(int ncols) { return use_pair(ncols) ? pair_tile() : ct::kCtTileT; }
 
-hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st) {
+// persistent pass B (TEXBIAS_KSPACE_PERSIST=0: the one-tile-per-workgroup grid)
+static bool use_persist() {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_KSPACE_PERSIST");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+template <class K>
+static int kspace_occupancy(K kern, int nt, size_t lds) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(reinterpret_cast<const void*>(kern));
+  if (it != cache.end()) return it->second;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, nt, lds) != hipSuccess || occ < 1) occ = 1;
+  cache[reinterpret_cast<const void*>(kern)] = occ;
+  return occ;
+}
+
+hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t st) {
   const bool pair = use_pair(a.pl.W * (a.pl.D / 2 + 1));
+  if (pair && use_persist() && pair_tile() == 16) {
+#define TB_X(h)                                                                           \
+    if (a.pl.H == h) {                                                                    \
+      constexpr size_t lds = ct::TilePlan<h, 16>::LDS_BYTES;                              \
+      hipError_t e = allow_lds(k_kspace_ct2p<h, 16, 128>, lds);                           \
+      if (e != hipSuccess) return e;                                                      \
+      const int units = (int)(grid.x * grid.y);                                           \
+      int g = ncu * kspace_occupancy(k_kspace_ct2p<h, 16, 128>, 128, lds);                \
+      g = g < units ? g : units;                                                          \
+      hipLaunchKernelGGL((k_kspace_ct2p<h, 16, 128>), dim3(g), dim3(128), lds, st, a);    \
+      return hipGetLastError();                                                           \
+    }
+    TB_CT_TILE_H(TB_X)
+#undef TB_X
+  }
 #define TB_X(h)                                                                         \
   if (a.pl.H == h && pair && pair_tile() == 8) {                                        \
     constexpr size_t lds = ct::TilePlan<h, 8>::LDS_BYTES;                               \

@@ -148,13 +148,11 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
   const float* xrd = stg + role * a.RS + g * D + 8 * kb;                            // + 32 s + j
   int cur = -1;
   float lo = FLT_MAX, hi = -FLT_MAX;
-  for (int u = ub + wv; u < ue; u += WRAP_NT / 64) {
+  // the quad's four role chunks (rows 4 gq + rw W/2 + g of slabs hq + rh H/2) of unit u into v
+  auto load_unit = [&](int u, float4 (&v)[4][NF]) {
     const int bcl = u / per_bc, rem = u - bcl * per_bc, hq = rem / NG, gq = rem - hq * NG;
-    const int bc = a.bc0 + bcl, sl = bcl / a.C;
+    const int bc = a.bc0 + bcl;
     const int nrow = Wh - 4 * gq < 4 ? Wh - 4 * gq : 4, len = nrow * D;
-    const float w00 = wts[sl][0], w10 = wts[sl][1], w01 = wts[sl][2], w11 = wts[sl][3];
-    // ---- the quad's four role chunks (rows 4 gq + rw W/2 + g of slabs hq + rh H/2), 2-tap combine
-    float4 v[4][NF];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float* xr = a.x + (int64_t)bc * a.xsbc + (int64_t)(hq + (r & 1) * Hh) * a.xsh +
@@ -185,6 +183,14 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
         }
       }
     }
+  };
+  float4 v[4][NF];
+  if (ub + wv < ue) load_unit(ub + wv, v);
+  for (int u = ub + wv; u < ue; u += WRAP_NT / 64) {
+    const int bcl = u / per_bc, rem = u - bcl * per_bc, hq = rem / NG, gq = rem - hq * NG;
+    const int bc = a.bc0 + bcl, sl = bcl / a.C;
+    const int nrow = Wh - 4 * gq < 4 ? Wh - 4 * gq : 4;
+    const float w00 = wts[sl][0], w10 = wts[sl][1], w01 = wts[sl][2], w11 = wts[sl][3];
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
@@ -217,6 +223,8 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
           *reinterpret_cast<float4*>(stg + r * a.RS + 4 * f) = make_float4(s4.x * sx, s4.y * sx, s4.z * sx, s4.w * sx);
         }
       }
+    // the wave's next unit: its loads fly during this unit's products and stores
+    if (u + WRAP_NT / 64 < ue) load_unit(u + WRAP_NT / 64, v);
     // ---- T_d: Y^T = K^T X^T in split f16
     f32x4v acc[NTO];
 #pragma unroll
@@ -257,6 +265,11 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
     }
     float* yrow = a.y + (int64_t)bc * a.ysbc + (int64_t)(hq + (role & 1) * Hh) * a.ysh +
                   (int64_t)(4 * gq + (role >> 1) * Wh + g) * a.ysw;
+    // per-lane column limits, opaque to the compiler: hoisted out of the unit loop, the 40 compares
+    // below became SGPR-pair masks that spilled to VGPR lanes and came back by ~240 v_readlane per unit
+    int dq = D - 4 * kb, nq = ncolo - 4 * kb;  // column 16 t + 4 kb + r is an image / stored column
+    asm volatile("" : "+v"(dq), "+v"(nq));
+    const int dqr = rowok ? dq : -(1 << 20), nqr = rowok ? nq : -(1 << 20);
 #pragma unroll
     for (int t = 0; t < NTO; ++t) {
       if (16 * t >= ncolo) break;  // wave-uniform
@@ -264,17 +277,17 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
       float o[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool in = d0 + r < D;
-        o[r] = in ? acc[t][r] * inv : 0.f;
-        lo = fminf(lo, (in && rowok) ? o[r] : FLT_MAX);
-        hi = fmaxf(hi, (in && rowok) ? o[r] : -FLT_MAX);
+        o[r] = 16 * t + r < dq ? acc[t][r] * inv : 0.f;
+        const bool in = 16 * t + r < dqr;
+        lo = fminf(lo, in ? o[r] : FLT_MAX);
+        hi = fmaxf(hi, in ? o[r] : -FLT_MAX);
       }
       if (vst && 16 * t + 16 <= ncolo) {  // wave-uniform: the whole tile inside the stored row
         if (rowok) *reinterpret_cast<float4*>(yrow + d0) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (rowok && d0 + r < ncolo) yrow[d0 + r] = o[r];
+          if (16 * t + r < nqr) yrow[d0 + r] = o[r];
       }
     }
   }

@@ -37,6 +37,7 @@ struct KspaceArgs {
   int bc0, C, T;
   int cofs;  // channel-volume index of blockIdx.y = 0 within ops (bc0 - first sample's bc)
   BatchOps ops;
+  int nbc;   // channel-volumes of the launch (the persistent pass B walks nbc * tiles units)
 };
 
 struct SlabInvArgs {
@@ -74,7 +75,7 @@ hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st);
 // Compile-time pass-B plans (kspace_ct.h, kern_kspace_ct.hip): tile width kspace_ct_tile() columns.
 bool kspace_ct_supported(int H);
 int kspace_ct_tile(int ncols);
-hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, hipStream_t st);
+hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t st);
 
 // Direct-DFT fallback (kern_generic.hip) for sizes the mixed-radix passes do not take: full complex
 // spectrum in two ping-pong buffers S[2][nbc][H][W][D] (gen_workspace_bytes).

@@ -147,6 +147,34 @@ TB_HD void b_mid(v2* lds, const SO& so, int chan, const FreqCol& fc, int it) {
   TB_UNROLL
   for (int q = 0; q < P::Q1; ++q) t[q * P::T] = a[q];
 }
+// b_mid with the op program applied one coefficient at a time from the LDS tile (a rolled loop over
+// the butterfly's Q1 coefficients, apply_ops per coefficient): the fully unrolled ops_bfly keeps every
+// op kind's code for all Q1 coefficients live and pins pass B at 256 VGPRs (1 wave per SIMD).
+template <class P, class SO>
+TB_HD void b_mid_lds(v2* lds, const SO& so, int chan, const FreqCol& fc, int it) {
+  const int blk = it / P::T, c = it - blk * P::T;
+  v2* t = lds + (blk * P::L) * P::T + c;
+  v2 a[P::Q1];
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) a[q] = t[q * P::T];
+  Dv<P::Q1, true>::run(a);
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) t[q * P::T] = a[q];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+  for (int q = 0; q < P::Q1; ++q) {  // slot blk*L + q holds kh = blk + Q0*q
+    const v2 v = t[q * P::T];
+    const cf o = apply_ops(so, chan, mk(v.x, v.y), fc, blk + P::Q0 * q, P::H);
+    t[q * P::T] = V(o.x, o.y);
+  }
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) a[q] = t[q * P::T];
+  Dv<P::Q1, false>::run(a);
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) t[q * P::T] = a[q];
+}
+
 template <class P>
 TB_HD void b_s1(const v2* lds, v2* __restrict__ Sc, int64_t ncols, int it) {
   const int j = it / P::T, c = it - j * P::T;
@@ -178,6 +206,39 @@ TB_HD void b_s0_pair(v2* lds, const v2* __restrict__ Sc, int64_t ncols, int it) 
     const f4 u = s[q * st];
     a[q] = V(u.x, u.y);
     b[q] = V(u.z, u.w);
+  }
+  const v2* tw = lds + P::OFF_TW;
+  Dv<P::Q0, true>::run(a);
+  Dv<P::Q0, true>::run(b);
+  f4* t = reinterpret_cast<f4*>(lds + j * P::T + c);
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) {
+    v2 x = a[q], y = b[q];
+    if (q && j) {
+      const v2 w = tw[j * q];
+      x = cmul(x, w);
+      y = cmul(y, w);
+    }
+    t[q * P::L * P::T / 2] = f4{x.x, x.y, y.x, y.y};
+  }
+}
+// b_s0_pair split in two for the persistent pass B: the loads (issued one unit ahead) and the DFT
+template <class P>
+TB_HD void b_load_pair(f4* r, const v2* __restrict__ Sc, int64_t ncols, int it) {
+  const int j = it / (P::T / 2), c = 2 * (it - j * (P::T / 2));
+  const f4* s = reinterpret_cast<const f4*>(Sc + (int64_t)j * ncols + c);
+  const int64_t st = (int64_t)P::L * (ncols / 2);
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) r[q] = s[q * st];
+}
+template <class P>
+TB_HD void b_s0_pair_regs(v2* lds, const f4* r, int it) {
+  const int j = it / (P::T / 2), c = 2 * (it - j * (P::T / 2));
+  v2 a[P::Q0], b[P::Q0];
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) {
+    a[q] = V(r[q].x, r[q].y);
+    b[q] = V(r[q].z, r[q].w);
   }
   const v2* tw = lds + P::OFF_TW;
   Dv<P::Q0, true>::run(a);

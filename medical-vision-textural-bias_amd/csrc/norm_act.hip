@@ -6,10 +6,11 @@
 // batch_norm over [1, N*C, ...] (few, huge channels: one reduction block per channel) plus separate
 // PReLU kernels and a PReLU weight-gradient reduction -- ~30 ms of a 89 ms train step.  Here each
 // direction is two HBM sweeps over [N*C instances][S voxels] with the reductions split over the
-// whole grid (float per-lane partials over <= 64 voxels, double across lanes, blocks and the grid):
+// whole grid (float64 per-thread partials, then across lanes, blocks and the grid):
 //   forward   K1 sums(x) -> K2 y = prelu((x - mean) * rstd)                  read 2S, write S
 //   backward  K3 sums(g, g z, dy z [z<=0]) -> K4 dx = rstd (g - mean g - z mean(g z))
 //             with z = (x - mean) rstd, g = dy * (z > 0 ? 1 : a)            read 4S, write S
+//             (backward arithmetic in float64 per voxel: see K3)
 // Statistics: biased variance, rstd = 1/sqrt(var + eps) (torch.nn.functional.instance_norm).
 #include <hip/hip_runtime.h>
 
@@ -74,7 +75,10 @@ __device__ __forceinline__ float prelu(float z, float a) { return z > 0.f ? z : 
 __global__ __launch_bounds__(NT) void k_in_stats(const float* __restrict__ x, double* __restrict__ acc, int64_t S,
                                                  int vec) {
   const Chunk c = chunk_of(S);
-  float s1 = 0.f, s2 = 0.f;
+  // float64 per thread (x^2 of a float32 is exact in float64): the statistics reach the backward's
+  // g - mean g - z mean(g z), whose cancellation at the top of the U-Net turns a 1e-6 error in
+  // rstd into a visible one in the input gradient (scripts/diag/grad_noise.py)
+  double s1 = 0.0, s2 = 0.0;
   if (vec) {
     const float4* p = reinterpret_cast<const float4*>(x + c.base + c.begin);
     const int n4 = (int)((c.end - c.begin) >> 2);
@@ -86,17 +90,18 @@ __global__ __launch_bounds__(NT) void k_in_stats(const float* __restrict__ x, do
     }
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
-      s2 += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
+      const double a = v[k].x, b = v[k].y, e = v[k].z, f = v[k].w;
+      s1 += (a + b) + (e + f);
+      s2 += (a * a + b * b) + (e * e + f * f);
     }
   } else {
     for (int64_t i = c.begin + threadIdx.x; i < c.end; i += NT) {
-      const float v = x[c.base + i];
+      const double v = x[c.base + i];
       s1 += v;
       s2 += v * v;
     }
   }
-  double r[2] = {(double)s1, (double)s2};
+  double r[2] = {s1, s2};
   block_atomic_add<2>(r, acc + 2 * blockIdx.y);
 }
 
@@ -243,18 +248,21 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_stats(const float* __restri
                                                            double* __restrict__ acc_a, int64_t S, int vec) {
   const Chunk c = chunk_of(S);
   const float mean = mean_in[blockIdx.y], rstd = rstd_in[blockIdx.y], a = *aw;
-  float s1 = 0.f, s2 = 0.f;
-  // the PReLU weight gradient is one scalar over every voxel of the layer whose terms cancel to
-  // 1e-6..1e-8 of their magnitude: its per-thread sum runs in float64, so this kernel adds nothing to
-  // the float32 noise its input gradient already carries (tests/test_gpu_train_prod.py)
-  double sa = 0.0;
+  const double md = mean, rd = rstd;
+  // Every sum runs in float64 per thread.  The PReLU weight gradient is one scalar over every voxel
+  // of the layer whose terms cancel to 1e-6..1e-8 of their magnitude, and K4's g - mean g - z mean(g z)
+  // cancels as deeply where the incoming gradient is nearly affine in z (the top of the U-Net):
+  // float32 rounding of z, g z or the partial sums there is what made the step's gradients several
+  // times noisier than ATen's (scripts/diag/grad_noise.py).  z is formed in float64 from the stored
+  // float32 statistics; the PReLU branch follows the forward's float32 z.
+  double s1 = 0.0, s2 = 0.0, sa = 0.0;
   auto visit = [&](float xv, float gv) {
-    const float z = (xv - mean) * rstd;
-    const bool pos = z > 0.f;
-    const float g = pos ? gv : a * gv;
+    const bool pos = (xv - mean) * rstd > 0.f;
+    const double z = ((double)xv - md) * rd;
+    const double g = pos ? (double)gv : (double)a * (double)gv;
     s1 += g;
     s2 += g * z;
-    sa += pos ? 0.0 : (double)gv * (double)z;
+    sa += pos ? 0.0 : (double)gv * z;
   };
   if (vec) {
     const float4* px = reinterpret_cast<const float4*>(x + c.base + c.begin);
@@ -282,7 +290,7 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_stats(const float* __restri
   } else {
     for (int64_t i = c.begin + threadIdx.x; i < c.end; i += NT) visit(x[c.base + i], dy[c.base + i]);
   }
-  double r[3] = {(double)s1, (double)s2, sa};
+  double r[3] = {s1, s2, sa};
   __shared__ double red[3][NT / 64];
 #pragma unroll
   for (int k = 0; k < 3; ++k) r[k] = wave_sum(r[k]);
@@ -310,13 +318,15 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_apply(const float* __restri
                                                            float* __restrict__ dw, int64_t S, int vec) {
   const Chunk c = chunk_of(S);
   const float mean = mean_in[blockIdx.y], rstd = rstd_in[blockIdx.y], a = *aw;
-  const float mg = (float)(acc[2 * blockIdx.y] / (double)S);
-  const float mgz = (float)(acc[2 * blockIdx.y + 1] / (double)S);
+  const double md = mean, rd = rstd;
+  const double mg = acc[2 * blockIdx.y] / (double)S;
+  const double mgz = acc[2 * blockIdx.y + 1] / (double)S;
   if (dw && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *dw = (float)(*acc_a);
-  auto f = [&](float xv, float gv) {
-    const float z = (xv - mean) * rstd;
-    const float g = z > 0.f ? gv : a * gv;
-    return rstd * (g - mg - z * mgz);
+  auto f = [&](float xv, float gv) {  // float64 combination (see K3): rounded once
+    const bool pos = (xv - mean) * rstd > 0.f;
+    const double z = ((double)xv - md) * rd;
+    const double g = pos ? (double)gv : (double)a * (double)gv;
+    return (float)(rd * (g - mg - z * mgz));
   };
   if (vec) {
     const float4* px = reinterpret_cast<const float4*>(x + c.base + c.begin);

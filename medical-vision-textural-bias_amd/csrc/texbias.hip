@@ -716,10 +716,10 @@ static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* 
       Timer t(1, st, 2.0 * spec, (g_compiled_plans && p->ct_tile) ? "k_kspace_ct2" : "k_kspace");
       if (g_compiled_plans && p->ct_tile) {
         const int Tc = tb::kspace_ct_tile(W * Dh);
-        KspaceArgs ka{p->dev, S, bc0, C, Tc, c0, bo};
-        TB_HIP(tb::launch_kspace_ct(ka, dim3((W * Dh + Tc - 1) / Tc, ng), st));
+        KspaceArgs ka{p->dev, S, bc0, C, Tc, c0, bo, ng};
+        TB_HIP(tb::launch_kspace_ct(ka, dim3((W * Dh + Tc - 1) / Tc, ng), p->ncu, st));
       } else {
-        KspaceArgs ka{p->dev, S, bc0, C, T, c0, bo};
+        KspaceArgs ka{p->dev, S, bc0, C, T, c0, bo, ng};
         TB_HIP(launch_kspace<RB>(ka, dim3(ntiles, ng), lds_b, st));
       }
     }
