@@ -21,6 +21,8 @@ namespace {
 
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x2v __attribute__((ext_vector_type(2)));
 
 constexpr float WRAP_K_SCALE = 64.f;  // circulant entries x 2^6 before the f16 split (lo parts stay normal)
 
@@ -191,6 +193,7 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
     const int bc = a.bc0 + bcl, sl = bcl / a.C;
     const int nrow = Wh - 4 * gq < 4 ? Wh - 4 * gq : 4;
     const float w00 = wts[sl][0], w10 = wts[sl][1], w01 = wts[sl][2], w11 = wts[sl][3];
+    // the H / W 2-tap combine at load time (it commutes with T_d; 4 FMAs per voxel)
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
@@ -234,15 +237,17 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
     for (int s = 0; s < KS; ++s) {
       float xv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[j] = xrd[32 * s + j];
+      for (int j = 0; j < 8; ++j) xv[j] = (rowok && 32 * s + 8 * kb + j < D) ? xrd[32 * s + j] : 0.f;
       h16x8 bh, bl;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float t = (rowok && 32 * s + 8 * kb + j < D) ? xv[j] : 0.f;
-        _Float16 h, l;
-        split_f16(t, h, l);
-        bh[j] = h;
-        bl[j] = l;
+      for (int j = 0; j < 8; j += 2) {  // packed conversions: v_cvt_pk_f16_f32
+        const f32x2v p = {xv[j], xv[j + 1]};
+        const h16x2v h = __builtin_convertvector(p, h16x2v);
+        const h16x2v l = __builtin_convertvector(p - __builtin_convertvector(h, f32x2v), h16x2v);
+        bh[j] = h[0];
+        bh[j + 1] = h[1];
+        bl[j] = l[0];
+        bl[j + 1] = l[1];
       }
 #pragma unroll
       for (int t = 0; t < NTO; ++t) {
@@ -265,22 +270,36 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
     }
     float* yrow = a.y + (int64_t)bc * a.ysbc + (int64_t)(hq + (role & 1) * Hh) * a.ysh +
                   (int64_t)(4 * gq + (role >> 1) * Wh + g) * a.ysw;
-    // per-lane column limits, opaque to the compiler: hoisted out of the unit loop, the 40 compares
-    // below became SGPR-pair masks that spilled to VGPR lanes and came back by ~240 v_readlane per unit
+    // Tiles whose 16 columns are all image columns, in a unit whose 16 rows all exist (wave-uniform),
+    // store and reduce without per-lane predicates; the rest compare against per-lane limits that are
+    // opaque to the compiler (hoisted out of the unit loop, the compares became SGPR-pair masks that
+    // spilled to VGPR lanes and came back by ~240 v_readlane per unit).
     int dq = D - 4 * kb, nq = ncolo - 4 * kb;  // column 16 t + 4 kb + r is an image / stored column
     asm volatile("" : "+v"(dq), "+v"(nq));
     const int dqr = rowok ? dq : -(1 << 20), nqr = rowok ? nq : -(1 << 20);
+    const bool full = nrow == 4;
 #pragma unroll
     for (int t = 0; t < NTO; ++t) {
       if (16 * t >= ncolo) break;  // wave-uniform
       const int d0 = 16 * t + 4 * kb;
       float o[4];
+      if (full && 16 * t + 16 <= D) {  // wave-uniform fast path
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        o[r] = 16 * t + r < dq ? acc[t][r] * inv : 0.f;
-        const bool in = 16 * t + r < dqr;
-        lo = fminf(lo, in ? o[r] : FLT_MAX);
-        hi = fmaxf(hi, in ? o[r] : -FLT_MAX);
+        for (int r = 0; r < 4; ++r) o[r] = acc[t][r] * inv;
+        lo = fminf(lo, fminf(fminf(o[0], o[1]), fminf(o[2], o[3])));
+        hi = fmaxf(hi, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+        if (vst) {
+          *reinterpret_cast<float4*>(yrow + d0) = make_float4(o[0], o[1], o[2], o[3]);
+          continue;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[r] = 16 * t + r < dq ? acc[t][r] * inv : 0.f;
+          const bool in = 16 * t + r < dqr;
+          lo = fminf(lo, in ? o[r] : FLT_MAX);
+          hi = fmaxf(hi, in ? o[r] : -FLT_MAX);
+        }
       }
       if (vst && 16 * t + 16 <= ncolo) {  // wave-uniform: the whole tile inside the stored row
         if (rowok) *reinterpret_cast<float4*>(yrow + d0) = make_float4(o[0], o[1], o[2], o[3]);

@@ -80,6 +80,21 @@ def main():
     print("parameter gradients (normwise vs float64):")
     for n in gtb:
         print(f"  {n:60s} aten {gat[n]:10.3e} texbias {gtb[n]:10.3e} ratio {gtb[n] / max(gat[n], 1e-12):7.2f}")
+    # one texbias family at a time (the others on ATen): which one moves the scalar (PReLU) gradients
+    print("scalar parameter gradients with ONE texbias family enabled (conv / norm / loss):")
+    fams = {}
+    for fam in ("conv", "norm", "loss"):
+        C.ENABLED, N.ENABLED, L.ENABLED = fam == "conv", fam == "norm", fam == "loss"
+        mf = copy.deepcopy(model)
+        mf.zero_grad(set_to_none=True)
+        loss_fn(mf(x), lab).backward()
+        fams[fam] = {n: relmax(p.grad, g64[n]) for n, p in mf.named_parameters()}
+        del mf
+    C.ENABLED, N.ENABLED, L.ENABLED = saved
+    for n, p in model.named_parameters():
+        if p.numel() == 1:
+            print(f"  {n:60s} aten {gat[n]:9.2e} all {gtb[n]:9.2e} conv {fams['conv'][n]:9.2e} "
+                  f"norm {fams['norm'][n]:9.2e} loss {fams['loss'][n]:9.2e}")
 
 
 if __name__ == "__main__":
