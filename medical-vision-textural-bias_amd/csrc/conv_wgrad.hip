@@ -289,6 +289,178 @@ __global__ __launch_bounds__(NT) void k_conv3d_wgrad_mz(WgArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Stride 1, 16-channel tiles: the block MARCHES along the input planes zi of its (n, YB-row block,
+// z segment).  With z = zi - tz + 1,
+//   dW[m][c][tz][ty][tx] += sum_{y,x} G[m][zi - tz + 1][y][x] * X[c][zi][y + ty - 1][x + tx - 1]
+// so one staged input plane (X slab: 16 c x (YB + 2) rows + x halo) meets the three G planes
+// zi + 1, zi, zi - 1 kept in a 4-slot ring: every z step stages ONE new X slab and ONE new G slab
+// (the im2col re-staging of the chunked kernel was 6x the input per output plane).  Each k-step of 4
+// positions reads 3 A fragments (the tz planes) and 9 B fragments (the (ty, tx) shifts) for 27 MFMAs
+// (16x16x4 f32: rows m, columns c) into 27 accumulators per wave; the waves split the positions and
+// meet in LDS at the end, one float atomic per dW entry per block.  The next plane's slabs are loaded
+// into registers while the current plane's MFMAs run (one barrier per z step).
+struct ZmArgs {
+  const float* G;
+  const float* X;
+  float* dW;
+  int N, M, Cc, D, H, W;       // G and X both [N][.][D][H][W] (stride 1, padding 1)
+  int YB, nyb, ZS, zlen;       // rows per block, row blocks, z segments, planes per segment
+  int MS, RX, PX, W4;          // LDS pitches (floats): G channel, X channel, X row; k-step row length
+  int mtiles, ctiles;
+};
+
+template <int YB, int WV>  // WV: most float4 per row (W <= 4 WV)
+__global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
+  constexpr int NXR = YB + 2;  // staged X rows
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int W = a.W, H = a.H, D = a.D, W4 = a.W4;
+  const int GS = 16 * a.MS, XS = 16 * a.RX;  // slab sizes
+  float* gsl = smem;                        // [4 slots][16 m][MS]: row yy at yy * W4, zero past W
+  float* xsl = smem + 4 * GS;               // [2 slots][16 c][RX]: row r at r * PX, x at col x + 2
+  // block -> (tile, n, row block, z segment)
+  const int tile = (int)blockIdx.y, mt = tile / a.ctiles, ct = tile - mt * a.ctiles;
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int m0 = 16 * mt, c0 = 16 * ct;
+  const int mv = min(16, a.M - m0), cv = min(16, a.Cc - c0);
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
+  for (int i = tid; i < 4 * GS + 2 * XS; i += 256) smem[i] = 0.f;  // halos, pads, absent rows stay 0
+  const int64_t plane = (int64_t)H * W;
+  const float* Gb = a.G + ((int64_t)n * a.M + m0) * D * plane;
+  const float* Xb = a.X + ((int64_t)n * a.Cc + c0) * D * plane;
+  // staging items, fixed per thread for the whole march: global offset within a plane (-1: none)
+  // and LDS offset within a slab -- X (c, r, q) with row y0 - 1 + r in range, G (m, yy, q)
+  const int W4v = W >> 2;
+  constexpr int NXL = (16 * NXR * WV + 255) / 256, NGL = (16 * YB * WV + 255) / 256;
+  int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
+#pragma unroll
+  for (int j = 0; j < NXL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4v, t = i / W4v, r = t % NXR, c = t / NXR;
+    const int y = y0 - 1 + r;
+    const bool ok = c < cv && y >= 0 && y < H;
+    xg[j] = ok ? (int)(((int64_t)c * D) * plane / 4 + (y * W + 4 * q) / 4) : -1;  // in float4 of the plane-0 base
+    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
+  }
+#pragma unroll
+  for (int j = 0; j < NGL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4v, t = i / W4v, yy = t % YB, m = t / YB;
+    const int y = y0 + yy;
+    const bool ok = m < mv && y < H;
+    gg[j] = ok ? (int)(((int64_t)m * D) * plane / 4 + (y * W + 4 * q) / 4) : -1;
+    gl[j] = m * a.MS + yy * W4 + 4 * q;
+  }
+  float4 rx[NXL], rg[NGL];
+  const int64_t plane4 = plane / 4;
+  auto load_x = [&](int zi) {
+    const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)zi * plane4;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      rx[j] = xg[j] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+    }
+  };
+  auto store_x = [&](int slot) {
+    float* d = xsl + slot * XS;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j)
+      if (xg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + xl[j]);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
+      }
+  };
+  auto load_g = [&](int pz) {  // G plane pz (zero outside [0, D))
+    const bool in = pz >= 0 && pz < D;
+    const float4* src = reinterpret_cast<const float4*>(Gb) + (int64_t)(in ? pz : 0) * plane4;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = src[gg[j] < 0 ? 0 : gg[j]];
+      rg[j] = (in && gg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_g = [&](int slot) {
+    float* d = gsl + slot * GS;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j)
+      if (gg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + gl[j]);
+        p[0] = make_float2(rg[j].x, rg[j].y);
+        p[1] = make_float2(rg[j].z, rg[j].w);
+      }
+  };
+  __syncthreads();  // the zero fill is done before any slab store
+  // prologue: G planes z0 - 1 and z0 into their ring slots, then X[z0] and G[z0 + 1] in registers
+  load_g(z0 - 1);
+  store_g((z0 + 3) & 3);
+  load_g(z0);
+  store_g(z0 & 3);
+  load_x(z0);
+  load_g(z0 + 1);
+
+  const int li = lane & 15, lk = lane >> 4;
+  const int aoff = li * a.MS + lk;                 // A: G[m = li][yy][x0 + lk]
+  const int boff = li * a.RX + lk + 1;             // B: X[c = li][yy + ty][x0 + lk + tx - 1] at col + 2
+  const int nks = YB * (W4 >> 2);                  // k-steps per plane (YB rows of W4 / 4)
+  const int kpr = W4 >> 2;
+  f32x4 acc[27];
+#pragma unroll
+  for (int j = 0; j < 27; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int zi = z0; zi < z1; ++zi) {
+    store_x(zi & 1);
+    store_g((zi + 1) & 3);
+    __syncthreads();  // slabs of this step visible; every wave is past the step that last read these slots
+    if (zi + 1 < z1) {  // next step's slabs fly during this step's MFMAs
+      load_x(zi + 1);
+      load_g(zi + 2);
+    }
+    const float* g0 = gsl + ((zi + 1) & 3) * GS + aoff;  // tz = 0: plane zi + 1
+    const float* g1 = gsl + (zi & 3) * GS + aoff;        // tz = 1: plane zi
+    const float* g2 = gsl + ((zi + 3) & 3) * GS + aoff;  // tz = 2: plane zi - 1
+    const float* xb = xsl + (zi & 1) * XS + boff;
+    for (int ks = wave; ks < nks; ks += 4) {
+      const int yy = ks / kpr, x0 = 4 * (ks - yy * kpr);
+      const int ga = yy * W4 + x0, xa = yy * a.PX + x0;
+      float av[3], bv[9];
+      av[0] = g0[ga];
+      av[1] = g1[ga];
+      av[2] = g2[ga];
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) bv[ty * 3 + tx] = xb[xa + ty * a.PX + tx];
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[tz * 9 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tz], bv[t], acc[tz * 9 + t], 0, 0, 0);
+    }
+  }
+  // the waves' sums meet in LDS (the ring is free after this barrier), one atomic per entry
+  __syncthreads();
+  float* red = smem;  // [27][4 waves][4 rr][64 lanes]
+#pragma unroll
+  for (int j = 0; j < 27; ++j)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[((j * 4 + wave) * 4 + rr) * 64 + lane] = acc[j][rr];
+  __syncthreads();
+  for (int e = tid; e < 27 * 4 * 64; e += 256) {  // e = (j, rr, lane)
+    const int ln = e & 63, rr = (e >> 6) & 3, j = e >> 8;
+    const int m = (ln >> 4) * 4 + rr, c = ln & 15;
+    if (m >= mv || c >= cv) continue;
+    const float v = red[((j * 4 + 0) * 4 + rr) * 64 + ln] + red[((j * 4 + 1) * 4 + rr) * 64 + ln] +
+                    red[((j * 4 + 2) * 4 + rr) * 64 + ln] + red[((j * 4 + 3) * 4 + rr) * 64 + ln];
+    atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], v);
+  }
+}
+
 int pad_mod32(int v, int rem) {
   while ((v & 31) != rem) ++v;
   return v;
@@ -426,12 +598,98 @@ int wg_setup(WgArgs& a, int& seg, int& TX, int& by, size_t& lds, int N, int M, i
   return TB_OK;
 }
 
+
+// z-marching stride-1 kernel (k_conv3d_wgrad_zm): 16-channel tiles, W % 4 == 0 (16-B rows), W <= 80,
+// at least 8 output and 8 input channels (the few-channel layers keep their own tilings)
+bool use_zm(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZM");
+    return !(e && e[0] == '0');
+  }();
+  return on && stride == 1 && M >= 8 && Cc >= 8 && Do == Di && Ho == Hi && Wo == Wi && Wo % 4 == 0 && Wo <= 80 &&
+         (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+
+int zm_setup(ZmArgs& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, int H, int W, int ncu) {
+  a.N = N; a.M = M; a.Cc = Cc; a.D = D; a.H = H; a.W = W;
+  a.W4 = W;  // W % 4 == 0
+  static const int yb_env = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZM_YB");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.PX = ((W + 3 + 1) / 2) * 2;  // cols 0..W + 2 (data at 2..W + 1), even (8-B stores)
+  a.YB = 0;
+  for (int yb : {4, 2}) {
+    if (yb_env && yb != yb_env) continue;
+    const int ms = pad_mod32(yb * a.W4, 2), rx = pad_mod32((yb + 2) * a.PX, 2);
+    const size_t bytes = (size_t)4 * (4 * 16 * ms + 2 * 16 * rx);
+    if (bytes <= 163840 && bytes >= (size_t)27 * 4 * 4 * 64 * 4) {
+      a.YB = yb; a.MS = ms; a.RX = rx;
+      lds = bytes;
+      break;
+    }
+    if (bytes <= 163840) {  // the end's reduction needs 110.6 KB
+      a.YB = yb; a.MS = ms; a.RX = rx;
+      lds = (size_t)27 * 4 * 4 * 64 * 4;
+      break;
+    }
+  }
+  if (!a.YB) return TB_ERR_UNSUPPORTED_SIZE;
+  a.nyb = (H + a.YB - 1) / a.YB;
+  a.mtiles = (M + 15) / 16;
+  a.ctiles = (Cc + 15) / 16;
+  // z segments: one block per CU at a time (the ring fills the LDS), so the launch takes
+  // ceil(blocks / CUs) rounds of zlen + 2 plane steps (two ring-fill planes per segment): the
+  // segment length minimising that
+  const int base = N * a.nyb * a.mtiles * a.ctiles;
+  int best = 1 << 30;
+  a.zlen = D;
+  for (int zl = D; zl >= 4 || zl == D; --zl) {
+    const int zs = (D + zl - 1) / zl;
+    const int rounds = (base * zs + ncu - 1) / ncu;
+    const int cost = rounds * (zl + 2);
+    if (cost < best) {
+      best = cost;
+      a.zlen = zl;
+    }
+    if (zl <= 1) break;
+  }
+  a.ZS = (D + a.zlen - 1) / a.zlen;
+  grid = dim3((unsigned)(N * a.nyb * a.ZS), (unsigned)(a.mtiles * a.ctiles));
+  return TB_OK;
+}
+
+int launch_zm(const ZmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
+  auto kern = a.W <= 40 ? (a.YB == 4 ? k_conv3d_wgrad_zm<4, 10> : k_conv3d_wgrad_zm<2, 10>)
+                        : (a.YB == 4 ? k_conv3d_wgrad_zm<4, 20> : k_conv3d_wgrad_zm<2, 20>);
+  const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  if (attr != hipSuccess) return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
 }  // namespace
 
 // dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2, padding 1 (file header).
 int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
                         int Hi, int Wi, int stride, int pad, void* stream) {
   if (!G || !X || !dW) return TB_ERR_INVALID_ARG;
+  hipStream_t st0 = reinterpret_cast<hipStream_t>(stream);
+  if (pad == 1 && N >= 1 && use_zm(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+      return n;
+    }();
+    ZmArgs z{};
+    size_t lds = 0;
+    dim3 grid;
+    if (zm_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, ncu) == TB_OK) {
+      z.G = G; z.X = X; z.dW = dW;
+      if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st0) != hipSuccess) return TB_ERR_HIP;
+      return launch_zm(z, lds, grid, st0);
+    }
+  }
   WgArgs a{};
   int seg = 0, TX = 0, by = 0;
   size_t lds = 0;

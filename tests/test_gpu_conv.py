@@ -46,6 +46,26 @@ def test_conv3d_wgrad(conv, cin, cout, stride, shape, fast, monkeypatch):
     torch.testing.assert_close(gwo, gwr, rtol=1e-4, atol=1e-3 * gwr.abs().max().item())
 
 
+@pytest.mark.parametrize("cin,cout,shape", [(16, 16, (2, 12, 10, 40)), (32, 32, (1, 9, 13, 20)), (24, 40, (1, 7, 6, 16)),
+                                             (16, 16, (1, 3, 5, 8)), (16, 8, (2, 30, 6, 80)), (64, 64, (2, 5, 7, 12))])
+def test_conv3d_wgrad_zmarch(conv, cin, cout, shape, monkeypatch):
+    """Stride-1 layers of >= 8 channels and rows of 4k <= 80 floats take the z-marching kernel
+    (k_conv3d_wgrad_zm: one staged input plane meets a ring of three G planes); partial channel
+    tiles, a row block past H, z segments of unequal length."""
+    monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)
+    torch.manual_seed(0)
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
+    g = torch.randn((shape[0], cout) + shape[1:], device="cuda")
+    w = torch.zeros((cout, cin, 3, 3, 3), device="cuda", requires_grad=True)
+    ref, = torch.autograd.grad(torch.nn.functional.conv3d(x, w, padding=1), w, g)
+    ours = conv.wgrad(g, x, w.shape, 1, 1)
+    x64, g64 = x.double(), g.double()
+    w64 = torch.zeros((cout, cin, 3, 3, 3), device="cuda", dtype=torch.float64, requires_grad=True)
+    r64, = torch.autograd.grad(torch.nn.functional.conv3d(x64, w64, padding=1), w64, g64)
+    scale = r64.abs().max().item()
+    assert (ours.double() - r64).abs().max().item() <= 4 * max((ref.double() - r64).abs().max().item(), 1e-6 * scale)
+
+
 @pytest.mark.parametrize("cin,cout,shape", [(32, 3, (2, 12, 10, 20)), (64, 16, (1, 12, 10, 16))])
 def test_convtranspose3d_wgrad(conv, cin, cout, shape, monkeypatch):
     monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)
