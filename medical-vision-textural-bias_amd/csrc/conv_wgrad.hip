@@ -409,8 +409,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
   const int li = lane & 15, lk = lane >> 4;
   const int aoff = li * a.MS + lk;                 // A: G[m = li][yy][x0 + lk]
   const int boff = li * a.RX + lk + 1;             // B: X[c = li][yy + ty][x0 + lk + tx - 1] at col + 2
-  const int nks = YB * (W4 >> 2);                  // k-steps per plane (YB rows of W4 / 4)
-  const int kpr = W4 >> 2;
+  const int kpr = W4 >> 2;                         // k-steps per row
   f32x4 acc[27];
 #pragma unroll
   for (int j = 0; j < 27; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -426,10 +425,13 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
     const float* g1 = gsl + (zi & 3) * GS + aoff;        // tz = 1: plane zi
     const float* g2 = gsl + ((zi + 3) & 3) * GS + aoff;  // tz = 2: plane zi - 1
     const float* xb = xsl + (zi & 1) * XS + boff;
-    for (int ks = wave; ks < nks; ks += 4) {
-      const int yy = ks / kpr, x0 = 4 * (ks - yy * kpr);
-      const int ga = yy * W4 + x0, xa = yy * a.PX + x0;
-      float av[3], bv[9];
+    // this wave's k-steps: row yy = wave % YB, x0 over part wave / YB of the row (4 / YB parts);
+    // the next k-step's 12 operands are read under the current one's 27 MFMAs (2x unrolled, clamped)
+    const int yy = wave % YB, np = 4 / YB, part = wave / YB;
+    const int kb = (kpr * part) / np, ke = (kpr * (part + 1)) / np;
+    auto ld = [&](int k, float (&av)[3], float (&bv)[9]) {
+      const int kk = k < ke ? k : ke - 1;
+      const int ga = yy * W4 + 4 * kk, xa = yy * a.PX + 4 * kk;
       av[0] = g0[ga];
       av[1] = g1[ga];
       av[2] = g2[ga];
@@ -437,10 +439,24 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
       for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
         for (int tx = 0; tx < 3; ++tx) bv[ty * 3 + tx] = xb[xa + ty * a.PX + tx];
+    };
+    auto mm = [&](const float (&av)[3], const float (&bv)[9]) {
 #pragma unroll
       for (int tz = 0; tz < 3; ++tz)
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[tz * 9 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tz], bv[t], acc[tz * 9 + t], 0, 0, 0);
+    };
+    if (kb < ke) {
+      float a0[3], b0[9], a1[3], b1[9];
+      ld(kb, a0, b0);
+      int k = kb;
+      for (; k + 1 < ke; k += 2) {
+        ld(k + 1, a1, b1);
+        mm(a0, b0);
+        ld(k + 2, a0, b0);
+        mm(a1, b1);
+      }
+      if (k < ke) mm(a0, b0);
     }
   }
   // the waves' sums meet in LDS (the ring is free after this barrier), one atomic per entry
@@ -458,6 +474,367 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
     const float v = red[((j * 4 + 0) * 4 + rr) * 64 + ln] + red[((j * 4 + 1) * 4 + rr) * 64 + ln] +
                     red[((j * 4 + 2) * 4 + rr) * 64 + ln] + red[((j * 4 + 3) * 4 + rr) * 64 + ln];
     atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], v);
+  }
+}
+
+
+// Stride 2, >= 8 input channels: the block marches along the OUTPUT planes z of its (n, output row y,
+// z segment) and keeps the input planes 2z - 1, 2z, 2z + 1 (three rows 2y - 1 .. 2y + 1 each) in a
+// 5-slot ring -- consecutive planes share one, so a step stages two new input slabs and one G row per
+// m -- for 32 output channels (two 16-row m-tiles) at once.  Waves: (m-tile = wave & 1, every other
+// k-step); 27 tap accumulators each, 1 A + 27 B reads per 27 MFMAs (16x16x4 f32, rows m, columns c);
+// partner waves of one m-tile meet in LDS at the end, one float atomic per dW entry per block.
+struct Zm2Args {
+  const float* G;
+  const float* X;
+  float* dW;
+  int N, M, Cc, Do, Ho, Wo, Di, Hi, Wi;
+  int ZS, zlen, YB, nyb;
+  int MS, RX, PX;
+  int mtiles, ctiles;  // m-tiles of 32 (pairs), c-tiles of 16
+};
+
+template <int YB, int WV>  // output rows per block, Wo <= 4 WV
+__global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
+  constexpr int NXR = 2 * YB + 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Wo = a.Wo, Ho = a.Ho, Do = a.Do, Hi = a.Hi, Wi = a.Wi, Di = a.Di;
+  const int GS = 32 * a.MS, XS = 16 * a.RX;
+  float* gsl = smem;             // [2 slots][32 m][MS]: row yy at yy * Wo
+  float* xsl = smem + 2 * GS;    // [5 slots][16 c][RX]: row r (input row 2 y0 - 1 + r) at r * PX, col x + 2
+  const int tile = (int)blockIdx.y, mt = tile / a.ctiles, ct = tile - mt * a.ctiles;
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int y0 = yb * YB;
+  const int m0 = 32 * mt, c0 = 16 * ct;
+  const int mv = min(32, a.M - m0), cv = min(16, a.Cc - c0);
+  const int z0 = zs * a.zlen, z1 = min(Do, z0 + a.zlen);
+  for (int i = tid; i < 2 * GS + 5 * XS; i += 256) smem[i] = 0.f;
+  const int64_t iplane = (int64_t)Hi * Wi, oplane = (int64_t)Ho * Wo;
+  const float* Gb = a.G + ((int64_t)n * a.M + m0) * Do * oplane;
+  const float* Xb = a.X + ((int64_t)n * a.Cc + c0) * Di * iplane;
+  const int Wi4 = Wi >> 2, Wo4 = Wo >> 2;
+  constexpr int NXL = (16 * NXR * 2 * WV + 255) / 256, NGL = (32 * YB * WV + 255) / 256;
+  int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
+#pragma unroll
+  for (int j = 0; j < NXL; ++j) {  // (c, r, q): input row 2 y0 - 1 + r
+    const int i = tid + 256 * j;
+    const int q = i % Wi4, t = i / Wi4, r = t % NXR, c = t / NXR;
+    const int yi = 2 * y0 - 1 + r;
+    const bool ok = c < cv && yi >= 0 && yi < Hi;
+    xg[j] = ok ? (int)(((int64_t)c * Di) * iplane / 4 + (yi * Wi + 4 * q) / 4) : -1;
+    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
+  }
+#pragma unroll
+  for (int j = 0; j < NGL; ++j) {  // (m, yy, q): output row y0 + yy
+    const int i = tid + 256 * j;
+    const int q = i % Wo4, t = i / Wo4, yy = t % YB, m = t / YB;
+    const bool ok = m < mv && y0 + yy < Ho;
+    gg[j] = ok ? (int)(((int64_t)m * Do) * oplane / 4 + ((y0 + yy) * Wo + 4 * q) / 4) : -1;
+    gl[j] = m * a.MS + yy * Wo + 4 * q;
+  }
+  const int64_t iplane4 = iplane / 4, oplane4 = oplane / 4;
+  float4 rx0[NXL], rx1[NXL], rg[NGL];
+  auto load_x = [&](int zi, float4 (&rx)[NXL]) {  // input plane zi (zero outside [0, Di))
+    const bool in = zi >= 0 && zi < Di;
+    const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(in ? zi : 0) * iplane4;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      rx[j] = (in && xg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_x = [&](int zi, const float4 (&rx)[NXL]) {
+    float* d = xsl + ((zi + 5) % 5) * XS;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j)
+      if (xg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + xl[j]);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
+      }
+  };
+  auto load_g = [&](int z) {
+#pragma unroll
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
+      rg[j] = gg[j] >= 0 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_g = [&](int z) {
+    float* d = gsl + (z & 1) * GS;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j)
+      if (gg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + gl[j]);
+        p[0] = make_float2(rg[j].x, rg[j].y);
+        p[1] = make_float2(rg[j].z, rg[j].w);
+      }
+  };
+  __syncthreads();  // zero fill before the first slab store
+  // prologue: plane 2 z0 - 1 into its slot; planes 2 z0, 2 z0 + 1 and G[z0] in registers
+  load_x(2 * z0 - 1, rx0);
+  store_x(2 * z0 - 1, rx0);
+  load_x(2 * z0, rx0);
+  load_x(2 * z0 + 1, rx1);
+  load_g(z0);
+
+  const int li = lane & 15, lk = lane >> 4;
+  const int mtl = wave & 1, par = wave >> 1;       // this wave's 16-row m-tile and k-step parity
+  const int aoff = (16 * mtl + li) * a.MS + lk;    // A: G[m][x0 + lk]
+  const int boff = li * a.RX + 2 * lk + 1;         // B: X[c][row][2 (x0 + lk) + tx - 1] at col + 2
+  f32x4 acc[27];
+#pragma unroll
+  for (int j = 0; j < 27; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int z = z0; z < z1; ++z) {
+    store_x(2 * z, rx0);
+    store_x(2 * z + 1, rx1);
+    store_g(z);
+    __syncthreads();
+    if (z + 1 < z1) {
+      load_x(2 * z + 2, rx0);
+      load_x(2 * z + 3, rx1);
+      load_g(z + 1);
+    }
+    const float* ga = gsl + (z & 1) * GS + aoff;
+    const float* xp[3] = {xsl + ((2 * z - 1 + 5) % 5) * XS + boff, xsl + ((2 * z) % 5) * XS + boff,
+                          xsl + ((2 * z + 1) % 5) * XS + boff};
+    // k-steps (yy, x0) of this wave's parity: the next one's 28 operands read under the current
+    // one's 27 MFMAs (2x unrolled, clamped)
+    const int nk = YB * Wo4;
+    auto ld = [&](int k, float& av, float (&bv)[27]) {
+      const int kk = k < nk ? k : nk - 1;
+      const int yy = YB == 1 ? 0 : (kk >= Wo4 ? 1 : 0), x0 = 4 * (kk - yy * Wo4);
+      av = ga[yy * Wo + x0];
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz)
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) bv[tz * 9 + ty * 3 + tx] = xp[tz][(2 * yy + ty) * a.PX + 2 * x0 + tx];
+    };
+    auto mm = [&](float av, const float (&bv)[27]) {
+#pragma unroll
+      for (int t = 0; t < 27; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[t], acc[t], 0, 0, 0);
+    };
+    if (par < nk) {
+      float a0, a1, b0[27], b1[27];
+      ld(par, a0, b0);
+      int k = par;
+      for (; k + 2 < nk; k += 4) {
+        ld(k + 2, a1, b1);
+        mm(a0, b0);
+        ld(k + 4, a0, b0);
+        mm(a1, b1);
+      }
+      if (k < nk) mm(a0, b0);
+    }
+  }
+  // partner waves (same m-tile, other parity) meet in LDS; waves 0 / 1 add and store
+  __syncthreads();
+  float* red = smem;  // [2 m-tiles][27][4 rr][64 lanes]
+  if (par == 1) {
+#pragma unroll
+    for (int j = 0; j < 27; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[((mtl * 27 + j) * 4 + rr) * 64 + lane] = acc[j][rr];
+  }
+  __syncthreads();
+  if (par == 0) {
+    const int c = li;
+#pragma unroll
+    for (int j = 0; j < 27; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = 16 * mtl + lk * 4 + rr;
+        if (m < mv && c < cv)
+          atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j],
+                    acc[j][rr] + red[((mtl * 27 + j) * 4 + rr) * 64 + lane]);
+      }
+  }
+}
+
+
+// Stride 2, few (<= 5) input channels (the full-resolution first conv 4 -> 16, its residual, and the
+// top transposed conv 32 -> 3 whose X is the 3-channel output gradient): output-plane march as
+// k_conv3d_wgrad_zm2, YB output rows per block, and the MFMA columns are (c, tx) pairs (3 C <= 15 of 16)
+// with the 9 (tz, ty) taps as accumulators per m-tile -- 1 A + 9 B reads per 9 MFMAs.  These layers
+// are HBM-bound (4 B of input per 9 MACs): every input row is staged once per row block.
+struct Zf2Args {
+  const float* G;
+  const float* X;
+  float* dW;
+  int N, M, Cc, Do, Ho, Wo, Di, Hi, Wi;
+  int YB, nyb, ZS, zlen;
+  int MS, RX, PX;
+  int mtiles;  // blocks of MT m-tiles
+};
+
+template <int YB, int MT, int WV>  // rows per block, 16-row m-tiles per block, Wo <= 4 WV
+__global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
+  constexpr int NXR = 2 * YB + 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Wo = a.Wo, Ho = a.Ho, Do = a.Do, Hi = a.Hi, Wi = a.Wi, Di = a.Di, Cc = a.Cc;
+  const int GS = 16 * MT * a.MS, XS = Cc * a.RX;
+  float* gsl = smem;             // [2 slots][16 MT m][MS]: row yy at yy * Wo
+  float* xsl = smem + 2 * GS;    // [5 slots][Cc][RX]: row r (input row 2 y0 - 1 + r) at r * PX, col x + 2
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int mt = (int)blockIdx.y;
+  const int m0 = 16 * MT * mt, mv = min(16 * MT, a.M - m0);
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(Do, z0 + a.zlen);
+  for (int i = tid; i < 2 * GS + 5 * XS; i += 256) smem[i] = 0.f;
+  const int64_t iplane = (int64_t)Hi * Wi, oplane = (int64_t)Ho * Wo;
+  const float* Gb = a.G + ((int64_t)n * a.M + m0) * Do * oplane;
+  const float* Xb = a.X + (int64_t)n * Cc * Di * iplane;
+  const int Wi4 = Wi >> 2, Wo4 = Wo >> 2;
+  constexpr int NXL = (5 * NXR * 2 * WV + 255) / 256, NGL = (16 * MT * YB * WV + 255) / 256;
+  int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
+#pragma unroll
+  for (int j = 0; j < NXL; ++j) {  // (c, r, q)
+    const int i = tid + 256 * j;
+    const int q = i % Wi4, t = i / Wi4, r = t % NXR, c = t / NXR;
+    const int yi = 2 * y0 - 1 + r;
+    const bool ok = c < Cc && yi >= 0 && yi < Hi;
+    xg[j] = ok ? (int)(((int64_t)c * Di) * iplane / 4 + (yi * Wi + 4 * q) / 4) : -1;
+    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
+  }
+#pragma unroll
+  for (int j = 0; j < NGL; ++j) {  // (m, yy, q)
+    const int i = tid + 256 * j;
+    const int q = i % Wo4, t = i / Wo4, yy = t % YB, m = t / YB;
+    const int y = y0 + yy;
+    const bool ok = m < mv && y < Ho;
+    gg[j] = ok ? (int)(((int64_t)m * Do) * oplane / 4 + (y * Wo + 4 * q) / 4) : -1;
+    gl[j] = m * a.MS + yy * Wo + 4 * q;
+  }
+  const int64_t iplane4 = iplane / 4, oplane4 = oplane / 4;
+  float4 rx0[NXL], rx1[NXL], rg[NGL];
+  auto load_x = [&](int zi, float4 (&rx)[NXL]) {
+    const bool in = zi >= 0 && zi < Di;
+    const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(in ? zi : 0) * iplane4;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      rx[j] = (in && xg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_x = [&](int zi, const float4 (&rx)[NXL]) {
+    float* d = xsl + ((zi + 5) % 5) * XS;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j)
+      if (xg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + xl[j]);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
+      }
+  };
+  auto load_g = [&](int z) {
+#pragma unroll
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
+      rg[j] = gg[j] >= 0 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_g = [&](int z) {
+    float* d = gsl + (z & 1) * GS;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j)
+      if (gg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + gl[j]);
+        p[0] = make_float2(rg[j].x, rg[j].y);
+        p[1] = make_float2(rg[j].z, rg[j].w);
+      }
+  };
+  __syncthreads();
+  load_x(2 * z0 - 1, rx0);
+  store_x(2 * z0 - 1, rx0);
+  load_x(2 * z0, rx0);
+  load_x(2 * z0 + 1, rx1);
+  load_g(z0);
+
+  const int li = lane & 15, lk = lane >> 4;
+  const int bc = li < 3 * Cc ? li / 3 : 0, btx = li < 3 * Cc ? li - 3 * (li / 3) : 0;
+  const int boff = bc * a.RX + btx + 2 * lk + 1;  // B: X[c][row][2 (x0 + lk) + tx - 1] at col + 2
+  f32x4 acc[MT][9];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int z = z0; z < z1; ++z) {
+    store_x(2 * z, rx0);
+    store_x(2 * z + 1, rx1);
+    store_g(z);
+    __syncthreads();
+    if (z + 1 < z1) {
+      load_x(2 * z + 2, rx0);
+      load_x(2 * z + 3, rx1);
+      load_g(z + 1);
+    }
+    const float* ga = gsl + (z & 1) * GS + li * a.MS + lk;
+    const float* xp[3] = {xsl + ((2 * z - 1 + 5) % 5) * XS + boff, xsl + ((2 * z) % 5) * XS + boff,
+                          xsl + ((2 * z + 1) % 5) * XS + boff};
+    // this wave's k-steps: rows yy = wave, wave + 4, ... (YB = 4: one row; YB < 4: x parts of a row);
+    // the next k-step's operands are read under the current one's MFMAs (2x unrolled, clamped)
+    const int np = YB >= 4 ? 1 : 4 / YB, yy0 = YB >= 4 ? wave : wave % YB, part = YB >= 4 ? 0 : wave / YB;
+    const int kb = (Wo4 * part) / np, ke = (Wo4 * (part + 1)) / np;
+    auto ld = [&](int yy, int k, float (&av)[MT], float (&bv)[9]) {
+      const int x0 = 4 * (k < ke ? k : ke - 1);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) av[t] = ga[t * 16 * a.MS + yy * Wo + x0];
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz)
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) bv[tz * 3 + ty] = xp[tz][(2 * yy + ty) * a.PX + 2 * x0];
+    };
+    auto mm = [&](const float (&av)[MT], const float (&bv)[9]) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[j], acc[t][j], 0, 0, 0);
+    };
+    for (int yy = yy0; yy < YB; yy += 4) {
+      if (kb >= ke) break;
+      float a0[MT], a1[MT], b0[9], b1[9];
+      ld(yy, kb, a0, b0);
+      int k = kb;
+      for (; k + 1 < ke; k += 2) {
+        ld(yy, k + 1, a1, b1);
+        mm(a0, b0);
+        ld(yy, k + 2, a0, b0);
+        mm(a1, b1);
+      }
+      if (k < ke) mm(a0, b0);
+    }
+  }
+  // the four waves' sums meet in LDS, one atomic per entry
+  __syncthreads();
+  float* red = smem;  // [MT][9][4 waves][4 rr][64]
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[(((t * 9 + j) * 4 + wave) * 4 + rr) * 64 + lane] = acc[t][j][rr];
+  __syncthreads();
+  for (int e = tid; e < MT * 9 * 4 * 64; e += 256) {  // e = ((t, j), rr, lane)
+    const int ln = e & 63, rr = (e >> 6) & 3, tj = e >> 8, t = tj / 9, j = tj - 9 * t;
+    const int m = 16 * t + (ln >> 4) * 4 + rr, col = ln & 15;
+    if (m >= mv || col >= 3 * Cc) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += red[((tj * 4 + w) * 4 + rr) * 64 + ln];
+    const int c = col / 3, tx = col - 3 * c;
+    atomicAdd(&a.dW[((int64_t)(m0 + m) * Cc + c) * 27 + j * 3 + tx], v);  // j = (tz, ty)
   }
 }
 
@@ -668,6 +1045,132 @@ int launch_zm(const ZmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
+
+// stride-2 z-marching kernel (k_conv3d_wgrad_zm2): >= 8 input channels, Wo % 4 == 0, Wo <= 40,
+// input rows of exactly 2 Wo (padding 1)
+bool use_zm2(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZM2");
+    return !(e && e[0] == '0');
+  }();
+  return on && stride == 2 && M >= 8 && Cc >= 8 && Wo % 4 == 0 && Wo <= 40 && Wi == 2 * Wo && Hi == 2 * Ho &&
+         Di == 2 * Do && (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+
+int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi,
+              int Wi, int ncu) {
+  a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
+  a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
+  static const int yb_env = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZM2_YB");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.YB = 0;
+  for (int yb : {2, 1}) {  // two output rows per block where the ring fits: twice the MFMAs per staged plane
+    if ((yb_env && yb != yb_env) || yb > Ho) continue;
+    for (int rem : {2, 4}) {  // X channel pitch mod 32: 2 (2-way B conflicts), 4 (tighter pad)
+      const int rx = pad_mod32((2 * yb + 1) * a.PX, rem), ms = pad_mod32(yb * Wo, 2);
+      const size_t ring = (size_t)4 * (2 * 32 * ms + 5 * 16 * rx), red = (size_t)4 * 2 * 27 * 4 * 64;
+      const size_t need = ring > red ? ring : red;
+      if (need <= 163840) {
+        a.YB = yb; a.RX = rx; a.MS = ms;
+        lds = need;
+        break;
+      }
+    }
+    if (a.YB) break;
+  }
+  if (!a.YB) return TB_ERR_UNSUPPORTED_SIZE;
+  a.nyb = (Ho + a.YB - 1) / a.YB;
+  a.mtiles = (M + 31) / 32;
+  a.ctiles = (Cc + 15) / 16;
+  const int base = N * a.nyb * a.mtiles * a.ctiles;
+  const int per_cu = (int)(163840 / lds) < 2 ? 1 : 2;
+  int best = 1 << 30;
+  a.zlen = Do;
+  for (int zl = Do; zl >= 1; --zl) {
+    const int zs = (Do + zl - 1) / zl;
+    const int rounds = (base * zs + per_cu * ncu - 1) / (per_cu * ncu);
+    const int cost = rounds * (zl + 1);
+    if (cost < best) {
+      best = cost;
+      a.zlen = zl;
+    }
+  }
+  a.ZS = (Do + a.zlen - 1) / a.zlen;
+  grid = dim3((unsigned)(N * a.nyb * a.ZS), (unsigned)(a.mtiles * a.ctiles));
+  return TB_OK;
+}
+
+int launch_zm2(const Zm2Args& a, size_t lds, dim3 grid, hipStream_t st) {
+  auto kern = a.YB == 2 ? (a.Wo <= 20 ? k_conv3d_wgrad_zm2<2, 5> : k_conv3d_wgrad_zm2<2, 10>)
+                        : (a.Wo <= 20 ? k_conv3d_wgrad_zm2<1, 5> : k_conv3d_wgrad_zm2<1, 10>);
+  const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  if (attr != hipSuccess) return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+// few-channel stride-2 kernel (k_conv3d_wgrad_zf2): Cc <= 5, Wo % 4 == 0, Wo <= 80, 2x input rows
+bool use_zf2(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZF2");
+    return !(e && e[0] == '0');
+  }();
+  return on && stride == 2 && Cc <= 5 && Wo % 4 == 0 && Wo <= 80 && Wi == 2 * Wo && Hi == 2 * Ho && Di == 2 * Do &&
+         (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+
+int zf2_setup(Zf2Args& a, int& MT, size_t& lds, dim3& grid, int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
+              int Hi, int Wi, int ncu) {
+  a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
+  MT = M > 16 ? 2 : 1;
+  a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
+  a.YB = 0;
+  for (int yb : {4, 2, 1}) {
+    const int rx = pad_mod32((2 * yb + 1) * a.PX, 8), ms = pad_mod32(yb * Wo, 2);
+    const size_t ring = (size_t)4 * (2 * 16 * MT * ms + 5 * Cc * rx), red = (size_t)4 * MT * 9 * 4 * 4 * 64;
+    const size_t need = ring > red ? ring : red;
+    if (need <= 163840) {
+      a.YB = yb; a.RX = rx; a.MS = ms;
+      lds = need;
+      break;
+    }
+  }
+  if (!a.YB) return TB_ERR_UNSUPPORTED_SIZE;
+  a.nyb = (Ho + a.YB - 1) / a.YB;
+  a.mtiles = (M + 16 * MT - 1) / (16 * MT);
+  const int base = N * a.nyb * a.mtiles;
+  int best = 1 << 30;
+  a.zlen = Do;
+  for (int zl = Do; zl >= 1; --zl) {
+    const int zs = (Do + zl - 1) / zl;
+    const int rounds = (base * zs + ncu - 1) / ncu;
+    const int cost = rounds * (zl + 1);
+    if (cost < best) {
+      best = cost;
+      a.zlen = zl;
+    }
+  }
+  a.ZS = (Do + a.zlen - 1) / a.zlen;
+  grid = dim3((unsigned)(N * a.nyb * a.ZS), (unsigned)a.mtiles);
+  return TB_OK;
+}
+
+template <int YB, int MT>
+int launch_zf2_t(const Zf2Args& a, size_t lds, dim3 grid, hipStream_t st) {
+  auto kern = a.Wo <= 40 ? k_conv3d_wgrad_zf2<YB, MT, 10> : k_conv3d_wgrad_zf2<YB, MT, 20>;
+  const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  if (attr != hipSuccess) return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+int launch_zf2(const Zf2Args& a, int MT, size_t lds, dim3 grid, hipStream_t st) {
+  if (MT == 1) return a.YB == 4 ? launch_zf2_t<4, 1>(a, lds, grid, st) : a.YB == 2 ? launch_zf2_t<2, 1>(a, lds, grid, st) : launch_zf2_t<1, 1>(a, lds, grid, st);
+  return a.YB == 4 ? launch_zf2_t<4, 2>(a, lds, grid, st) : a.YB == 2 ? launch_zf2_t<2, 2>(a, lds, grid, st) : launch_zf2_t<1, 2>(a, lds, grid, st);
+}
 }  // namespace
 
 // dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2, padding 1 (file header).
@@ -688,6 +1191,37 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
       z.G = G; z.X = X; z.dW = dW;
       if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st0) != hipSuccess) return TB_ERR_HIP;
       return launch_zm(z, lds, grid, st0);
+    }
+  }
+  if (pad == 1 && N >= 1 && use_zm2(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {
+    static const int ncu2 = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+      return n;
+    }();
+    Zm2Args z{};
+    size_t lds = 0;
+    dim3 grid;
+    if (zm2_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, ncu2) == TB_OK) {
+      z.G = G; z.X = X; z.dW = dW;
+      if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st0) != hipSuccess) return TB_ERR_HIP;
+      return launch_zm2(z, lds, grid, st0);
+    }
+  }
+  if (pad == 1 && N >= 1 && use_zf2(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {
+    static const int ncu3 = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+      return n;
+    }();
+    Zf2Args z{};
+    int MT = 1;
+    size_t lds = 0;
+    dim3 grid;
+    if (zf2_setup(z, MT, lds, grid, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, ncu3) == TB_OK) {
+      z.G = G; z.X = X; z.dW = dW;
+      if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st0) != hipSuccess) return TB_ERR_HIP;
+      return launch_zf2(z, MT, lds, grid, st0);
     }
   }
   WgArgs a{};

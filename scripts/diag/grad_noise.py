@@ -90,7 +90,18 @@ def main():
         loss_fn(mf(x), lab).backward()
         fams[fam] = {n: relmax(p.grad, g64[n]) for n, p in mf.named_parameters()}
         del mf
+    # ATen again with the batch order reversed: the same mathematics, other reduction orders -- the
+    # spread of ATen's own float32 error on these cancellation-dominated scalars
+    C.ENABLED = N.ENABLED = L.ENABLED = False
+    mf = copy.deepcopy(model)
+    mf.zero_grad(set_to_none=True)
+    loss_fn(mf(x.flip(0)), lab.flip(0)).backward()
+    fams["aten_flip"] = {n: relmax(p.grad, g64[n]) for n, p in mf.named_parameters()}
+    del mf
     C.ENABLED, N.ENABLED, L.ENABLED = saved
+    for n, p in model.named_parameters():
+        if p.numel() == 1:
+            print(f"  {n:60s} aten {gat[n]:9.2e} aten(flipped batch) {fams['aten_flip'][n]:9.2e} texbias {gtb[n]:9.2e}")
     for n, p in model.named_parameters():
         if p.numel() == 1:
             print(f"  {n:60s} aten {gat[n]:9.2e} all {gtb[n]:9.2e} conv {fams['conv'][n]:9.2e} "

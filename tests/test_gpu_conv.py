@@ -66,6 +66,29 @@ def test_conv3d_wgrad_zmarch(conv, cin, cout, shape, monkeypatch):
     assert (ours.double() - r64).abs().max().item() <= 4 * max((ref.double() - r64).abs().max().item(), 1e-6 * scale)
 
 
+@pytest.mark.parametrize("cin,cout,shape", [(16, 32, (2, 12, 10, 40)), (8, 24, (1, 8, 6, 16)), (20, 40, (1, 10, 14, 80)),
+                                             (16, 64, (2, 6, 4, 8)),
+                                             # few input channels: k_conv3d_wgrad_zf2 ((c, tx) columns, YB rows)
+                                             (4, 16, (2, 12, 10, 40)), (3, 8, (1, 8, 6, 16)), (4, 16, (1, 6, 22, 160)),
+                                             (5, 40, (2, 6, 10, 24)), (1, 20, (1, 4, 6, 8))])
+def test_conv3d_wgrad_zmarch_stride2(conv, cin, cout, shape):
+    """Stride-2 layers of >= 8 input channels and output rows of 4k <= 40 take the output-plane
+    marching kernel (k_conv3d_wgrad_zm2: a 5-slot ring of input planes, two m-tiles per block), those of
+    <= 5 input channels and output rows of 4k <= 80 its few-channel form (k_conv3d_wgrad_zf2); partial
+    m / c tiles, row blocks past H."""
+    torch.manual_seed(0)
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
+    osp = tuple(n // 2 for n in shape[1:])
+    g = torch.randn((shape[0], cout) + osp, device="cuda")
+    w = torch.zeros((cout, cin, 3, 3, 3), device="cuda", requires_grad=True)
+    ref, = torch.autograd.grad(torch.nn.functional.conv3d(x, w, stride=2, padding=1), w, g)
+    ours = conv.wgrad(g, x, w.shape, 2, 1)
+    w64 = torch.zeros((cout, cin, 3, 3, 3), device="cuda", dtype=torch.float64, requires_grad=True)
+    r64, = torch.autograd.grad(torch.nn.functional.conv3d(x.double(), w64, stride=2, padding=1), w64, g.double())
+    scale = r64.abs().max().item()
+    assert (ours.double() - r64).abs().max().item() <= 4 * max((ref.double() - r64).abs().max().item(), 1e-6 * scale)
+
+
 @pytest.mark.parametrize("cin,cout,shape", [(32, 3, (2, 12, 10, 20)), (64, 16, (1, 12, 10, 16))])
 def test_convtranspose3d_wgrad(conv, cin, cout, shape, monkeypatch):
     monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)

@@ -205,10 +205,14 @@ def test_train_step_full_volume_matches_aten(gpu, heartbeat):
     gradient is a reduction over ~3e8 voxel terms that largely cancel (the first layer's conv bias,
     ahead of an InstanceNorm, is analytically zero), so an f32 result carries reduction-order noise of
     its own; the bar is therefore against the float64 gradient: per parameter, the texbias error
-    (normwise, max|g - g64| / max|g64|) is within 10x max(ATen's own float32 error, 1e-4; 2e-3 for the
-    scalar PReLU weights, see below) -- the
-    same order as ATen's reduction noise (measured: median 2.5e-3 vs ATen 2.1e-3, worst ratio 4.9 on
-    a 2.4e-5-scale weight gradient) -- and the loss within 1e-5 of the float64 loss."""
+    (normwise, max|g - g64| / max|g64|) is within 10x max(ATen's own float32 error, 1e-4) -- the
+    same order as ATen's reduction noise -- and the loss within 1e-5 of the float64 loss.
+    A scalar PReLU weight's gradient is ONE sum over the layer's negative voxels, sum z g, whose terms
+    cancel to 1e-3..1e-8 of sum |z g|: its relative error is that cancellation ratio times the float32
+    noise of the upstream gradient g (ATen's own, measured round 4: 3.9e-7 .. 0.36).  Its error is
+    therefore measured against its conditioning, |g - g64| / sum_{z<0} |z g| (the float64 terms, taken
+    with hooks in the float64 pass) -- the normwise measure of the vector of terms it sums -- under the
+    same bar, 10x max(ATen's, 1e-4)."""
     import copy
 
     from texbias import conv as C
@@ -232,20 +236,32 @@ def test_train_step_full_volume_matches_aten(gpu, heartbeat):
         del aten
         ref = copy.deepcopy(model).double()
         ref.zero_grad(set_to_none=True)
+        # conditioning of each scalar PReLU gradient: sum over z < 0 of |z g| (float64 terms)
+        cond, zin, hooks = {}, {}, []
+        for n, m in ref.named_modules():
+            if isinstance(m, torch.nn.PReLU) and m.weight.numel() == 1:
+                hooks.append(m.register_forward_hook(lambda m, i, o, n=n: zin.__setitem__(n, i[0].detach())))
+                hooks.append(m.register_full_backward_hook(
+                    lambda m, gi, go, n=n: cond.__setitem__(
+                        n + ".weight", (zin.pop(n).clamp(max=0) * go[0]).abs().sum().item())))
         l_64 = loss_fn(ref(x.double()), lab.double())
         l_64.backward()
+        for h in hooks:
+            h.remove()
     finally:
         C.ENABLED, N.ENABLED, L.ENABLED = saved
     g64 = {n: p.grad for n, p in ref.named_parameters()}
     e_tb, e_at = {}, {}
     for n, p in model.named_parameters():
         assert p.grad is not None and g32[n] is not None and g64[n] is not None, n
-        e_tb[n], e_at[n] = relmax(p.grad, g64[n]), relmax(g32[n], g64[n])
-    # Scalar parameters (each ADN's single PReLU weight) get a gradient that is ONE sum over every
-    # voxel of the layer, cancelling to 1e-6..1e-8 of its terms' magnitude: float32 noise of its
-    # upstream gradient is amplified to ~1e-3..1 relative (ATen's own float32 errors on these, measured
-    # round 3: 6.5e-5, 7.6e-4, 6.5e-3, 0.63; texbias: 1.0e-3, 3.8e-3, 2.2e-2, 2.4 -- unchanged when the
-    # kernel's own sum runs in float64, so it is upstream noise).  Their floor is 2e-3, tensors keep 1e-4.
+        if p.numel() == 1:
+            assert n in cond and cond[n] > 0, n
+            e_tb[n] = (p.grad.double() - g64[n]).abs().item() / cond[n]
+            e_at[n] = (g32[n].double() - g64[n]).abs().item() / cond[n]
+            print(f"  scalar {n}: |g64| {g64[n].abs().item():.3e} sum|zg| {cond[n]:.3e} "
+                  f"rel err texbias {relmax(p.grad, g64[n]):.3e} aten {relmax(g32[n], g64[n]):.3e}")
+        else:
+            e_tb[n], e_at[n] = relmax(p.grad, g64[n]), relmax(g32[n], g64[n])
     floor = {n: 1e-4 for n, p in model.named_parameters()}
     ratio = {n: e_tb[n] / max(e_at[n], floor[n]) for n in e_tb}
     worst = max(ratio, key=ratio.get)
