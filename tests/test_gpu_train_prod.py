@@ -211,8 +211,10 @@ def test_train_step_full_volume_matches_aten(gpu, heartbeat):
     cancel to 1e-3..1e-8 of sum |z g|: its relative error is that cancellation ratio times the float32
     noise of the upstream gradient g (ATen's own, measured round 4: 3.9e-7 .. 0.36).  Its error is
     therefore measured against its conditioning, |g - g64| / sum_{z<0} |z g| (the float64 terms, taken
-    with hooks in the float64 pass) -- the normwise measure of the vector of terms it sums -- under the
-    same bar, 10x max(ATen's, 1e-4)."""
+    with hooks in the float64 pass) -- the normwise measure of the vector of terms it sums -- within
+    10x max(ATen's, 1e-6) (measured round 4: texbias 2e-9 .. 4.2e-6, ATen 6e-9 .. 1.0e-6).  Tensor
+    gradients are chaotic at the same level: the worst tensor ratio (6.2 on an 8e-6-scale
+    ConvTranspose weight) swaps sides under a different seed (scripts/diag/grad_noise.py: 0.14)."""
     import copy
 
     from texbias import conv as C
@@ -262,7 +264,7 @@ def test_train_step_full_volume_matches_aten(gpu, heartbeat):
                   f"rel err texbias {relmax(p.grad, g64[n]):.3e} aten {relmax(g32[n], g64[n]):.3e}")
         else:
             e_tb[n], e_at[n] = relmax(p.grad, g64[n]), relmax(g32[n], g64[n])
-    floor = {n: 1e-4 for n, p in model.named_parameters()}
+    floor = {n: 1e-6 if p.numel() == 1 else 1e-4 for n, p in model.named_parameters()}
     ratio = {n: e_tb[n] / max(e_at[n], floor[n]) for n in e_tb}
     worst = max(ratio, key=ratio.get)
     print(f"loss texbias {l_tb.item():.8f} aten {l_at.item():.8f} f64 {l_64.item():.8f}; worst {worst}: "
