@@ -106,21 +106,24 @@ def parse():
     return a
 
 
-TRAFFIC_DIR = os.path.join(ROOT, "profiles", "r3")  # traffic_<config>.json (scripts/make_traffic.py)
+# traffic_<config or chain>.json (scripts/make_traffic.py), newest round first
+TRAFFIC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r4", "r3")]
 
 
-def pmc_traffic(kernel: str, launch_bytes: int, config: str = "c3"):
-    """HBM bytes per launch of a filter kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
-    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), or None when not measured for launches of
-    this size (the record carries the kernel name and the algorithmic bytes of the launches it measured)."""
-    try:
-        with open(os.path.join(TRAFFIC_DIR, f"traffic_{config}.json")) as f:
-            rec = json.load(f)["kernels"].get(kernel)
-        if not rec or abs(int(rec.get("algorithmic_bytes_per_launch", -1)) - int(launch_bytes)) > 0.001 * launch_bytes:
-            return None
-        return int(rec["traffic_bytes"])
-    except (OSError, ValueError, KeyError):
-        return None
+def pmc_traffic(kernel: str, launch_bytes: int, key: str = "c3"):
+    """(HBM bytes per launch of a filter kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), the file) or (None, None) when not measured for
+    launches of this size (a record carries the kernel name and the algorithmic bytes it measured)."""
+    for d in TRAFFIC_DIRS:
+        path = os.path.join(d, f"traffic_{key}.json")
+        try:
+            with open(path) as f:
+                rec = json.load(f)["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if rec and abs(int(rec.get("algorithmic_bytes_per_launch", -1)) - int(launch_bytes)) <= 0.001 * launch_bytes:
+            return int(rec["traffic_bytes"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def maybe_launch_ranks(args) -> None:
@@ -323,6 +326,8 @@ def main():
                         + (" [FILTER ONLY diagnostic]" if args.filter_only else ""))
         else:
             workload = "C2 Gibbs truncation: RandFourierDiskMaskd(r=12.5) low-pass alone, batched 4x128^3 volumes"
+        traffic, traffic_file = pmc_traffic(passes[dom]["kernel"], dom_bytes,
+                                            args.chain if args.config == "c3" and args.chain != "ref" else args.config)
         line = {
             "metric": METRIC,
             "value": round(vols / elapsed, 4),
@@ -346,8 +351,8 @@ def main():
             },
             "roofline": {"kernel": passes[dom]["kernel"], "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(passes[dom]["kernel"], dom_bytes, args.config),
-                         "traffic_unit": f"bytes per launch (rocprofv3 PMC, profiles/r3/traffic_{args.config}.json)",
+                         "traffic": traffic,
+                         "traffic_unit": f"bytes per launch (rocprofv3 PMC, {traffic_file})",
                          "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / args.steps, 4),

@@ -503,7 +503,11 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   const int Wo = a.Wo, Ho = a.Ho, Do = a.Do, Hi = a.Hi, Wi = a.Wi, Di = a.Di;
   const int GS = 32 * a.MS, XS = 16 * a.RX;
   float* gsl = smem;             // [2 slots][32 m][MS]: row yy at yy * Wo
-  float* xsl = smem + 2 * GS;    // [5 slots][16 c][RX]: row r (input row 2 y0 - 1 + r) at r * PX, col x + 2
+  // [5 slots][16 c][RX]: row r (input row 2 y0 - 1 + r) at r * PX, its even columns x = 2j at j and odd
+  // ones x = 2j + 1 at OB + j (OB = Wo + 2, zero at OB - 1 for x = -1): the stride-2 B reads of a wave
+  // then step by one float per lane (conflict-free at RX = 2 mod 32)
+  float* xsl = smem + 2 * GS;
+  const int OB = Wo + 2;
   const int tile = (int)blockIdx.y, mt = tile / a.ctiles, ct = tile - mt * a.ctiles;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < cv && yi >= 0 && yi < Hi;
     xg[j] = ok ? (int)(((int64_t)c * Di) * iplane / 4 + (yi * Wi + 4 * q) / 4) : -1;
-    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
+    xl[j] = c * a.RX + r * a.PX + 2 * q;
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {  // (m, yy, q): output row y0 + yy
@@ -553,9 +557,8 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
-        float2* p = reinterpret_cast<float2*>(d + xl[j]);
-        p[0] = make_float2(rx[j].x, rx[j].y);
-        p[1] = make_float2(rx[j].z, rx[j].w);
+        *reinterpret_cast<float2*>(d + xl[j]) = make_float2(rx[j].x, rx[j].z);
+        *reinterpret_cast<float2*>(d + xl[j] + OB) = make_float2(rx[j].y, rx[j].w);
       }
   };
   auto load_g = [&](int z) {
@@ -586,7 +589,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   const int li = lane & 15, lk = lane >> 4;
   const int mtl = wave & 1, par = wave >> 1;       // this wave's 16-row m-tile and k-step parity
   const int aoff = (16 * mtl + li) * a.MS + lk;    // A: G[m][x0 + lk]
-  const int boff = li * a.RX + 2 * lk + 1;         // B: X[c][row][2 (x0 + lk) + tx - 1] at col + 2
+  const int boff = li * a.RX + lk;                 // B: X[c][row][2 (x0 + lk) + tx - 1] (even / odd halves)
   f32x4 acc[27];
 #pragma unroll
   for (int j = 0; j < 27; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -615,7 +618,8 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-          for (int tx = 0; tx < 3; ++tx) bv[tz * 9 + ty * 3 + tx] = xp[tz][(2 * yy + ty) * a.PX + 2 * x0 + tx];
+          for (int tx = 0; tx < 3; ++tx)
+            bv[tz * 9 + ty * 3 + tx] = xp[tz][(2 * yy + ty) * a.PX + x0 + (tx == 1 ? 0 : OB - 1 + (tx >> 1))];
     };
     auto mm = [&](float av, const float (&bv)[27]) {
 #pragma unroll
@@ -670,7 +674,7 @@ struct Zf2Args {
   float* dW;
   int N, M, Cc, Do, Ho, Wo, Di, Hi, Wi;
   int YB, nyb, ZS, zlen;
-  int MS, RX, PX;
+  int MS, RX, PX, OB;  // OB: odd input columns' offset in a row (even ones at 0)
   int mtiles;  // blocks of MT m-tiles
 };
 
@@ -683,7 +687,11 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
   const int Wo = a.Wo, Ho = a.Ho, Do = a.Do, Hi = a.Hi, Wi = a.Wi, Di = a.Di, Cc = a.Cc;
   const int GS = 16 * MT * a.MS, XS = Cc * a.RX;
   float* gsl = smem;             // [2 slots][16 MT m][MS]: row yy at yy * Wo
-  float* xsl = smem + 2 * GS;    // [5 slots][Cc][RX]: row r (input row 2 y0 - 1 + r) at r * PX, col x + 2
+  // [5 slots][Cc][RX]: row r (input row 2 y0 - 1 + r) at r * PX, even columns x = 2j at j, odd ones
+  // x = 2j + 1 at OB + j (zero at OB - 1 for x = -1): a wave's stride-2 B reads step one float per lane,
+  // conflict-free at RX = 6, OB = 4 or 30 (mod 32)
+  float* xsl = smem + 2 * GS;
+  const int OB = a.OB;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -706,7 +714,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < Cc && yi >= 0 && yi < Hi;
     xg[j] = ok ? (int)(((int64_t)c * Di) * iplane / 4 + (yi * Wi + 4 * q) / 4) : -1;
-    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
+    xl[j] = c * a.RX + r * a.PX + 2 * q;
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {  // (m, yy, q)
@@ -733,9 +741,8 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
-        float2* p = reinterpret_cast<float2*>(d + xl[j]);
-        p[0] = make_float2(rx[j].x, rx[j].y);
-        p[1] = make_float2(rx[j].z, rx[j].w);
+        *reinterpret_cast<float2*>(d + xl[j]) = make_float2(rx[j].x, rx[j].z);
+        *reinterpret_cast<float2*>(d + xl[j] + OB) = make_float2(rx[j].y, rx[j].w);
       }
   };
   auto load_g = [&](int z) {
@@ -764,7 +771,8 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 
   const int li = lane & 15, lk = lane >> 4;
   const int bc = li < 3 * Cc ? li / 3 : 0, btx = li < 3 * Cc ? li - 3 * (li / 3) : 0;
-  const int boff = bc * a.RX + btx + 2 * lk + 1;  // B: X[c][row][2 (x0 + lk) + tx - 1] at col + 2
+  // B: X[c][row][2 (x0 + lk) + tx - 1]: even half for tx = 1, odd half (x0 + lk - 1 + tx / 2) otherwise
+  const int boff = bc * a.RX + (btx == 1 ? 0 : OB - 1 + (btx >> 1)) + lk;
   f32x4 acc[MT][9];
 #pragma unroll
   for (int t = 0; t < MT; ++t)
@@ -794,7 +802,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 #pragma unroll
       for (int tz = 0; tz < 3; ++tz)
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty) bv[tz * 3 + ty] = xp[tz][(2 * yy + ty) * a.PX + 2 * x0];
+        for (int ty = 0; ty < 3; ++ty) bv[tz * 3 + ty] = xp[tz][(2 * yy + ty) * a.PX + x0];
     };
     auto mm = [&](const float (&av)[MT], const float (&bv)[9]) {
 #pragma unroll
@@ -835,6 +843,182 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
     for (int w = 0; w < 4; ++w) v += red[((tj * 4 + w) * 4 + rr) * 64 + ln];
     const int c = col / 3, tx = col - 3 * c;
     atomicAdd(&a.dW[((int64_t)(m0 + m) * Cc + c) * 27 + j * 3 + tx], v);  // j = (tz, ty)
+  }
+}
+
+
+// Stride 1, few channels (9 M <= 32, 3 Cc <= 16: the 3->3 full-resolution layer).  MFMA rows are
+// (m, tz, ty) -- 27 of two 16-row tiles at M = 3 -- and columns (c, tx), so one k-step of 4 output
+// columns px of input row qy (plane qz) is 2 MFMAs (16x16x4 f32) reading 2 A values and 1 B value
+// per lane: A[(m, tz, ty)][px] = G[m][qz - tz + 1][qy - ty + 1][px], B[px][(c, tx)] =
+// X[c][qz][qy][px + tx - 1].  The block marches its (n, input row block, z segment) along qz: one
+// X plane (YB rows) and one G plane (YB + 2 rows) staged per step, G in a 4-slot ring; the next
+// step's slabs and the next k-step's operands are in flight while the MFMAs run.
+struct Zf1Args {
+  const float* G;
+  const float* X;
+  float* dW;
+  int N, M, Cc, D, H, W;
+  int YB, nyb, ZS, zlen;
+  int GR, GM, GS;  // G: row pitch, channel pitch, slot pitch (floats)
+  int XR, XC, XS;  // X: row pitch (data at col 4), channel pitch, slot pitch
+};
+
+template <int YB, int WV>  // input rows per block, W <= 4 WV
+__global__ __launch_bounds__(256) void k_conv3d_wgrad_zf1(Zf1Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int W = a.W, H = a.H, D = a.D, M = a.M, Cc = a.Cc;
+  float* gsl = smem;               // [4 slots][m][YB + 2 rows][GR]
+  float* xsl = smem + 4 * a.GS;    // [2 slots][c][YB rows][XR], x at col x + 4
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
+  for (int i = tid; i < 4 * a.GS + 2 * a.XS; i += 256) smem[i] = 0.f;  // halos and absent rows stay 0
+  const int64_t plane = (int64_t)H * W, plane4 = plane / 4;
+  const float* Gb = a.G + (int64_t)n * M * D * plane;
+  const float* Xb = a.X + (int64_t)n * Cc * D * plane;
+  const int W4v = W >> 2;
+  constexpr int NXL = (5 * YB * WV + 255) / 256, NGL = (3 * (YB + 2) * WV + 255) / 256;
+  int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
+#pragma unroll
+  for (int j = 0; j < NXL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4v, t = i / W4v, yy = t % YB, c = t / YB;
+    const bool ok = c < Cc && y0 + yy < H;
+    xg[j] = ok ? (int)(((int64_t)c * D) * plane4 + ((y0 + yy) * W + 4 * q) / 4) : -1;
+    xl[j] = c * a.XC + yy * a.XR + 4 + 4 * q;
+  }
+#pragma unroll
+  for (int j = 0; j < NGL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4v, t = i / W4v, r = t % (YB + 2), m = t / (YB + 2);
+    const int y = y0 - 1 + r;
+    const bool ok = m < M && y >= 0 && y < H;
+    gg[j] = ok ? (int)(((int64_t)m * D) * plane4 + (y * W + 4 * q) / 4) : -1;
+    gl[j] = m * a.GM + r * a.GR + 4 * q;
+  }
+  // the slabs of the next ZP steps are in flight in registers (a step's MFMAs take less than an HBM
+  // round trip): set p holds X[zi] and G[zi + 1] for the steps zi = p (mod ZP)
+  constexpr int ZP = 3;
+  float4 rx[ZP][NXL], rg[ZP][NGL];
+  auto load_x = [&](int zi, float4 (&r)[NXL]) {  // (planes past the segment: clamped, never stored)
+    const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(zi < D ? zi : D - 1) * plane4;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      r[j] = xg[j] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+    }
+  };
+  auto store_x = [&](int slot, const float4 (&r)[NXL]) {
+#pragma unroll
+    for (int j = 0; j < NXL; ++j)
+      if (xg[j] >= 0) *reinterpret_cast<float4*>(xsl + slot * a.XS + xl[j]) = r[j];
+  };
+  auto load_g = [&](int pz, float4 (&r)[NGL]) {  // G plane pz (zero outside [0, D))
+    const bool in = pz >= 0 && pz < D;
+    const float4* src = reinterpret_cast<const float4*>(Gb) + (int64_t)(in ? pz : 0) * plane4;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = src[gg[j] < 0 ? 0 : gg[j]];
+      r[j] = (in && gg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_g = [&](int slot, const float4 (&r)[NGL]) {
+#pragma unroll
+    for (int j = 0; j < NGL; ++j)
+      if (gg[j] >= 0) *reinterpret_cast<float4*>(gsl + slot * a.GS + gl[j]) = r[j];
+  };
+  __syncthreads();
+  load_g(z0 - 1, rg[0]);
+  store_g((z0 + 3) & 3, rg[0]);
+  load_g(z0, rg[0]);
+  store_g(z0 & 3, rg[0]);
+#pragma unroll
+  for (int p = 0; p < ZP; ++p) {
+    load_x(z0 + p, rx[p]);
+    load_g(z0 + p + 1, rg[p]);
+  }
+  // lane roles: A rows r = 16 t + (lane & 15) -> (m, tz, ty); B column (c, tx) = lane & 15; k = lane >> 4
+  const int li = lane & 15, lk = lane >> 4;
+  int atz[2], aoff[2];
+  bool aok[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int r = 16 * t + li, m = r / 9, tz = (r / 3) % 3, ty = r % 3;
+    aok[t] = m < M;
+    atz[t] = tz;
+    aoff[t] = aok[t] ? m * a.GM + (2 - ty) * a.GR + lk : 0;  // G row y0 - 1 + (yy - ty + 2)
+  }
+  const int bc = li / 3, btx = li - 3 * bc;
+  const bool bok = bc < Cc;
+  const int boff = bok ? bc * a.XC + 3 + btx + lk : 0;  // X col px + tx - 1 at +4
+  const int kpr = W >> 2, np = 4 / YB, yy = wave % YB, part = wave / YB;
+  const int kb = (kpr * part) / np, ke = (kpr * (part + 1)) / np;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) acc[0][t] = acc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto step = [&](int zi, float4 (&rxp)[NXL], float4 (&rgp)[NGL]) {
+    store_x(zi & 1, rxp);
+    store_g((zi + 1) & 3, rgp);
+    __syncthreads();
+    if (zi + ZP < z1) {
+      load_x(zi + ZP, rxp);
+      load_g(zi + ZP + 1, rgp);
+    }
+    // G plane qz - tz + 1 sits in slot (zi + 1 - tz) & 3
+    const float* ga0 = gsl + ((zi + 1 - atz[0]) & 3) * a.GS + aoff[0] + yy * a.GR;
+    const float* ga1 = gsl + ((zi + 1 - atz[1]) & 3) * a.GS + aoff[1] + yy * a.GR;
+    const float* xb = xsl + (zi & 1) * a.XS + boff + yy * a.XR;
+    auto ld = [&](int k, float& v0, float& v1, float& u) {
+      const int px = 4 * (k < ke ? k : ke - 1);
+      v0 = aok[0] ? ga0[px] : 0.f;
+      v1 = aok[1] ? ga1[px] : 0.f;
+      u = bok ? xb[px] : 0.f;
+    };
+    if (kb < ke) {
+      float p0, p1, pu, q0, q1, qu;
+      ld(kb, p0, p1, pu);
+      int k = kb;
+      for (; k + 1 < ke; k += 2) {
+        ld(k + 1, q0, q1, qu);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(p0, pu, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(p1, pu, acc[0][1], 0, 0, 0);
+        ld(k + 2, p0, p1, pu);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(q0, qu, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(q1, qu, acc[1][1], 0, 0, 0);
+      }
+      if (k < ke) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(p0, pu, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(p1, pu, acc[0][1], 0, 0, 0);
+      }
+    }
+  };
+  for (int zi = z0; zi < z1; zi += ZP) {
+    step(zi, rx[0], rg[0]);
+    if (zi + 1 < z1) step(zi + 1, rx[1], rg[1]);
+    if (zi + 2 < z1) step(zi + 2, rx[2], rg[2]);
+  }
+  __syncthreads();
+  float* red = smem;  // [2 tiles][4 waves][4 rr][64 lanes]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[((t * 4 + wave) * 4 + rr) * 64 + lane] = acc[0][t][rr] + acc[1][t][rr];
+  __syncthreads();
+  for (int e = tid; e < 2 * 4 * 64; e += 256) {  // e = (t, rr, lane)
+    const int ln = e & 63, rr = (e >> 6) & 3, t = e >> 8;
+    const int r = 16 * t + 4 * (ln >> 4) + rr, col = ln & 15;
+    const int m = r / 9, c = col / 3;
+    if (m >= M || c >= Cc) continue;
+    const int tz = (r / 3) % 3, ty = r % 3, tx = col - 3 * c;
+    const float v = red[((t * 4 + 0) * 4 + rr) * 64 + ln] + red[((t * 4 + 1) * 4 + rr) * 64 + ln] +
+                    red[((t * 4 + 2) * 4 + rr) * 64 + ln] + red[((t * 4 + 3) * 4 + rr) * 64 + ln];
+    atomicAdd(&a.dW[((int64_t)m * Cc + c) * 27 + tz * 9 + ty * 3 + tx], v);
   }
 }
 
@@ -1060,7 +1244,7 @@ bool use_zm2(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, 
 int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi,
               int Wi, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
-  a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
+  a.PX = 2 * Wo + 2;  // even half 0 .. Wo - 1, odd half Wo + 2 .. 2 Wo + 1 (zeros at Wo, Wo + 1)
   static const int yb_env = [] {
     const char* e = std::getenv("TEXBIAS_WGRAD_ZM2_YB");
     return e ? std::atoi(e) : 0;
@@ -1068,7 +1252,7 @@ int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do,
   a.YB = 0;
   for (int yb : {2, 1}) {  // two output rows per block where the ring fits: twice the MFMAs per staged plane
     if ((yb_env && yb != yb_env) || yb > Ho) continue;
-    for (int rem : {2, 4}) {  // X channel pitch mod 32: 2 (2-way B conflicts), 4 (tighter pad)
+    for (int rem : {2, 4}) {  // X channel pitch mod 32: 2 (conflict-free B reads), 4 (tighter pad, 2-way)
       const int rx = pad_mod32((2 * yb + 1) * a.PX, rem), ms = pad_mod32(yb * Wo, 2);
       const size_t ring = (size_t)4 * (2 * 32 * ms + 5 * 16 * rx), red = (size_t)4 * 2 * 27 * 4 * 64;
       const size_t need = ring > red ? ring : red;
@@ -1126,10 +1310,12 @@ int zf2_setup(Zf2Args& a, int& MT, size_t& lds, dim3& grid, int N, int M, int Cc
               int Hi, int Wi, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
   MT = M > 16 ? 2 : 1;
-  a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
+  a.OB = Wo + 2;  // even, >= Wo + 1, = 4 or 30 (mod 32)
+  while ((a.OB & 31) != 4 && (a.OB & 31) != 30) a.OB += 2;
+  a.PX = a.OB + Wo;
   a.YB = 0;
   for (int yb : {4, 2, 1}) {
-    const int rx = pad_mod32((2 * yb + 1) * a.PX, 8), ms = pad_mod32(yb * Wo, 2);
+    const int rx = pad_mod32((2 * yb + 1) * a.PX, 6), ms = pad_mod32(yb * Wo, 2);
     const size_t ring = (size_t)4 * (2 * 16 * MT * ms + 5 * Cc * rx), red = (size_t)4 * MT * 9 * 4 * 4 * 64;
     const size_t need = ring > red ? ring : red;
     if (need <= 163840) {
@@ -1171,6 +1357,73 @@ int launch_zf2(const Zf2Args& a, int MT, size_t lds, dim3 grid, hipStream_t st) 
   if (MT == 1) return a.YB == 4 ? launch_zf2_t<4, 1>(a, lds, grid, st) : a.YB == 2 ? launch_zf2_t<2, 1>(a, lds, grid, st) : launch_zf2_t<1, 1>(a, lds, grid, st);
   return a.YB == 4 ? launch_zf2_t<4, 2>(a, lds, grid, st) : a.YB == 2 ? launch_zf2_t<2, 2>(a, lds, grid, st) : launch_zf2_t<1, 2>(a, lds, grid, st);
 }
+
+// few-channel stride-1 z-marching kernel (k_conv3d_wgrad_zf1): 9 M <= 32, 3 Cc <= 16, W % 4 == 0
+bool use_zf1(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZF1");
+    return !(e && e[0] == '0');
+  }();
+  return on && stride == 1 && M <= 3 && Cc <= 5 && Do == Di && Ho == Hi && Wo == Wi && Wo % 4 == 0 && Wo <= 256 &&
+         (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+
+int zf1_setup(Zf1Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, int H, int W, int ncu) {
+  a.N = N; a.M = M; a.Cc = Cc; a.D = D; a.H = H; a.W = W;
+  static const int yb_env = [] {
+    const char* e = std::getenv("TEXBIAS_WGRAD_ZF1_YB");
+    return e ? std::atoi(e) : 0;
+  }();
+  // pitches: rows of one G channel 4 banks apart, channels and slots spread over the banks
+  a.GR = pad_mod32(W, 4);
+  a.XR = pad_mod32(W + 8, 4);
+  a.YB = 0;
+  for (int yb : {2, 4, 1}) {
+    if (yb_env && yb != yb_env) continue;
+    const int gm = pad_mod32((yb + 2) * a.GR, 12), gs = pad_mod32(M * gm, 20);
+    const int xc = pad_mod32(yb * a.XR, 8), xs = pad_mod32(Cc * xc, 16);
+    const size_t bytes = (size_t)4 * (4 * gs + 2 * xs);
+    if (bytes <= 81920) {  // two blocks per CU
+      a.YB = yb; a.GM = gm; a.GS = gs; a.XC = xc; a.XS = xs;
+      lds = bytes > (size_t)2 * 4 * 4 * 64 * 4 ? bytes : (size_t)2 * 4 * 4 * 64 * 4;
+      break;
+    }
+  }
+  if (!a.YB) return TB_ERR_UNSUPPORTED_SIZE;
+  a.nyb = (H + a.YB - 1) / a.YB;
+  // z segments: two blocks per CU; ceil(blocks / (2 CUs)) rounds of zlen + 2 plane steps
+  const int base = N * a.nyb;
+  int best = 1 << 30;
+  a.zlen = D;
+  for (int zl = D; zl >= 1; --zl) {
+    const int zs = (D + zl - 1) / zl;
+    const int rounds = (base * zs + 2 * ncu - 1) / (2 * ncu);
+    const int cost = rounds * (zl + 2);
+    if (cost < best) {
+      best = cost;
+      a.zlen = zl;
+    }
+  }
+  a.ZS = (D + a.zlen - 1) / a.zlen;
+  grid = dim3((unsigned)(N * a.nyb * a.ZS));
+  return TB_OK;
+}
+
+template <int YB>
+int launch_zf1_t(const Zf1Args& a, size_t lds, dim3 grid, hipStream_t st) {
+  auto kern = a.W <= 128 ? k_conv3d_wgrad_zf1<YB, 32>
+                         : a.W <= 160 ? k_conv3d_wgrad_zf1<YB, 40> : k_conv3d_wgrad_zf1<YB, 64>;
+  const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  if (attr != hipSuccess) return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+int launch_zf1(const Zf1Args& a, size_t lds, dim3 grid, hipStream_t st) {
+  return a.YB == 4 ? launch_zf1_t<4>(a, lds, grid, st) : a.YB == 2 ? launch_zf1_t<2>(a, lds, grid, st)
+                                                                    : launch_zf1_t<1>(a, lds, grid, st);
+}
 }  // namespace
 
 // dW (M x Cc x 27, zeroed here) of a 3x3x3 convolution with stride 1 or 2, padding 1 (file header).
@@ -1206,6 +1459,21 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
       z.G = G; z.X = X; z.dW = dW;
       if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st0) != hipSuccess) return TB_ERR_HIP;
       return launch_zm2(z, lds, grid, st0);
+    }
+  }
+  if (pad == 1 && N >= 1 && use_zf1(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {
+    static const int ncu4 = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+      return n;
+    }();
+    Zf1Args z{};
+    size_t lds = 0;
+    dim3 grid;
+    if (zf1_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, ncu4) == TB_OK) {
+      z.G = G; z.X = X; z.dW = dW;
+      if (hipMemsetAsync(dW, 0, sizeof(float) * (size_t)M * Cc * 27, st0) != hipSuccess) return TB_ERR_HIP;
+      return launch_zf1(z, lds, grid, st0);
     }
   }
   if (pad == 1 && N >= 1 && use_zf2(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {

@@ -66,23 +66,37 @@ __device__ __forceinline__ double wave_sum(double v) {
 // consecutive quads (coalesced); a thread issues all loads of a round before using them.
 constexpr int PT_QU = 4;
 
-__device__ __forceinline__ void load_quad(const float* row, int d0, int D, bool vec, float (&v)[4]) {
-  if (vec && d0 + 4 <= D) {
-    const float4 q = *reinterpret_cast<const float4*>(row + d0);
-    v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
-  } else {
+// A whole quad is one 16-B load even where the row is only dword aligned (the 155-column BraTS rows):
+// gfx950's global loads take dword-aligned dwordx4 addresses, and 64 lanes still sweep ~1 KB of
+// consecutive bytes.  The partial last quad of a row loads the row's last 4 floats and shifts them
+// down with selects: no branch, so no lane's tail forces a wait on the loads already in flight
+// (a divergent scalar tail path made the compiler drain vmcnt at every row end).  D >= 4.
+typedef float f32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ void load_quad(const float* row, int d0, int D, bool ok, float (&v)[4]) {
+  const int dl = d0 + 4 <= D ? d0 : D - 4, sh = ok ? d0 - dl : 4;  // sh 4: nothing
+  const f32x4_a4 q = *reinterpret_cast<const f32x4_a4*>(row + dl);
+  const float e[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = d0 + j < D ? row[d0 + j] : 0.f;
+  for (int j = 0; j < 4; ++j) {
+    float t = 0.f;
+#pragma unroll
+    for (int s = 0; s + j < 4; ++s) t = sh == s ? e[j + s] : t;
+    v[j] = t;
   }
 }
 
-// per-axis twiddle tables of the active spikes: t[k][i] = e^{sgn 2 pi i f_k,axis i / n}, i < n (+3 zero
-// entries past D for the partial last quad)
-__device__ __forceinline__ void point_tables(const int* act, int na, int H, int W, int D, float sgn, float2* tD,
-                                             float2* tW, float2* tH) {
-  const int Dp = D + 3;
-  for (int t = threadIdx.x; t < na * Dp; t += POINT_NT) {
-    const int k = t / Dp, d = t - k * Dp;
+// per-axis twiddle tables of the active spikes: along D quad-major, tD[(k * 4 + j) * NQ + q] =
+// e^{sgn 2 pi i f_k,d (4q + j) / D} (zero for 4q + j >= D), so the lanes of a wave (consecutive quads)
+// read consecutive entries; tW[k][w], tH[k][h] (one entry per row: broadcast reads)
+// (QM false: d-major, tD[k][d] -- the many-spike kernels, whose 4 reads per quad then share one
+// address register)
+template <bool QM>
+__device__ __forceinline__ void point_tables(const int* act, int na, int H, int W, int D, int NQ, float sgn,
+                                             float2* tD, float2* tW, float2* tH) {
+  for (int t = threadIdx.x; t < na * 4 * NQ; t += POINT_NT) {
+    const int k = t / (4 * NQ), r = t - k * 4 * NQ;
+    const int d = QM ? 4 * (r % NQ) + r / NQ : r;
     tD[t] = d < D ? cis_f(mulmod(act[3 + 4 * k], d, D), D, sgn) : make_float2(0.f, 0.f);
   }
   for (int t = threadIdx.x; t < na * W; t += POINT_NT) {
@@ -95,10 +109,115 @@ __device__ __forceinline__ void point_tables(const int* act, int na, int H, int 
   }
 }
 
+// A thread's rounds: QU quads POINT_NT apart per round, consecutive rounds STEP quads apart.  The
+// (h, w, quad) of each slot is advanced by STEP with two carries instead of divided out per quad, and
+// the row offset is 32-bit (point_strides_ok); a used quad travels as one code h << 20 | w << 10 | q
+// (-1 past the range: its values are 0).
+template <int QU>
+struct QuadWalk {
+  static constexpr int STEP = QU * POINT_NT;
+  typedef float Vals[QU][4];
+  typedef int Codes[QU];
+  const float* xb;
+  uint32_t xsh, xsw;
+  int qb, qe, nq, W, D;
+  int dq, dw, dh;  // STEP = (dh W + dw) nq + dq
+  struct State {
+    int lin[QU], h[QU], w[QU], q[QU];
+  };
+  __device__ __forceinline__ static QuadWalk make(const float* xb, int64_t xsh, int64_t xsw, int qb, int qe, int nq,
+                                                  int W, int D) {
+    QuadWalk k{xb, (uint32_t)xsh, (uint32_t)xsw, qb, qe, nq, W, D, 0, 0, 0};
+    const int rows = STEP / nq;
+    k.dq = STEP - rows * nq;
+    k.dh = rows / W;
+    k.dw = rows - k.dh * W;
+    return k;
+  }
+  __device__ __forceinline__ void init(int q0, State& s) const {
+#pragma unroll
+    for (int u = 0; u < QU; ++u) {
+      const int l = q0 + u * POINT_NT, t = l < qe ? l : qb;
+      const int h = t / (W * nq), r = t - h * (W * nq), w = r / nq;
+      s.lin[u] = l;
+      s.h[u] = h;
+      s.w[u] = w;
+      s.q[u] = r - w * nq;
+    }
+  }
+  __device__ __forceinline__ void load(State& s, Vals& v, Codes& c) const {
+#pragma unroll
+    for (int u = 0; u < QU; ++u) {
+      const bool ok = s.lin[u] < qe;
+      const uint32_t off = ok ? (uint32_t)s.h[u] * xsh + (uint32_t)s.w[u] * xsw : 0u;
+      load_quad(xb + off, 4 * s.q[u], D, ok && 4 * s.q[u] < D, v[u]);
+      c[u] = ok ? (s.h[u] << 20) | (s.w[u] << 10) | s.q[u] : -1;
+      // next round
+      s.lin[u] += STEP;
+      int q = s.q[u] + dq, w = s.w[u] + dw, h = s.h[u] + dh;
+      const bool cq = q >= nq;
+      q -= cq ? nq : 0;
+      w += cq ? 1 : 0;
+      const bool cw = w >= W;
+      w -= cw ? W : 0;
+      h += cw ? 1 : 0;
+      s.q[u] = q;
+      s.w[u] = w;
+      s.h[u] = h;
+    }
+  }
+  // body(values, codes) over every round of [qb, qe) from thread tid with the next DEPTH - 1 rounds'
+  // loads in flight while the current one is used (DEPTH 1: load, use, load, ... -- the many-spike
+  // kernels, whose bodies need the registers)
+  template <int DEPTH, class F>
+  __device__ __forceinline__ void run(int tid, F&& body) const {
+    State s;
+    init(qb + tid, s);
+    Vals va, vb, vc;
+    Codes ca, cb, cc;
+    if (DEPTH == 1) {
+      while (s.lin[0] < qe) {
+        load(s, va, ca);
+        body(va, ca);
+      }
+    } else if (DEPTH == 2) {
+      load(s, va, ca);
+      while (ca[0] >= 0) {
+        load(s, vb, cb);
+        body(va, ca);
+        if (cb[0] < 0) break;
+        load(s, va, ca);
+        body(vb, cb);
+      }
+    } else {
+      load(s, va, ca);
+      load(s, vb, cb);
+      while (true) {
+        if (ca[0] < 0) break;
+        load(s, vc, cc);
+        body(va, ca);
+        if (cb[0] < 0) break;
+        load(s, va, ca);
+        body(vb, cb);
+        if (cc[0] < 0) break;
+        load(s, vb, cb);
+        body(vc, cc);
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ void quad_decode(int code, int& h, int& w, int& q) {
+  h = code >> 20;
+  w = (code >> 10) & 1023;
+  q = code & 1023;
+}
+
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+template <int NA>  // most spikes per volume-channel the launch handles (1, or TB_MAX_OPS)
 __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
   const PointArgs& a = kargs<PointArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -109,63 +228,56 @@ __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
   point_active(a, bcl, act);
   const int na = __builtin_amdgcn_readfirstlane(act[0]);
   if (na == 0) return;
-  const int Dp = D + 3;
+  const int NQ = (D + 3) / 4, TQ = 4 * NQ;
   // the D factors again as float64 pairs (exact widenings of the float table: the inner product's
   // FMAs then read them without two conversions per voxel and spike)
   double2* tDd = reinterpret_cast<double2*>(smem);
-  float2* tD = reinterpret_cast<float2*>(tDd + a.namax * Dp);  // e^{-2 pi i f . n / N}, [namax][n] per axis
-  float2* tW = tD + a.namax * Dp;
+  float2* tD = reinterpret_cast<float2*>(tDd + a.namax * TQ);  // e^{-2 pi i f . n / N}, per axis
+  float2* tW = tD + a.namax * TQ;
   float2* tH = tW + a.namax * W;
   double* red = reinterpret_cast<double*>(tH + a.namax * H);  // [4 waves][TB_MAX_OPS][2]
-  point_tables(act, na, H, W, D, -1.f, tD, tW, tH);
+  point_tables<NA == 1>(act, na, H, W, D, NQ, -1.f, tD, tW, tH);
   __syncthreads();
-  for (int t = tid; t < na * Dp; t += POINT_NT) tDd[t] = make_double2((double)tD[t].x, (double)tD[t].y);
+  for (int t = tid; t < na * TQ; t += POINT_NT) tDd[t] = make_double2((double)tD[t].x, (double)tD[t].y);
   __syncthreads();
-  const float* xb = a.x + (int64_t)bc * a.xsbc;
-  const bool vec = (a.xsw & 3) == 0 && (a.xsh & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
-  const int nq = (D + 3) / 4, nrow = W * nq;
+  const int nrow = W * NQ;
   const int64_t nall = (int64_t)H * nrow;
-  const int qb = (int)(nall * part / a.parts), qe = (int)(nall * (part + 1) / a.parts);
-  const FastDiv frow = FastDiv::make(nrow), fq = FastDiv::make(nq);
+  // one spike: two rounds (8 KB per wave) in flight -- the read-only stream has nothing else to cover
+  // the HBM latency with
+  constexpr int QU = PT_QU;
+  using QW = QuadWalk<QU>;
+  const QW qw = QW::make(a.x + (int64_t)bc * a.xsbc, a.xsh, a.xsw, (int)(nall * part / a.parts),
+                         (int)(nall * (part + 1) / a.parts), NQ, W, D);
   // float64 sums: the coefficient of a bin whose value is cancellation noise (the DC of a zero-mean
   // channel) keeps the sign of the exact sum, as the reference's FFT mostly does
-  double accr[TB_MAX_OPS], acci[TB_MAX_OPS];
+  double accr[NA], acci[NA];
 #pragma unroll
-  for (int k = 0; k < TB_MAX_OPS; ++k) accr[k] = acci[k] = 0.0;
-  for (int q0 = qb + tid; q0 < qe; q0 += PT_QU * POINT_NT) {
-    float v[PT_QU][4];
-    int hh[PT_QU], ww[PT_QU], dd[PT_QU];
+  for (int k = 0; k < NA; ++k) accr[k] = acci[k] = 0.0;
+  qw.template run<NA == 1 ? 3 : 1>(tid, [&](const typename QW::Vals& v, const typename QW::Codes& cd) {
 #pragma unroll
-    for (int u = 0; u < PT_QU; ++u) {
-      const int q = q0 + u * POINT_NT < qe ? q0 + u * POINT_NT : qb;
-      const int h = frow.div(q), r = q - h * nrow, w = fq.div(r);
-      hh[u] = q0 + u * POINT_NT < qe ? h : -1;
-      ww[u] = w;
-      dd[u] = 4 * (r - w * nq);
-      load_quad(xb + (int64_t)h * a.xsh + (int64_t)w * a.xsw, dd[u], hh[u] >= 0 ? D : 0, vec, v[u]);
-    }
+    for (int u = 0; u < QU; ++u) {
+      if (NA > 1 && cd[u] < 0) break;
+      int h, w, q;
+      quad_decode(cd[u] < 0 ? 0 : cd[u], h, w, q);  // past the range: the values are 0, any twiddles do
 #pragma unroll
-    for (int u = 0; u < PT_QU; ++u) {
-      if (hh[u] < 0) break;
-#pragma unroll
-      for (int k = 0; k < TB_MAX_OPS; ++k) {
+      for (int k = 0; k < NA; ++k) {
         if (k >= na) break;
-        const double2* t = tDd + k * Dp + dd[u];
+        const double2* t = tDd + 4 * k * NQ + (NA == 1 ? q : 4 * q);
         double sr = 0.0, si = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const double2 tj = t[j];
+          const double2 tj = t[NA == 1 ? j * NQ : j];
           sr = fma((double)v[u][j], tj.x, sr);
           si = fma((double)v[u][j], tj.y, si);
         }
-        const float2 r = cmul(tW[k * W + ww[u]], tH[k * H + hh[u]]);
-        accr[k] += sr * (double)r.x - si * (double)r.y;
-        acci[k] += sr * (double)r.y + si * (double)r.x;
+        const float2 rr = cmul(tW[k * W + w], tH[k * H + h]);
+        accr[k] += sr * (double)rr.x - si * (double)rr.y;
+        acci[k] += sr * (double)rr.y + si * (double)rr.x;
       }
     }
-  }
+  });
 #pragma unroll
-  for (int k = 0; k < TB_MAX_OPS; ++k) {
+  for (int k = 0; k < NA; ++k) {
     if (k >= na) break;
     const double vr = wave_sum(accr[k]), vi = wave_sum(acci[k]);
     if (lane == 0) {
@@ -224,6 +336,7 @@ __global__ __launch_bounds__(64) void k_point_delta(PointArgs) {
   }
 }
 
+template <int NA>
 __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
   const PointArgs& a = kargs<PointArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -233,67 +346,58 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
   __shared__ float2 dls[TB_MAX_OPS];
   point_active(a, bcl, act);
   const int na = __builtin_amdgcn_readfirstlane(act[0]);
-  const int Dp = D + 3;
-  float2* tD = reinterpret_cast<float2*>(smem);  // e^{+2 pi i f . n / N} factors, [namax][n] per axis
-  float2* tW = tD + a.namax * Dp;
+  const int ncol = D + a.ypad;
+  const int NQ = (ncol + 3) / 4, TQ = 4 * NQ;  // quads of output columns (the table is zero past D)
+  float2* tD = reinterpret_cast<float2*>(smem);  // e^{+2 pi i f . n / N} factors, per axis
+  float2* tW = tD + a.namax * TQ;
   float2* tH = tW + a.namax * W;
   float* red = reinterpret_cast<float*>(tH + a.namax * H);
-  point_tables(act, na, H, W, D, 1.f, tD, tW, tH);
+  point_tables<NA == 1>(act, na, H, W, D, NQ, 1.f, tD, tW, tH);
   if (tid < na) dls[tid] = reinterpret_cast<const float2*>(a.delta)[bcl * TB_MAX_OPS + act[4 + 4 * tid]];
   __syncthreads();
-  const float* xb = a.x + (int64_t)bc * a.xsbc;
   float* yb = a.y + (int64_t)bc * a.ysbc;
-  const int ncol = D + a.ypad;
-  const bool vin = (a.xsw & 3) == 0 && (a.xsh & 3) == 0 && (reinterpret_cast<uintptr_t>(xb) & 15) == 0;
   const bool vout = (a.ysw & 3) == 0 && (a.ysh & 3) == 0 && (reinterpret_cast<uintptr_t>(yb) & 15) == 0;
-  const int nq = (ncol + 3) / 4, nrow = W * nq;  // quads of output columns
+  const int nrow = W * NQ;
   const int64_t nall = (int64_t)H * nrow;
-  const int qb = (int)(nall * part / a.parts_apply), qe = (int)(nall * (part + 1) / a.parts_apply);
-  const FastDiv frow = FastDiv::make(nrow), fq = FastDiv::make(nq);
+  using QW = QuadWalk<PT_QU>;
+  const QW qw = QW::make(a.x + (int64_t)bc * a.xsbc, a.xsh, a.xsw, (int)(nall * part / a.parts_apply),
+                         (int)(nall * (part + 1) / a.parts_apply), NQ, W, D);
   float lo = 3.402823466e38f, hi = -3.402823466e38f;
-  for (int q0 = qb + tid; q0 < qe; q0 += PT_QU * POINT_NT) {
-    float v[PT_QU][4];
-    int hh[PT_QU], ww[PT_QU], dd[PT_QU];
+  qw.template run<NA == 1 ? 2 : 1>(tid, [&](const typename QW::Vals& vin, const typename QW::Codes& cd) {
 #pragma unroll
     for (int u = 0; u < PT_QU; ++u) {
-      const int q = q0 + u * POINT_NT < qe ? q0 + u * POINT_NT : qb;
-      const int h = frow.div(q), r = q - h * nrow, w = fq.div(r);
-      hh[u] = q0 + u * POINT_NT < qe ? h : -1;
-      ww[u] = w;
-      dd[u] = 4 * (r - w * nq);
-      load_quad(xb + (int64_t)h * a.xsh + (int64_t)w * a.xsw, dd[u], hh[u] >= 0 ? D : 0, vin, v[u]);
-    }
+      if (cd[u] < 0) break;
+      int h, w, q;
+      quad_decode(cd[u], h, w, q);
+      const int d0 = 4 * q;
+      float v[4] = {vin[u][0], vin[u][1], vin[u][2], vin[u][3]};
 #pragma unroll
-    for (int u = 0; u < PT_QU; ++u) {
-      if (hh[u] < 0) break;
-      const int d0 = dd[u];
-#pragma unroll
-      for (int k = 0; k < TB_MAX_OPS; ++k) {
+      for (int k = 0; k < NA; ++k) {
         if (k >= na) break;
-        const float2 r = cmul(dls[k], cmul(tH[k * H + hh[u]], tW[k * W + ww[u]]));
-        const float2* t = tD + k * Dp + (d0 < D ? d0 : 0);
+        const float2 rr = cmul(dls[k], cmul(tH[k * H + h], tW[k * W + w]));
+        const float2* t = tD + 4 * k * NQ + (NA == 1 ? q : 4 * q);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float2 tj = t[j];
-          v[u][j] += d0 < D ? r.x * tj.x - r.y * tj.y : 0.f;
+          const float2 tj = t[NA == 1 ? j * NQ : j];  // zero past D: the padding stays 0
+          v[j] += rr.x * tj.x - rr.y * tj.y;
         }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (d0 + j < D) {
-          lo = fminf(lo, v[u][j]);
-          hi = fmaxf(hi, v[u][j]);
+          lo = fminf(lo, v[j]);
+          hi = fmaxf(hi, v[j]);
         }
-      float* yr = yb + (int64_t)hh[u] * a.ysh + (int64_t)ww[u] * a.ysw;
+      float* yr = yb + ((uint32_t)h * (uint32_t)a.ysh + (uint32_t)w * (uint32_t)a.ysw);
       if (vout && d0 + 4 <= ncol) {
-        *reinterpret_cast<float4*>(yr + d0) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+        *reinterpret_cast<float4*>(yr + d0) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (d0 + j < ncol) yr[d0 + j] = v[u][j];
+          if (d0 + j < ncol) yr[d0 + j] = v[j];
       }
     }
-  }
+  });
   if (!a.mm) return;
   // per-workgroup (min, max), then the last workgroup to arrive writes every sample's keys (no
   // same-address atomics from thousands of workgroups)
@@ -351,7 +455,7 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
 }
 
 bool point_program(const tb_sample_ops& s, int H, int W, int D) {
-  if (s.n < 1 || (size_t)TB_MAX_OPS * (H + W + D + 3) * sizeof(float2) > 65536) return false;
+  if (s.n < 1 || D < 4 || (size_t)TB_MAX_OPS * (H + W + D + 3) * sizeof(float2) > 65536) return false;
   // k_point_dft adds the float64 D table (and its wave sums)
   if ((size_t)TB_MAX_OPS * ((H + W + D + 3) * sizeof(float2) + (D + 3) * sizeof(double2)) +
           4 * TB_MAX_OPS * 2 * sizeof(double) > 163840)
@@ -374,8 +478,9 @@ bool point_program(const tb_sample_ops& s, int H, int W, int D) {
 }
 
 static size_t point_lds(const PointArgs& a, int stage) {
-  const size_t tabs = (size_t)a.namax * (a.D + 3 + a.W + a.H) * sizeof(float2);
-  return stage == 0 ? (size_t)a.namax * (a.D + 3) * sizeof(double2) + tabs + 4 * TB_MAX_OPS * 2 * sizeof(double)
+  const int tq = stage == 0 ? 4 * ((a.D + 3) / 4) : 4 * ((a.D + a.ypad + 3) / 4);
+  const size_t tabs = (size_t)a.namax * (tq + a.W + a.H) * sizeof(float2);
+  return stage == 0 ? (size_t)a.namax * tq * sizeof(double2) + tabs + 4 * TB_MAX_OPS * 2 * sizeof(double)
                     : tabs + 2 * POINT_NT / 64 * sizeof(float);
 }
 
@@ -402,20 +507,28 @@ static int point_parts(K kern, size_t lds, int nbc, int ncu) {
 }
 
 void point_grid(PointArgs& a, int ncu) {
-  (void)allow_lds(k_point_dft, point_lds(a, 0));  // occupancy is queried at the launch's LDS size
-  a.parts = point_parts(k_point_dft, point_lds(a, 0), a.nbc, ncu);
-  a.parts_apply = point_parts(k_point_apply, point_lds(a, 2), a.nbc, ncu);
+  // occupancy is queried at the launch's LDS size
+  const auto kd = a.namax == 1 ? k_point_dft<1> : k_point_dft<TB_MAX_OPS>;
+  const auto ka = a.namax == 1 ? k_point_apply<1> : k_point_apply<TB_MAX_OPS>;
+  (void)allow_lds(kd, point_lds(a, 0));
+  a.parts = point_parts(kd, point_lds(a, 0), a.nbc, ncu);
+  (void)allow_lds(ka, point_lds(a, 2));
+  a.parts_apply = point_parts(ka, point_lds(a, 2), a.nbc, ncu);
 }
 
 hipError_t launch_point(const PointArgs& a, hipStream_t st, int stage) {
   if (stage == 0) {
-    const hipError_t e = allow_lds(k_point_dft, point_lds(a, 0));
+    const auto kd = a.namax == 1 ? k_point_dft<1> : k_point_dft<TB_MAX_OPS>;
+    const hipError_t e = allow_lds(kd, point_lds(a, 0));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_point_dft, dim3(a.parts, a.nbc), dim3(POINT_NT), point_lds(a, 0), st, a);
+    hipLaunchKernelGGL(kd, dim3(a.parts, a.nbc), dim3(POINT_NT), point_lds(a, 0), st, a);
   } else if (stage == 1) {
     hipLaunchKernelGGL(k_point_delta, dim3(a.nbc), dim3(64), 0, st, a);
   } else {
-    hipLaunchKernelGGL(k_point_apply, dim3(a.parts_apply, a.nbc), dim3(POINT_NT), point_lds(a, 2), st, a);
+    const auto ka = a.namax == 1 ? k_point_apply<1> : k_point_apply<TB_MAX_OPS>;
+    const hipError_t e = allow_lds(ka, point_lds(a, 2));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ka, dim3(a.parts_apply, a.nbc), dim3(POINT_NT), point_lds(a, 2), st, a);
   }
   return hipGetLastError();
 }

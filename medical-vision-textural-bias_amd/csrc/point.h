@@ -52,6 +52,15 @@ inline PointWs point_ws(int nbc) {
 
 // Every op is a spike and no two touch (same or conjugate frequency in an overlapping channel).
 bool point_program(const tb_sample_ops& s, int H, int W, int D);
+// The kernels' index codes and 32-bit row offsets hold: H <= 2048, W <= 1024, (D + pad + 3) / 4 < 1024
+// quads, and every row of a volume-channel of x and y within 2^32 elements of its first.
+inline bool point_strides_ok(int H, int W, int D, int ypad, const int64_t* xs, const int64_t* ys) {
+  if (H > 2048 || W > 1024 || (D + ypad + 3) / 4 >= 1024) return false;
+  const int64_t lim = (int64_t)1 << 32;
+  return (int64_t)(H - 1) * xs[1] + (int64_t)(W - 1) * xs[2] + D < lim &&
+         (int64_t)(H - 1) * ys[1] + (int64_t)(W - 1) * ys[2] + D + ypad < lim && xs[1] >= 0 && xs[2] >= 0 &&
+         ys[1] >= 0 && ys[2] >= 0;
+}
 // Sets a.parts / a.parts_apply: one round of resident workgroups per launch (ncu x occupancy, at most
 // POINT_WG), split evenly over the launch's volume-channels.
 void point_grid(PointArgs& a, int ncu);

@@ -920,7 +920,8 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
       while (j < nb && route(b0 + j, &al) == run.route && (run.route != RUN_WRAP || al == al0)) ++j;
       run.s0 = b0 + i;
       run.s1 = b0 + j;
-      if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_ws(B * C).total) {
+      if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_ws(B * C).total &&
+          tb::point_strides_ok(p->dev.H, p->dev.W, p->dev.D, y_pad, xs, ys)) {
         bool pt = true;
         for (int s = run.s0; s < run.s1 && pt; ++s) pt = tb::point_program(ops[s], p->dev.H, p->dev.W, p->dev.D);
         if (pt) run.route = RUN_POINT;
@@ -1013,6 +1014,7 @@ int tb_planes_closed_form_f32(const tb_plan* p, const float* x, const int64_t* x
   for (int b = 0; b < B; ++b)
     if (ops[b].n < 1 || ops[b].n > TB_MAX_OPS || !tb::point_program(ops[b], p->dev.H, p->dev.W, p->dev.D))
       return TB_ERR_INVALID_ARG;  // not spike-only, or two spikes touch: tb_kspace_filter_f32 takes those
+  if (!tb::point_strides_ok(p->dev.H, p->dev.W, p->dev.D, y_pad, xs, ys)) return TB_ERR_UNSUPPORTED_SIZE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   for (int b0 = 0; b0 < B; b0 += TB_MAX_BATCH) {
     const int nb = (B - b0) < TB_MAX_BATCH ? (B - b0) : TB_MAX_BATCH;

@@ -111,6 +111,22 @@ def plane_waves(x: np.ndarray, idx: Sequence[int], intensity: float,
     return inv_shift_fourier(k2, 3)
 
 
+def spikes_exact(x: np.ndarray, sets) -> np.ndarray:
+    """The float64 exact result of a spike program: the same coefficient replacements as
+    plane_waves / kspace_spike (:370-393, :966-983 -- |k| := exp(val) at each location, phase kept or
+    overridden), in a float64 spectrum with every other coefficient left untouched (no float32 polar
+    round trip).  ``sets``: (idx, val, phase) with idx spatial (all channels) or (c, h, w, d);
+    phase None keeps angle(k).  The closed-form route's own target (it adds each spike's plane wave
+    to x), to ~1e-15."""
+    ax = _axes(3)
+    k = np.fft.fftshift(np.fft.fftn(np.asarray(x, np.float64), axes=ax), axes=ax)
+    for idx, val, phase in sets:
+        sel = tuple(idx) if len(idx) == 4 else (slice(None),) + tuple(idx)
+        ph = np.angle(k[sel]) if phase is None else np.float64(np.float32(phase))
+        k[sel] = np.exp(np.float64(np.float32(val))) * np.exp(1j * ph)
+    return np.fft.ifftn(np.fft.ifftshift(k, axes=ax), axes=ax).real
+
+
 def polar_roundtrip(x: np.ndarray) -> np.ndarray:
     """The reference's float32 polar round trip of every coefficient with nothing changed
     (filters_and_operators.py:383-391: log|k|, angle, exp(log) * exp(i angle), inverse `.real`): its

@@ -47,11 +47,15 @@ def test_conv3d_wgrad(conv, cin, cout, stride, shape, fast, monkeypatch):
 
 
 @pytest.mark.parametrize("cin,cout,shape", [(16, 16, (2, 12, 10, 40)), (32, 32, (1, 9, 13, 20)), (24, 40, (1, 7, 6, 16)),
-                                             (16, 16, (1, 3, 5, 8)), (16, 8, (2, 30, 6, 80)), (64, 64, (2, 5, 7, 12))])
+                                             (16, 16, (1, 3, 5, 8)), (16, 8, (2, 30, 6, 80)), (64, 64, (2, 5, 7, 12)),
+                                             # few channels: k_conv3d_wgrad_zf1 (rows (m, tz, ty), columns (c, tx))
+                                             (3, 3, (2, 12, 10, 40)), (3, 3, (1, 9, 7, 240)), (5, 2, (1, 6, 5, 16)),
+                                             (1, 1, (2, 5, 3, 8)), (4, 3, (1, 17, 11, 100))])
 def test_conv3d_wgrad_zmarch(conv, cin, cout, shape, monkeypatch):
     """Stride-1 layers of >= 8 channels and rows of 4k <= 80 floats take the z-marching kernel
-    (k_conv3d_wgrad_zm: one staged input plane meets a ring of three G planes); partial channel
-    tiles, a row block past H, z segments of unequal length."""
+    (k_conv3d_wgrad_zm: one staged input plane meets a ring of three G planes), those of <= 3 output and
+    <= 5 input channels its few-channel form (k_conv3d_wgrad_zf1); partial channel tiles, a row block
+    past H, z segments of unequal length."""
     monkeypatch.setattr(conv, "MIN_K_PER_OUTPUT", 1)
     torch.manual_seed(0)
     x = torch.randn((shape[0], cin) + shape[1:], device="cuda")

@@ -2,7 +2,8 @@
 (RandPlaneWaves_ellipsoid, filters_and_operators.py:370-393) and KSpaceSpikeNoise spikes (:906-983)
 against the full-spectrum passes (same program, tb_set_point_plans(0)) and the numpy oracle.
 
-Tolerances: closed form vs full passes max|d| / max|y| <= 2e-6; vs oracle <= 1e-5 (north_star), or
+Tolerances: closed form vs full passes and vs the float64 exact result (O.spikes_exact: the same
+replacements in a float64 spectrum) max|d| / max|y| <= 2e-6; vs oracle <= 1e-5 (north_star), or
 1.5x the reference's own polar round-trip floor where that is larger (its float32 log / angle / exp of
 EVERY coefficient moves a raw 240x240x155 volume by 1.4e-5 of max|x| against float64 -- no exact
 method can be closer to it than that; ``O.polar_roundtrip``); zero padding and min/max keys
@@ -173,3 +174,33 @@ def test_planes_closed_form_entry(rt):
     assert torch.equal(ya, yb) and torch.equal(mm_a, mm_b)
     with pytest.raises(rt.TexbiasError):
         rt.planes_closed_form(x, 3, [[K.wrap_op(0.5)]] * 2, 4)
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 240, 240, 155), (2, 3, 24, 20, 15), (1, 2, 31, 17, 30)])
+def test_closed_form_vs_float64_exact(rt, shape):
+    """The closed form against the float64 exact result of the same program (no polar round trip):
+    plane waves on sample 0, grouped per-channel spikes with a phase override on sample 1."""
+    torch.manual_seed(13)
+    x = torch.randn(shape, device="cuda")
+    sp = shape[2:]
+    C = shape[1]
+    s0 = [(tuple(int(n * f) for n, f in zip(sp, (0.8, 0.3, 0.65))), 13.0, None)]
+    s1 = [((0, 3, 4, 5), 11.0, None), ((C - 1, sp[0] - 4, 9, 2), 12.5, 0.3), ((0, 7, sp[1] - 2, sp[2] // 2), 10.0, None)]
+    sets = [s0, s1][: shape[0]]
+    progs = []
+    for ss in sets:
+        progs.append([spike(idx[-3:], sp, v, phase=ph, chan=idx[0] if len(idx) == 4 else -1,
+                            grouped=len(idx) == 4 and i > 0) for i, (idx, v, ph) in enumerate(ss)])
+    mm = torch.empty((shape[0], 2), dtype=torch.int32, device="cuda")
+    rt.set_pass_timing(True)
+    y = rt.kspace_filter(x, 3, progs, C, pad=2, minmax=mm)
+    _, _, _, names = rt.pass_stats()
+    rt.set_pass_timing(False)
+    torch.cuda.synchronize()
+    assert names[0] == "k_point_dft"
+    for b, ss in enumerate(sets):
+        ref = O.spikes_exact(x[b].double().cpu().numpy(), ss)
+        yb = y[b, ..., : sp[-1]].double().cpu().numpy()
+        err = np.abs(yb - ref).max() / np.abs(ref).max()
+        print(f"{shape} sample {b}: closed form vs float64 exact {err:.2e}")
+        assert err < 2e-6
