@@ -503,11 +503,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   const int Wo = a.Wo, Ho = a.Ho, Do = a.Do, Hi = a.Hi, Wi = a.Wi, Di = a.Di;
   const int GS = 32 * a.MS, XS = 16 * a.RX;
   float* gsl = smem;             // [2 slots][32 m][MS]: row yy at yy * Wo
-  // [5 slots][16 c][RX]: row r (input row 2 y0 - 1 + r) at r * PX, its even columns x = 2j at j and odd
-  // ones x = 2j + 1 at OB + j (OB = Wo + 2, zero at OB - 1 for x = -1): the stride-2 B reads of a wave
-  // then step by one float per lane (conflict-free at RX = 2 mod 32)
-  float* xsl = smem + 2 * GS;
-  const int OB = Wo + 2;
+  float* xsl = smem + 2 * GS;    // [5 slots][16 c][RX]: row r (input row 2 y0 - 1 + r) at r * PX, col x + 2
   const int tile = (int)blockIdx.y, mt = tile / a.ctiles, ct = tile - mt * a.ctiles;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
@@ -531,7 +527,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < cv && yi >= 0 && yi < Hi;
     xg[j] = ok ? (int)(((int64_t)c * Di) * iplane / 4 + (yi * Wi + 4 * q) / 4) : -1;
-    xl[j] = c * a.RX + r * a.PX + 2 * q;
+    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {  // (m, yy, q): output row y0 + yy
@@ -557,8 +553,9 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
-        *reinterpret_cast<float2*>(d + xl[j]) = make_float2(rx[j].x, rx[j].z);
-        *reinterpret_cast<float2*>(d + xl[j] + OB) = make_float2(rx[j].y, rx[j].w);
+        float2* p = reinterpret_cast<float2*>(d + xl[j]);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
       }
   };
   auto load_g = [&](int z) {
@@ -589,7 +586,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   const int li = lane & 15, lk = lane >> 4;
   const int mtl = wave & 1, par = wave >> 1;       // this wave's 16-row m-tile and k-step parity
   const int aoff = (16 * mtl + li) * a.MS + lk;    // A: G[m][x0 + lk]
-  const int boff = li * a.RX + lk;                 // B: X[c][row][2 (x0 + lk) + tx - 1] (even / odd halves)
+  const int boff = li * a.RX + 2 * lk + 1;         // B: X[c][row][2 (x0 + lk) + tx - 1] at col + 2
   f32x4 acc[27];
 #pragma unroll
   for (int j = 0; j < 27; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -618,8 +615,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
 #pragma unroll
         for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-          for (int tx = 0; tx < 3; ++tx)
-            bv[tz * 9 + ty * 3 + tx] = xp[tz][(2 * yy + ty) * a.PX + x0 + (tx == 1 ? 0 : OB - 1 + (tx >> 1))];
+          for (int tx = 0; tx < 3; ++tx) bv[tz * 9 + ty * 3 + tx] = xp[tz][(2 * yy + ty) * a.PX + 2 * x0 + tx];
     };
     auto mm = [&](float av, const float (&bv)[27]) {
 #pragma unroll
@@ -674,7 +670,7 @@ struct Zf2Args {
   float* dW;
   int N, M, Cc, Do, Ho, Wo, Di, Hi, Wi;
   int YB, nyb, ZS, zlen;
-  int MS, RX, PX, OB;  // OB: odd input columns' offset in a row (even ones at 0)
+  int MS, RX, PX;
   int mtiles;  // blocks of MT m-tiles
 };
 
@@ -687,11 +683,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
   const int Wo = a.Wo, Ho = a.Ho, Do = a.Do, Hi = a.Hi, Wi = a.Wi, Di = a.Di, Cc = a.Cc;
   const int GS = 16 * MT * a.MS, XS = Cc * a.RX;
   float* gsl = smem;             // [2 slots][16 MT m][MS]: row yy at yy * Wo
-  // [5 slots][Cc][RX]: row r (input row 2 y0 - 1 + r) at r * PX, even columns x = 2j at j, odd ones
-  // x = 2j + 1 at OB + j (zero at OB - 1 for x = -1): a wave's stride-2 B reads step one float per lane,
-  // conflict-free at RX = 6, OB = 4 or 30 (mod 32)
-  float* xsl = smem + 2 * GS;
-  const int OB = a.OB;
+  float* xsl = smem + 2 * GS;    // [5 slots][Cc][RX]: row r (input row 2 y0 - 1 + r) at r * PX, col x + 2
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -714,7 +706,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < Cc && yi >= 0 && yi < Hi;
     xg[j] = ok ? (int)(((int64_t)c * Di) * iplane / 4 + (yi * Wi + 4 * q) / 4) : -1;
-    xl[j] = c * a.RX + r * a.PX + 2 * q;
+    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {  // (m, yy, q)
@@ -741,8 +733,9 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
-        *reinterpret_cast<float2*>(d + xl[j]) = make_float2(rx[j].x, rx[j].z);
-        *reinterpret_cast<float2*>(d + xl[j] + OB) = make_float2(rx[j].y, rx[j].w);
+        float2* p = reinterpret_cast<float2*>(d + xl[j]);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
       }
   };
   auto load_g = [&](int z) {
@@ -771,8 +764,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 
   const int li = lane & 15, lk = lane >> 4;
   const int bc = li < 3 * Cc ? li / 3 : 0, btx = li < 3 * Cc ? li - 3 * (li / 3) : 0;
-  // B: X[c][row][2 (x0 + lk) + tx - 1]: even half for tx = 1, odd half (x0 + lk - 1 + tx / 2) otherwise
-  const int boff = bc * a.RX + (btx == 1 ? 0 : OB - 1 + (btx >> 1)) + lk;
+  const int boff = bc * a.RX + btx + 2 * lk + 1;  // B: X[c][row][2 (x0 + lk) + tx - 1] at col + 2
   f32x4 acc[MT][9];
 #pragma unroll
   for (int t = 0; t < MT; ++t)
@@ -802,7 +794,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 #pragma unroll
       for (int tz = 0; tz < 3; ++tz)
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty) bv[tz * 3 + ty] = xp[tz][(2 * yy + ty) * a.PX + x0];
+        for (int ty = 0; ty < 3; ++ty) bv[tz * 3 + ty] = xp[tz][(2 * yy + ty) * a.PX + 2 * x0];
     };
     auto mm = [&](const float (&av)[MT], const float (&bv)[9]) {
 #pragma unroll
@@ -845,7 +837,6 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
     atomicAdd(&a.dW[((int64_t)(m0 + m) * Cc + c) * 27 + j * 3 + tx], v);  // j = (tz, ty)
   }
 }
-
 
 // Stride 1, few channels (9 M <= 32, 3 Cc <= 16: the 3->3 full-resolution layer).  MFMA rows are
 // (m, tz, ty) -- 27 of two 16-row tiles at M = 3 -- and columns (c, tx), so one k-step of 4 output
@@ -1244,7 +1235,7 @@ bool use_zm2(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, 
 int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi,
               int Wi, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
-  a.PX = 2 * Wo + 2;  // even half 0 .. Wo - 1, odd half Wo + 2 .. 2 Wo + 1 (zeros at Wo, Wo + 1)
+  a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
   static const int yb_env = [] {
     const char* e = std::getenv("TEXBIAS_WGRAD_ZM2_YB");
     return e ? std::atoi(e) : 0;
@@ -1252,7 +1243,7 @@ int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do,
   a.YB = 0;
   for (int yb : {2, 1}) {  // two output rows per block where the ring fits: twice the MFMAs per staged plane
     if ((yb_env && yb != yb_env) || yb > Ho) continue;
-    for (int rem : {2, 4}) {  // X channel pitch mod 32: 2 (conflict-free B reads), 4 (tighter pad, 2-way)
+    for (int rem : {2, 4}) {  // X channel pitch mod 32: 2 (2-way B conflicts), 4 (tighter pad)
       const int rx = pad_mod32((2 * yb + 1) * a.PX, rem), ms = pad_mod32(yb * Wo, 2);
       const size_t ring = (size_t)4 * (2 * 32 * ms + 5 * 16 * rx), red = (size_t)4 * 2 * 27 * 4 * 64;
       const size_t need = ring > red ? ring : red;
@@ -1310,12 +1301,10 @@ int zf2_setup(Zf2Args& a, int& MT, size_t& lds, dim3& grid, int N, int M, int Cc
               int Hi, int Wi, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
   MT = M > 16 ? 2 : 1;
-  a.OB = Wo + 2;  // even, >= Wo + 1, = 4 or 30 (mod 32)
-  while ((a.OB & 31) != 4 && (a.OB & 31) != 30) a.OB += 2;
-  a.PX = a.OB + Wo;
+  a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
   a.YB = 0;
   for (int yb : {4, 2, 1}) {
-    const int rx = pad_mod32((2 * yb + 1) * a.PX, 6), ms = pad_mod32(yb * Wo, 2);
+    const int rx = pad_mod32((2 * yb + 1) * a.PX, 8), ms = pad_mod32(yb * Wo, 2);
     const size_t ring = (size_t)4 * (2 * 16 * MT * ms + 5 * Cc * rx), red = (size_t)4 * MT * 9 * 4 * 4 * 64;
     const size_t need = ring > red ? ring : red;
     if (need <= 163840) {

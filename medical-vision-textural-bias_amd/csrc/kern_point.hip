@@ -299,6 +299,170 @@ __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
   }
 }
 
+// Contiguous volume-channels (rows of D, slabs of W D, 16-B aligned, H W D % 4 == 0): the channel is
+// one flat array read as ALIGNED 16-B quads -- a row-relative quad of a 155-column row is only dword
+// aligned, and such reads ran at ~3 TB/s however many were in flight, as pass A''s aligned strip
+// loads do not.  A flat quad may straddle two rows: its elements past the row end take the next row's
+// twiddle (two partial sums S0, S1 per quad).  The D table is extended by 3 entries (tD[d] = tD[d - D]
+// past D) so a quad's four factors are consecutive whatever its start column.
+constexpr int PT_FQU = 4;
+
+struct FlatWalk {
+  static constexpr int STEP = PT_FQU * POINT_NT;  // quads per round
+  typedef float Vals[PT_FQU][4];
+  typedef int Codes[PT_FQU];
+  const float* xb;
+  int qb, qe, W, D;
+  int dd, dw, dh;  // 4 STEP elements = (dh W + dw) D + dd
+  struct State {
+    int lin[PT_FQU], h[PT_FQU], w[PT_FQU], d[PT_FQU];
+  };
+  __device__ __forceinline__ static FlatWalk make(const float* xb, int qb, int qe, int W, int D) {
+    FlatWalk k{xb, qb, qe, W, D, 0, 0, 0};
+    const int rows = 4 * STEP / D;
+    k.dd = 4 * STEP - rows * D;
+    k.dh = rows / W;
+    k.dw = rows - k.dh * W;
+    return k;
+  }
+  __device__ __forceinline__ void init(int q0, State& s) const {
+#pragma unroll
+    for (int u = 0; u < PT_FQU; ++u) {
+      const int l = q0 + u * POINT_NT, t = l < qe ? l : qb;
+      const int e = 4 * t, row = e / D, h = row / W;
+      s.lin[u] = l;
+      s.h[u] = h;
+      s.w[u] = row - h * W;
+      s.d[u] = e - row * D;
+    }
+  }
+  __device__ __forceinline__ void load(State& s, Vals& v, Codes& c) const {
+#pragma unroll
+    for (int u = 0; u < PT_FQU; ++u) {
+      const bool ok = s.lin[u] < qe;
+      const float4 q = *reinterpret_cast<const float4*>(xb + 4 * (ok ? s.lin[u] : qb));
+      v[u][0] = ok ? q.x : 0.f;
+      v[u][1] = ok ? q.y : 0.f;
+      v[u][2] = ok ? q.z : 0.f;
+      v[u][3] = ok ? q.w : 0.f;
+      c[u] = ok ? (s.h[u] << 20) | (s.w[u] << 10) | s.d[u] : -1;
+      s.lin[u] += STEP;
+      int d = s.d[u] + dd, w = s.w[u] + dw, h = s.h[u] + dh;
+      const bool cd = d >= D;
+      d -= cd ? D : 0;
+      w += cd ? 1 : 0;
+      const bool cw = w >= W;
+      w -= cw ? W : 0;
+      h += cw ? 1 : 0;
+      s.d[u] = d;
+      s.w[u] = w;
+      s.h[u] = h;
+    }
+  }
+  template <class F>
+  __device__ __forceinline__ void run(int tid, F&& body) const {  // three rounds: two in flight
+    State s;
+    init(qb + tid, s);
+    Vals va, vb, vc;
+    Codes ca, cb, cc;
+    load(s, va, ca);
+    load(s, vb, cb);
+    while (true) {
+      if (ca[0] < 0) break;
+      load(s, vc, cc);
+      body(va, ca);
+      if (cb[0] < 0) break;
+      load(s, va, ca);
+      body(vb, cb);
+      if (cc[0] < 0) break;
+      load(s, vb, cb);
+      body(vc, cc);
+    }
+  }
+};
+
+template <int NA>
+__global__ __launch_bounds__(POINT_NT) void k_point_dft_flat(PointArgs) {
+  const PointArgs& a = kargs<PointArgs>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int part = (int)blockIdx.x, bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
+  const int H = a.H, W = a.W, D = a.D, tid = (int)threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  __shared__ int act[PT_ACT];
+  point_active(a, bcl, act);
+  const int na = __builtin_amdgcn_readfirstlane(act[0]);
+  if (na == 0) return;
+  const int NQ = (D + 3) / 4, TQ = 4 * NQ, DX = D + 4;
+  double2* tDd = reinterpret_cast<double2*>(smem);                 // [namax][DX], extended
+  float2* tD = reinterpret_cast<float2*>(tDd + a.namax * DX);      // d-major [namax][TQ]
+  float2* tW = tD + a.namax * TQ;
+  float2* tH = tW + a.namax * W;
+  double* red = reinterpret_cast<double*>(tH + a.namax * H);       // [4 waves][TB_MAX_OPS][2]
+  point_tables<false>(act, na, H, W, D, NQ, -1.f, tD, tW, tH);
+  __syncthreads();
+  for (int t = tid; t < na * DX; t += POINT_NT) {
+    const int k = t / DX, d = t - k * DX;
+    const float2 f = tD[k * TQ + (d < D ? d : d - D)];
+    tDd[t] = make_double2((double)f.x, (double)f.y);
+  }
+  __syncthreads();
+  const int64_t nq = (int64_t)H * W * D / 4;
+  const FlatWalk fw = FlatWalk::make(a.x + (int64_t)bc * a.xsbc, (int)(nq * part / a.parts),
+                                     (int)(nq * (part + 1) / a.parts), W, D);
+  double accr[NA], acci[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) accr[k] = acci[k] = 0.0;
+  fw.run(tid, [&](const FlatWalk::Vals& v, const FlatWalk::Codes& cd) {
+#pragma unroll
+    for (int u = 0; u < PT_FQU; ++u) {
+      if (NA > 1 && cd[u] < 0) break;
+      int h, w, d0;
+      quad_decode(cd[u] < 0 ? 0 : cd[u], h, w, d0);  // past the range: the values are 0
+      const int w1 = w + 1 < W ? w + 1 : 0, h1r = w + 1 < W ? h : h + 1, h1 = h1r < H ? h1r : H - 1;
+#pragma unroll
+      for (int k = 0; k < NA; ++k) {
+        if (k >= na) break;
+        const double2* t = tDd + k * DX + d0;
+        double s0r = 0.0, s0i = 0.0, s1r = 0.0, s1i = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const double2 tj = t[j];
+          const bool nx = d0 + j >= D;  // this element is the next row's
+          const double x = (double)v[u][j], x0 = nx ? 0.0 : x, x1 = nx ? x : 0.0;
+          s0r = fma(x0, tj.x, s0r);
+          s0i = fma(x0, tj.y, s0i);
+          s1r = fma(x1, tj.x, s1r);
+          s1i = fma(x1, tj.y, s1i);
+        }
+        const float2 r0 = cmul(tW[k * W + w], tH[k * H + h]), r1 = cmul(tW[k * W + w1], tH[k * H + h1]);
+        accr[k] += s0r * (double)r0.x - s0i * (double)r0.y + s1r * (double)r1.x - s1i * (double)r1.y;
+        acci[k] += s0r * (double)r0.y + s0i * (double)r0.x + s1r * (double)r1.y + s1i * (double)r1.x;
+      }
+    }
+  });
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    if (k >= na) break;
+    const double vr = wave_sum(accr[k]), vi = wave_sum(acci[k]);
+    if (lane == 0) {
+      red[(wv * TB_MAX_OPS + k) * 2] = vr;
+      red[(wv * TB_MAX_OPS + k) * 2 + 1] = vi;
+    }
+  }
+  __syncthreads();
+  if (tid < na) {
+    const int k = tid;
+    double vr = 0.0, vi = 0.0;
+    for (int w = 0; w < POINT_NT / 64; ++w) {
+      vr += red[(w * TB_MAX_OPS + k) * 2];
+      vi += red[(w * TB_MAX_OPS + k) * 2 + 1];
+    }
+    double* o = a.part + ((int64_t)(bcl * a.parts + part) * TB_MAX_OPS + act[4 + 4 * k]) * 2;
+    o[0] = vr;
+    o[1] = vi;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_point_delta(PointArgs) {
   const PointArgs& a = kargs<PointArgs>();
   const int bcl = (int)blockIdx.x, lane = (int)threadIdx.x;
@@ -480,8 +644,16 @@ bool point_program(const tb_sample_ops& s, int H, int W, int D) {
 static size_t point_lds(const PointArgs& a, int stage) {
   const int tq = stage == 0 ? 4 * ((a.D + 3) / 4) : 4 * ((a.D + a.ypad + 3) / 4);
   const size_t tabs = (size_t)a.namax * (tq + a.W + a.H) * sizeof(float2);
-  return stage == 0 ? (size_t)a.namax * tq * sizeof(double2) + tabs + 4 * TB_MAX_OPS * 2 * sizeof(double)
+  const int dx = a.flat ? a.D + 4 : tq;  // the flat kernel's float64 D table is extended by 4
+  return stage == 0 ? (size_t)a.namax * dx * sizeof(double2) + tabs + 4 * TB_MAX_OPS * 2 * sizeof(double)
                     : tabs + 2 * POINT_NT / 64 * sizeof(float);
+}
+
+typedef void (*PointKern)(PointArgs);
+
+static PointKern point_dft_kernel(const PointArgs& a) {
+  if (a.flat) return k_point_dft_flat<1>;  // one spike per volume-channel (point_grid)
+  return a.namax == 1 ? k_point_dft<1> : k_point_dft<TB_MAX_OPS>;
 }
 
 template <class K>
@@ -507,8 +679,12 @@ static int point_parts(K kern, size_t lds, int nbc, int ncu) {
 }
 
 void point_grid(PointArgs& a, int ncu) {
+  // contiguous, aligned volume-channels: the DFT reads them as flat arrays of aligned quads
+  const int64_t vol = (int64_t)a.H * a.W * a.D;
+  a.flat = a.namax == 1 && a.xsw == a.D && a.xsh == (int64_t)a.W * a.D && vol % 4 == 0 && vol / 4 < ((int64_t)1 << 31) &&
+           a.xsbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 && a.D < 1024;
   // occupancy is queried at the launch's LDS size
-  const auto kd = a.namax == 1 ? k_point_dft<1> : k_point_dft<TB_MAX_OPS>;
+  const PointKern kd = point_dft_kernel(a);
   const auto ka = a.namax == 1 ? k_point_apply<1> : k_point_apply<TB_MAX_OPS>;
   (void)allow_lds(kd, point_lds(a, 0));
   a.parts = point_parts(kd, point_lds(a, 0), a.nbc, ncu);
@@ -518,7 +694,7 @@ void point_grid(PointArgs& a, int ncu) {
 
 hipError_t launch_point(const PointArgs& a, hipStream_t st, int stage) {
   if (stage == 0) {
-    const auto kd = a.namax == 1 ? k_point_dft<1> : k_point_dft<TB_MAX_OPS>;
+    const PointKern kd = point_dft_kernel(a);
     const hipError_t e = allow_lds(kd, point_lds(a, 0));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kd, dim3(a.parts, a.nbc), dim3(POINT_NT), point_lds(a, 0), st, a);

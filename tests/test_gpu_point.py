@@ -71,7 +71,7 @@ def test_planes_closed_form(rt, shape):
     idxs = [tuple(int(n * f) for n, f in zip(sp, (0.8, 0.3, 0.65))), tuple(int(n * 0.15) + 1 for n in sp)]
     progs = [[spike(idxs[b % 2], sp, 12.0 + b)] for b in range(shape[0])]
     yp, yf, names, mmp, mmf = both(rt, x, progs, shape[1], pad=5)
-    assert names[0] == "k_point_dft" and names[2] == "k_point_apply"
+    assert names[0].startswith("k_point_dft") and names[2] == "k_point_apply"
     assert torch.all(yp[..., sp[-1]:] == 0)
     assert (yp - yf).abs().max().item() / yf.abs().max().item() < 2e-6
     check_keys(rt, yp, mmp, sp[-1])
@@ -100,7 +100,7 @@ def test_planes_special_frequencies(rt, where):
         idx, phase = (5, 7, 3), 0.7
     progs = [[spike(idx, sp, 9.0, phase=phase)] for _ in range(2)]
     yp, yf, names, mmp, _ = both(rt, x, progs, 3)
-    assert names[0] == "k_point_dft"
+    assert names[0].startswith("k_point_dft")
     assert (yp - yf).abs().max().item() / yf.abs().max().item() < 2e-6
     check_keys(rt, yp, mmp, sp[-1])
     ref = O.plane_waves(x[1].cpu().numpy(), idx, 9.0, phase=None if phase is None else [phase] * 3)
@@ -119,7 +119,7 @@ def test_kspace_spike_groups_and_channels(rt):
     p0 = [spike(l[1:], sp, v, chan=l[0], grouped=i > 0) for i, (l, v) in enumerate(zip(locs, vals))]
     p1 = [spike((9, 9, 9), sp, 13.0)]
     yp, yf, names, mmp, _ = both(rt, x, [p0, p1], 4, pad=3)
-    assert names[0] == "k_point_dft"
+    assert names[0].startswith("k_point_dft")
     assert (yp - yf).abs().max().item() / yf.abs().max().item() < 2e-6
     check_keys(rt, yp, mmp, sp[-1])
     ref = O.kspace_spike(x[0].cpu().numpy(), locs, vals)
@@ -140,7 +140,7 @@ def test_touching_spikes_take_full_route(rt):
     rt.kspace_filter(x, 3, prog, 2)
     _, _, _, names = rt.pass_stats()
     rt.set_pass_timing(False)
-    assert names[0] != "k_point_dft"
+    assert not names[0].startswith("k_point_dft")
 
 
 def test_planes_in_place_strided(rt):
@@ -197,7 +197,7 @@ def test_closed_form_vs_float64_exact(rt, shape):
     _, _, _, names = rt.pass_stats()
     rt.set_pass_timing(False)
     torch.cuda.synchronize()
-    assert names[0] == "k_point_dft"
+    assert names[0].startswith("k_point_dft")
     for b, ss in enumerate(sets):
         ref = O.spikes_exact(x[b].double().cpu().numpy(), ss)
         yb = y[b, ..., : sp[-1]].double().cpu().numpy()
