@@ -833,44 +833,61 @@ static int run_generic(const tb_plan* p, const float* x, const int64_t* xs, floa
   return TB_OK;
 }
 
+// Samples per chain of the closed-form route's three launches (TEXBIAS_POINT_CHUNK, 0 = the whole
+// launch group): per-sample chains would let k_point_apply re-read a 142 MB sample from the Infinity
+// Cache, but cost more in launches and smaller grids than they saved.
+static int point_chunk(const tb_plan* p, int C) {
+  static const int env = [] {
+    const char* e = std::getenv("TEXBIAS_POINT_CHUNK");
+    return e ? std::atoi(e) : -1;
+  }();
+  (void)p;
+  (void)C;
+  return env >= 0 ? env : 0;  // measured: one sample per chain 0.240 vs 0.213 ms per C3 step (planes)
+}
+
 static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,
                      char* ws, int b0, int nb, int C, const tb_sample_ops* ops, uint32_t* minmax,
                      hipStream_t st) {
   const int H = p->dev.H, W = p->dev.W, D = p->dev.D;
-  const int nbc = nb * C;
-  tb::PointArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.H = H, a.W = W, a.D = D;
-  a.x = x, a.xsbc = xs[0], a.xsh = xs[1], a.xsw = xs[2];
-  a.y = y, a.ysbc = ys[0], a.ysh = ys[1], a.ysw = ys[2];
-  a.ypad = y_pad, a.bc0 = b0 * C, a.C = C, a.nbc = nbc, a.mm = minmax;
-  const tb::PointWs wl = tb::point_ws(nbc);
-  a.part = reinterpret_cast<double*>(ws + wl.part);
-  a.delta = reinterpret_cast<float*>(ws + wl.delta);
-  a.mmp = reinterpret_cast<float2*>(ws + wl.mmp);
-  a.cnt = reinterpret_cast<uint32_t*>(ws + wl.cnt);
-  a.namax = 1;
-  for (int i = 0; i < nb; ++i) {
-    a.ops.s[i] = ops[b0 + i];
-    for (int c = 0; c < C; ++c) {
-      int n = 0;
-      for (int o = 0; o < ops[b0 + i].n; ++o) n += ops[b0 + i].op[o].chan < 0 || ops[b0 + i].op[o].chan == c;
-      a.namax = n > a.namax ? n : a.namax;
+  const int cs = point_chunk(p, C) > 0 ? point_chunk(p, C) : nb;
+  for (int s0 = 0; s0 < nb; s0 += cs) {
+    const int ns = nb - s0 < cs ? nb - s0 : cs, sb = b0 + s0;
+    const int nbc = ns * C;
+    tb::PointArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.H = H, a.W = W, a.D = D;
+    a.x = x, a.xsbc = xs[0], a.xsh = xs[1], a.xsw = xs[2];
+    a.y = y, a.ysbc = ys[0], a.ysh = ys[1], a.ysw = ys[2];
+    a.ypad = y_pad, a.bc0 = sb * C, a.C = C, a.nbc = nbc, a.mm = minmax;
+    const tb::PointWs wl = tb::point_ws(nbc);
+    a.part = reinterpret_cast<double*>(ws + wl.part);
+    a.delta = reinterpret_cast<float*>(ws + wl.delta);
+    a.mmp = reinterpret_cast<float2*>(ws + wl.mmp);
+    a.cnt = reinterpret_cast<uint32_t*>(ws + wl.cnt);
+    a.namax = 1;
+    for (int i = 0; i < ns; ++i) {
+      a.ops.s[i] = ops[sb + i];
+      for (int c = 0; c < C; ++c) {
+        int n = 0;
+        for (int o = 0; o < ops[sb + i].n; ++o) n += ops[sb + i].op[o].chan < 0 || ops[sb + i].op[o].chan == c;
+        a.namax = n > a.namax ? n : a.namax;
+      }
     }
-  }
-  tb::point_grid(a, p->ncu);
-  const double vox = (double)nbc * H * W * D;
-  {
-    Timer t(0, st, vox * 4.0, a.flat ? "k_point_dft_flat" : "k_point_dft");
-    TB_HIP(tb::launch_point(a, st, 0));
-  }
-  {
-    Timer t(1, st, (double)nbc * a.parts * TB_MAX_OPS * 16.0, "k_point_delta");
-    TB_HIP(tb::launch_point(a, st, 1));
-  }
-  {
-    Timer t(2, st, vox * 4.0 + (double)nbc * H * W * (D + y_pad) * 4.0, "k_point_apply");
-    TB_HIP(tb::launch_point(a, st, 2));
+    tb::point_grid(a, p->ncu);
+    const double vox = (double)nbc * H * W * D;
+    {
+      Timer t(0, st, vox * 4.0, a.flat ? "k_point_dft_flat" : "k_point_dft");
+      TB_HIP(tb::launch_point(a, st, 0));
+    }
+    {
+      Timer t(1, st, (double)nbc * a.parts * TB_MAX_OPS * 16.0, "k_point_delta");
+      TB_HIP(tb::launch_point(a, st, 1));
+    }
+    {
+      Timer t(2, st, vox * 4.0 + (double)nbc * H * W * (D + y_pad) * 4.0, "k_point_apply");
+      TB_HIP(tb::launch_point(a, st, 2));
+    }
   }
   return TB_OK;
 }
