@@ -299,190 +299,6 @@ __global__ __launch_bounds__(POINT_NT) void k_point_dft(PointArgs) {
   }
 }
 
-// Contiguous volume-channels (rows of D, slabs of W D, 16-B aligned, H W D % 4 == 0): the channel is
-// one flat array of aligned 16-B quads, streamed by LDS-DMA (global_load_lds_dwordx4) into a 4-slot
-// ring per wave, three rounds in flight.  Register-staged rounds did not stay in flight: hipcc put an
-// s_waitcnt vmcnt(0) at the loop head (the loaded registers are loop-carried), so every round paid a
-// full HBM round trip.  The ring's reads are inline-asm ds_reads (the compiler drains vmcnt before any
-// LDS read while an LDS-DMA is in flight); the wave counts its own DMAs (vmcnt(12)).  A flat quad may
-// straddle two rows: its elements past the row end take the next row's twiddle.
-constexpr int PT_FQU = 4;   // DMA instructions (64 quads each) per wave and round
-constexpr int PT_RING = 4;  // ring slots per wave (rounds in flight + the one being read)
-
-struct FlatWalk {
-  static constexpr int STEP = PT_FQU * POINT_NT;  // quads per round of the workgroup
-  int qb, qe, W, D;
-  int dd, dw, dh;  // 4 STEP elements = (dh W + dw) D + dd
-  struct State {
-    int lin[PT_FQU], h[PT_FQU], w[PT_FQU], d[PT_FQU];
-  };
-  __device__ __forceinline__ static FlatWalk make(int qb, int qe, int W, int D) {
-    FlatWalk k{qb, qe, W, D, 0, 0, 0};
-    const int rows = 4 * STEP / D;
-    k.dd = 4 * STEP - rows * D;
-    k.dh = rows / W;
-    k.dw = rows - k.dh * W;
-    return k;
-  }
-  // slot u of thread tid: quad qb + u POINT_NT + tid (a wave's 64 lanes: 64 consecutive quads)
-  __device__ __forceinline__ void init(int tid, State& s) const {
-#pragma unroll
-    for (int u = 0; u < PT_FQU; ++u) {
-      const int l = qb + u * POINT_NT + tid, t = l < qe ? l : qb;
-      const int e = 4 * t, row = e / D, h = row / W;
-      s.lin[u] = l;
-      s.h[u] = h;
-      s.w[u] = row - h * W;
-      s.d[u] = e - row * D;
-    }
-  }
-  __device__ __forceinline__ void advance(State& s) const {
-#pragma unroll
-    for (int u = 0; u < PT_FQU; ++u) {
-      s.lin[u] += STEP;
-      int d = s.d[u] + dd, w = s.w[u] + dw, h = s.h[u] + dh;
-      const bool cd = d >= D;
-      d -= cd ? D : 0;
-      w += cd ? 1 : 0;
-      const bool cw = w >= W;
-      w -= cw ? W : 0;
-      h += cw ? 1 : 0;
-      s.d[u] = d;
-      s.w[u] = w;
-      s.h[u] = h;
-    }
-  }
-};
-
-// One spike per volume-channel.  Per quad the four D factors come from a table split by d mod 4
-// (tq[d & 3][d >> 2]: a wave's consecutive quads then read consecutive entries), the two partial sums
-// are float32 (four terms) and the accumulation over the channel float64.  A DC spike (kd = 0: every D
-// factor exactly 1) sums the quads in float64 outright, so a zero-mean channel's DC keeps the sign of
-// its exact sum as the reference's FFT does (the golden DC fixture).
-__global__ __launch_bounds__(POINT_NT) void k_point_dft_flat(PointArgs) {
-  const PointArgs& a = kargs<PointArgs>();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int part = (int)blockIdx.x, bcl = (int)blockIdx.y, bc = a.bc0 + bcl;
-  const int H = a.H, W = a.W, D = a.D, tid = (int)threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  __shared__ int act[PT_ACT];
-  point_active(a, bcl, act);
-  const int na = __builtin_amdgcn_readfirstlane(act[0]);
-  if (na == 0) return;
-  const int NQ = (D + 3) / 4, TQ = 4 * NQ, NX = (D + 4 + 3) / 4;
-  float4* ring = reinterpret_cast<float4*>(smem);  // [4 waves][PT_RING][PT_FQU][64 lanes]
-  float2* tq = reinterpret_cast<float2*>(ring + 4 * PT_RING * PT_FQU * 64);  // [4][NX]
-  float2* tD = tq + 4 * NX;                      // d-major [TQ] (point_tables)
-  float2* tW = tD + TQ;
-  float2* tH = tW + W;
-  double* red = reinterpret_cast<double*>(tH + H);  // [4 waves][2]
-  const int64_t nq = (int64_t)H * W * D / 4;
-  const FlatWalk fw = FlatWalk::make((int)(nq * part / a.parts), (int)(nq * (part + 1) / a.parts), W, D);
-  const float* xb = a.x + (int64_t)bc * a.xsbc;
-  FlatWalk::State si;
-  fw.init(tid, si);
-  float4* wring = ring + wv * PT_RING * PT_FQU * 64;
-  auto issue = [&](int slot) {
-#pragma unroll
-    for (int u = 0; u < PT_FQU; ++u) {
-      const int q = si.lin[u] < fw.qe ? si.lin[u] : fw.qb;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(xb + 4 * (int64_t)q),
-                                       (__attribute__((address_space(3))) void*)(wring + (slot * PT_FQU + u) * 64),
-                                       16, 0, 0);
-    }
-    fw.advance(si);
-  };
-  point_tables<false>(act, 1, H, W, D, NQ, -1.f, tD, tW, tH);
-  __syncthreads();
-  for (int t = tid; t < 4 * NX; t += POINT_NT) {
-    const int j = t / NX, d = 4 * (t - j * NX) + j;
-    tq[t] = d < D + 4 ? tD[d < D ? d : d - D] : make_float2(0.f, 0.f);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < PT_RING - 1; ++r) issue(r);
-  const bool dc = __builtin_amdgcn_readfirstlane(act[3]) == 0;  // kd = 0
-  FlatWalk::State su;
-  fw.init(tid, su);
-  double accr = 0.0, acci = 0.0;
-  for (int r = 0; su.lin[0] < fw.qe; ++r) {
-    issue((r + PT_RING - 1) & (PT_RING - 1));
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // this round's PT_FQU DMAs have landed
-    const int slot = r & (PT_RING - 1);
-#pragma unroll
-    for (int u = 0; u < PT_FQU; ++u) {
-      const bool ok = su.lin[u] < fw.qe;
-      const int h = su.h[u], w = su.w[u], d0 = su.d[u];
-      const int hc = h < H ? h : H - 1;
-      const int w1 = w + 1 < W ? w + 1 : 0, h1r = w + 1 < W ? hc : hc + 1, h1 = h1r < H ? h1r : H - 1;
-      // every LDS read of the quad in one asm block (ring quad, 4 D factors, 2 row twiddles): LDS reads
-      // the compiler sees would each be preceded by a vmcnt(0) drain of the ring's DMAs
-      float4 q4;
-      float2 t0, t1, t2, t3, wa, ha, wb, hb;
-      const unsigned lq = (unsigned)(uintptr_t)(wring + (slot * PT_FQU + u) * 64 + lane);
-      const unsigned l0 = (unsigned)(uintptr_t)(tq + ((d0 + 0) & 3) * NX + ((d0 + 0) >> 2));
-      const unsigned l1 = (unsigned)(uintptr_t)(tq + ((d0 + 1) & 3) * NX + ((d0 + 1) >> 2));
-      const unsigned l2 = (unsigned)(uintptr_t)(tq + ((d0 + 2) & 3) * NX + ((d0 + 2) >> 2));
-      const unsigned l3 = (unsigned)(uintptr_t)(tq + ((d0 + 3) & 3) * NX + ((d0 + 3) >> 2));
-      const unsigned lwa = (unsigned)(uintptr_t)(tW + w), lha = (unsigned)(uintptr_t)(tH + hc);
-      const unsigned lwb = (unsigned)(uintptr_t)(tW + w1), lhb = (unsigned)(uintptr_t)(tH + h1);
-      asm volatile(
-          "ds_read_b128 %0, %9\n ds_read_b64 %1, %10\n ds_read_b64 %2, %11\n ds_read_b64 %3, %12\n"
-          " ds_read_b64 %4, %13\n ds_read_b64 %5, %14\n ds_read_b64 %6, %15\n ds_read_b64 %7, %16\n"
-          " ds_read_b64 %8, %17\n s_waitcnt lgkmcnt(0)"
-          : "=&v"(q4), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(wa), "=&v"(ha), "=&v"(wb), "=&v"(hb)
-          : "v"(lq), "v"(l0), "v"(l1), "v"(l2), "v"(l3), "v"(lwa), "v"(lha), "v"(lwb), "v"(lhb));
-      const float v[4] = {ok ? q4.x : 0.f, ok ? q4.y : 0.f, ok ? q4.z : 0.f, ok ? q4.w : 0.f};
-      const float2 tjs[4] = {t0, t1, t2, t3};
-      const float2 r0 = cmul(wa, ha), r1 = cmul(wb, hb);
-      double s0r, s0i, s1r, s1i;
-      if (dc) {  // wave-uniform
-        double t0 = 0.0, t1 = 0.0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool nx = d0 + j >= D;  // this element is the next row's
-          t0 += nx ? 0.0 : (double)v[j];
-          t1 += nx ? (double)v[j] : 0.0;
-        }
-        s0r = t0, s0i = 0.0, s1r = t1, s1i = 0.0;
-      } else {
-        float p0r = 0.f, p0i = 0.f, p1r = 0.f, p1i = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float2 tj = tjs[j];
-          const bool nx = d0 + j >= D;
-          const float x0 = nx ? 0.f : v[j], x1 = nx ? v[j] : 0.f;
-          p0r = fmaf(x0, tj.x, p0r);
-          p0i = fmaf(x0, tj.y, p0i);
-          p1r = fmaf(x1, tj.x, p1r);
-          p1i = fmaf(x1, tj.y, p1i);
-        }
-        s0r = p0r, s0i = p0i, s1r = p1r, s1i = p1i;
-      }
-      accr += s0r * (double)r0.x - s0i * (double)r0.y + s1r * (double)r1.x - s1i * (double)r1.y;
-      acci += s0r * (double)r0.y + s0i * (double)r0.x + s1r * (double)r1.y + s1i * (double)r1.x;
-    }
-    fw.advance(su);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
-  const double vr = wave_sum(accr), vi = wave_sum(acci);
-  if (lane == 0) {
-    red[wv * 2] = vr;
-    red[wv * 2 + 1] = vi;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double sr = 0.0, si2 = 0.0;
-    for (int w = 0; w < POINT_NT / 64; ++w) {
-      sr += red[w * 2];
-      si2 += red[w * 2 + 1];
-    }
-    double* o = a.part + ((int64_t)(bcl * a.parts + part) * TB_MAX_OPS + act[4]) * 2;
-    o[0] = sr;
-    o[1] = si2;
-  }
-}
-
 __global__ __launch_bounds__(64) void k_point_delta(PointArgs) {
   const PointArgs& a = kargs<PointArgs>();
   const int bcl = (int)blockIdx.x, lane = (int)threadIdx.x;
@@ -664,9 +480,6 @@ bool point_program(const tb_sample_ops& s, int H, int W, int D) {
 static size_t point_lds(const PointArgs& a, int stage) {
   const int tq = stage == 0 ? 4 * ((a.D + 3) / 4) : 4 * ((a.D + a.ypad + 3) / 4);
   const size_t tabs = (size_t)a.namax * (tq + a.W + a.H) * sizeof(float2);
-  if (stage == 0 && a.flat)  // one spike: the DMA ring, the split D table (D + 4 entries), the float tables
-    return (size_t)4 * PT_RING * PT_FQU * 64 * 16 + (size_t)(4 * ((a.D + 7) / 4) + tq + a.W + a.H) * sizeof(float2) +
-           4 * 2 * sizeof(double);
   return stage == 0 ? (size_t)a.namax * tq * sizeof(double2) + tabs + 4 * TB_MAX_OPS * 2 * sizeof(double)
                     : tabs + 2 * POINT_NT / 64 * sizeof(float);
 }
@@ -674,7 +487,6 @@ static size_t point_lds(const PointArgs& a, int stage) {
 typedef void (*PointKern)(PointArgs);
 
 static PointKern point_dft_kernel(const PointArgs& a) {
-  if (a.flat) return k_point_dft_flat;  // one spike per volume-channel (point_grid)
   return a.namax == 1 ? k_point_dft<1> : k_point_dft<TB_MAX_OPS>;
 }
 
@@ -701,10 +513,6 @@ static int point_parts(K kern, size_t lds, int nbc, int ncu) {
 }
 
 void point_grid(PointArgs& a, int ncu) {
-  // contiguous, aligned volume-channels: the DFT reads them as flat arrays of aligned quads
-  const int64_t vol = (int64_t)a.H * a.W * a.D;
-  a.flat = a.namax == 1 && a.xsw == a.D && a.xsh == (int64_t)a.W * a.D && vol % 4 == 0 && vol / 4 < ((int64_t)1 << 31) &&
-           a.xsbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 && a.D < 1024;
   // occupancy is queried at the launch's LDS size
   const PointKern kd = point_dft_kernel(a);
   const auto ka = a.namax == 1 ? k_point_apply<1> : k_point_apply<TB_MAX_OPS>;

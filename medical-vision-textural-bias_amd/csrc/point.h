@@ -27,7 +27,6 @@ struct PointArgs {
   int ypad, bc0, C, nbc;  // bc0 = first sample * C (absolute); ops.s[i] = the run's i-th sample
   int parts;              // workgroups per volume-channel (each a contiguous range of the volume's quads)
   int parts_apply;        // the same for k_point_apply (its own occupancy)
-  int flat;               // k_point_dft reads each volume-channel as one aligned flat array (point_grid)
   int namax;              // most spikes any volume-channel of the launch has (twiddle-table stride)
   uint32_t* mm;           // per-sample min/max keys (written by the last apply workgroup) or null
   double* part;           // [nbc][parts][TB_MAX_OPS][2] per-workgroup coefficient sums

@@ -877,7 +877,7 @@ static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float*
     tb::point_grid(a, p->ncu);
     const double vox = (double)nbc * H * W * D;
     {
-      Timer t(0, st, vox * 4.0, a.flat ? "k_point_dft_flat" : "k_point_dft");
+      Timer t(0, st, vox * 4.0, "k_point_dft");
       TB_HIP(tb::launch_point(a, st, 0));
     }
     {
