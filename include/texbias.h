@@ -212,6 +212,23 @@ int tb_conv3d_small_f32(const float* x, const float* w, const float* b, float* y
                         int H, int W, void* stream);
 
 /*
+ * The U-Net's full-resolution stride-2 layers with few channels on one side (csrc/conv_up.hip; the
+ * train step of 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-243, MONAI UNet entry and exit):
+ * tb_conv3d_s2_fewin_f32: out[n][m][o] = bias[m] + sum_{c < Cin, t} Wm[m][c][t] in[n][c][2 o + t - 1]
+ *   (3x3x3, stride 2, padding 1; in [N][Cin][2 Do][2 Ho][2 Wo], out [N][Mout][Do][Ho][Wo]; Cin <= 4,
+ *   Mout 16 or 32, 3 Wo <= 256), K = Wm as output-channel pairs: K[m / 2][c][t][m % 2].  Serves
+ *   Conv3d(4 -> 16, s2)'s forward (Wm = its weight) and ConvTranspose3d(32 -> 3, s2)'s input gradient
+ *   (in = dY, Wm = the transposed conv's [32][3][27] weight).
+ * tb_convT3d_fewout_f32: ConvTranspose3d(Cin -> Mout, kernel 3, stride 2, padding 1, output_padding 1)
+ *   forward, x [N][Cin][Di][Hi][Wi] -> y [N][Mout][2 Di][2 Hi][2 Wi], W = [Cin][Mout][3][3][3] as the
+ *   module holds it; Mout <= 4, Cin <= 32, Wi % 4 == 0, Wi <= 128.  bias may be NULL for both.
+ */
+int tb_conv3d_s2_fewin_f32(const float* in, const float* K, const float* bias, float* out, int N, int Cin, int Mout,
+                           int Do, int Ho, int Wo, void* stream);
+int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, float* y, int N, int Cin, int Mout, int Di,
+                          int Hi, int Wi, void* stream);
+
+/*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
  * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution
  * (MONAI Convolution, used by 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-199).

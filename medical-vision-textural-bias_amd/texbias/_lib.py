@@ -47,6 +47,8 @@ def _proto(L):
         "tb_instnorm_prelu_bwd_f32": (I, [P, P, P, P, P, P, P, I64, I64, P, SZ, P]),
         "tb_channel_sum_f32": (I, [P, P, I64, I64, I64, P]),
         "tb_conv3d_small_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
+        "tb_conv3d_s2_fewin_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
+        "tb_convT3d_fewout_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
         "tb_dice_sums_f32": (I, [P, P, P, I64, I64, I, I, P]),
         "tb_dice_sums_bwd_f32": (I, [P, P, P, P, I64, I64, I, I, P]),
         "tb_dice_metric_sums_f32": (I, [P, P, P, I64, I64, P]),

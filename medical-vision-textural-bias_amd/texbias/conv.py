@@ -177,8 +177,119 @@ class _SmallConvFn(torch.autograd.Function):
         return gx, gw, gb
 
 
+# ---------------------------------------------------------------- full-resolution stride-2 layers
+def s2_pairs(wm: torch.Tensor) -> torch.Tensor:
+    """[Mout, Cin, 3, 3, 3] -> the kernel's output-channel pairs [Mout / 2, Cin 27, 2]."""
+    m = wm.shape[0]
+    return wm.reshape(m // 2, 2, -1).permute(0, 2, 1).contiguous()
+
+
+def conv_s2_fewin(inp: torch.Tensor, K: torch.Tensor, b, mout: int) -> torch.Tensor:
+    """out[n][m][o] = b[m] + sum_{c, t} Wm[m][c][t] inp[n][c][2 o + t - 1] (3x3x3, stride 2, padding 1;
+    tb_conv3d_s2_fewin_f32).  inp [N, Cin <= 4, 2 Do, 2 Ho, 2 Wo], K = s2_pairs(Wm)."""
+    inp = inp.contiguous()
+    N, Cin, Di, Hi, Wi = inp.shape
+    out = torch.empty((N, mout, Di // 2, Hi // 2, Wi // 2), dtype=torch.float32, device=inp.device)
+    with torch.cuda.device(inp.device):
+        check(lib().tb_conv3d_s2_fewin_f32(inp.data_ptr(), K.data_ptr(), b.data_ptr() if b is not None else None,
+                                           out.data_ptr(), N, Cin, mout, Di // 2, Hi // 2, Wi // 2, _stream(inp)),
+              "tb_conv3d_s2_fewin_f32")
+    return out
+
+
+def convT_fewout(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+    """ConvTranspose3d(Cin -> Cout <= 4, 3, stride 2, padding 1, output_padding 1) forward
+    (tb_convT3d_fewout_f32; w as the module holds it, [Cin, Cout, 3, 3, 3])."""
+    x = x.contiguous()
+    N, Cin, D, H, W = x.shape
+    Cout = w.shape[1]
+    y = torch.empty((N, Cout, 2 * D, 2 * H, 2 * W), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device):
+        check(lib().tb_convT3d_fewout_f32(x.data_ptr(), w.contiguous().data_ptr(),
+                                          b.data_ptr() if b is not None else None, y.data_ptr(), N, Cin, Cout, D, H,
+                                          W, _stream(x)), "tb_convT3d_fewout_f32")
+    return y
+
+
+def _s2_shape_ok(spatial) -> bool:
+    D, H, W = spatial
+    return D % 2 == 0 and H % 2 == 0 and W % 4 == 0 and W <= 160  # (the weight gradient's z-march: W <= 160)
+
+
+def s2_fewin_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
+    """Conv3d(Cin <= 4 -> 16 or 32, 3, stride 2, padding 1) on even spatial dims: k_conv_s2_fewin."""
+    return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and \
+        tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and w.shape[1] <= 4 and \
+        w.shape[0] in (16, 32) and _s2_shape_ok(x.shape[2:]) and x.data_ptr() % 16 == 0
+
+
+def convT_fewout_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, output_padding) -> bool:
+    """ConvTranspose3d(Cin <= 32 -> Cout <= 4, 3, 2, 1, output_padding 1): forward on k_convT_fewout and
+    input gradient on k_conv_s2_fewin (needs Cin 16 or 32)."""
+    return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and \
+        tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and tuple(output_padding) == (1, 1, 1) and \
+        w.shape[1] <= 4 and w.shape[0] in (16, 32) and x.shape[-1] % 4 == 0 and x.shape[-1] <= 80 and \
+        _s2_shape_ok(tuple(2 * n for n in x.shape[2:]))
+
+
+class _ConvS2FewInFn(torch.autograd.Function):
+    """Conv3d(Cin <= 4, stride 2): forward on the direct stride-2 kernel; weight gradient on the
+    z-marching MFMA kernel, bias gradient on the channel-sum kernel, input gradient (rarely needed:
+    the first layer's input is data) on ATen."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = conv_s2_fewin(x, s2_pairs(w), b, w.shape[0])
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx, _, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [2, 2, 2], [1, 1, 1], [1, 1, 1], False,
+                                                           [0, 0, 0], 1, [True, False, False])
+        if ctx.needs_input_grad[1]:
+            gw = wgrad(gy, x, w.shape, 2, 1)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = channel_sum(gy)
+        return gx, gw, gb
+
+
+class _ConvTFewOutFn(torch.autograd.Function):
+    """ConvTranspose3d(Cin -> Cout <= 4, stride 2): forward on the sub-pixel kernel, input gradient (a
+    stride-2 convolution of dY with Cout input channels) on the direct stride-2 kernel, weight gradient
+    on the z-marching MFMA kernel, bias gradient on the channel-sum kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = convT_fewout(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:  # dX[m][i] = sum_{c, t} W[m][c][t] dY[c][2 i + t - 1]
+            gx = conv_s2_fewin(gy, s2_pairs(w), None, w.shape[0])
+        if ctx.needs_input_grad[1]:  # dW[ci][co] = corr(x, dY)
+            gw = wgrad(x, gy, w.shape, 2, 1)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = channel_sum(gy)
+        return gx, gw, gb
+
+
 class Conv3d(nn.Conv3d):
     def forward(self, x):
+        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
+                s2_fewin_applies(x, self.weight, self.stride, self.padding):
+            return _ConvS2FewInFn.apply(x, self.weight, self.bias)
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
                 small_conv_applies(x, self.weight, self.stride, self.padding):
             return _SmallConvFn.apply(x, self.weight, self.bias)
@@ -193,6 +304,9 @@ class Conv3d(nn.Conv3d):
 
 class ConvTranspose3d(nn.ConvTranspose3d):
     def forward(self, x, output_size=None):
+        if output_size is None and self.groups == 1 and self.dilation == (1, 1, 1) and \
+                convT_fewout_applies(x, self.weight, self.stride, self.padding, self.output_padding):
+            return _ConvTFewOutFn.apply(x, self.weight, self.bias)
         if output_size is None and self.groups == 1 and self.dilation == (1, 1, 1) and \
                 custom_backward_applies(x, self.weight):
             fast = fast_wgrad_applies(x, self.weight, None, self.stride, self.padding, True, self.output_padding)

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""HIP-event timings of the direct full-resolution stride-2 kernels (csrc/conv_up.hip) at the bench shapes."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "medical-vision-textural-bias_amd"), ROOT]
+import torch  # noqa: E402
+
+from texbias import conv as C  # noqa: E402
+
+
+def timeit(fn, n=10):
+    ts = []
+    for _ in range(n + 3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts = sorted(ts[3:])
+    return ts[len(ts) // 2] * 1e3
+
+
+x = torch.randn((2, 4, 240, 240, 160), device="cuda")
+w = torch.randn((16, 4, 3, 3, 3), device="cuda")
+K = C.s2_pairs(w)
+t = timeit(lambda: C.conv_s2_fewin(x, K, None, 16))
+print(f"conv_s2_fewin 4->16 (entry conv fwd)      {t:8.1f} us  {2 * 16 * 4 * 27 * 2 * 120 * 120 * 80 / t / 1e6:6.1f} TF/s")
+xt = torch.randn((2, 32, 120, 120, 80), device="cuda")
+wt = torch.randn((32, 3, 3, 3, 3), device="cuda")
+t = timeit(lambda: C.convT_fewout(xt, wt, None))
+print(f"convT_fewout 32->3 (exit convT fwd)       {t:8.1f} us  {2 * 32 * 3 * 27 * 2 * 120 * 120 * 80 / t / 1e6:6.1f} TF/s")
+gy = torch.randn((2, 3, 240, 240, 160), device="cuda")
+Kt = C.s2_pairs(wt)
+t = timeit(lambda: C.conv_s2_fewin(gy, Kt, None, 32))
+print(f"conv_s2_fewin 3->32 (exit convT dgrad)    {t:8.1f} us  {2 * 32 * 3 * 27 * 2 * 120 * 120 * 80 / t / 1e6:6.1f} TF/s")

@@ -1,0 +1,90 @@
+"""The full-resolution stride-2 layers of the U-Net on the direct kernels (csrc/conv_up.hip):
+Conv3d(Cin <= 4 -> 16/32, stride 2) forward and ConvTranspose3d(Cin -> Cout <= 4, stride 2,
+output_padding 1) forward and input gradient, against PyTorch (MIOpen) float32 and a float64 reference:
+the error vs float64 within 4x max(PyTorch float32's, 1e-6 of the largest value)."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def conv(gpu):
+    from texbias import conv
+    return conv
+
+
+def close64(ours, ref32, ref64):
+    scale = ref64.abs().max().item()
+    e_ours = (ours.double() - ref64).abs().max().item()
+    e_ref = (ref32.double() - ref64).abs().max().item()
+    assert e_ours <= 4 * max(e_ref, 1e-6 * scale), (e_ours, e_ref, scale)
+
+
+@pytest.mark.parametrize("cin,cout,shape", [(4, 16, (2, 12, 10, 32)), (3, 32, (1, 8, 6, 16)), (1, 16, (1, 6, 4, 8)),
+                                            (4, 16, (1, 10, 14, 160)), (2, 32, (2, 4, 6, 24))])
+def test_conv_s2_fewin(conv, cin, cout, shape):
+    torch.manual_seed(0)
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
+    ours = conv.Conv3d(cin, cout, 3, stride=2, padding=1).cuda()
+    assert conv.s2_fewin_applies(x, ours.weight, ours.stride, ours.padding)
+    ref = nn.Conv3d(cin, cout, 3, stride=2, padding=1).cuda()
+    ref.load_state_dict(ours.state_dict())
+    y = ours(x)
+    yr = ref(x)
+    y64 = F.conv3d(x.double(), ref.weight.double(), ref.bias.double(), stride=2, padding=1)
+    close64(y, yr, y64)
+    g = torch.randn_like(y)
+    (gw, gb), (gwr, gbr) = torch.autograd.grad(y, (ours.weight, ours.bias), g), \
+        torch.autograd.grad(yr, (ref.weight, ref.bias), g)
+    w64 = ref.weight.double().detach().requires_grad_(True)
+    gw64, = torch.autograd.grad(F.conv3d(x.double(), w64, None, stride=2, padding=1), w64, g.double())
+    close64(gw, gwr, gw64)
+    torch.testing.assert_close(gb, gbr, rtol=1e-4, atol=1e-4 * gbr.abs().max().item())
+
+
+@pytest.mark.parametrize("cin,cout,shape", [(32, 3, (2, 6, 5, 20)), (16, 2, (1, 4, 6, 8)), (32, 4, (1, 5, 3, 12)),
+                                            (32, 3, (1, 4, 4, 80)), (16, 1, (2, 3, 7, 4))])
+def test_convT_fewout(conv, cin, cout, shape):
+    torch.manual_seed(1)
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda", requires_grad=True)
+    ours = conv.ConvTranspose3d(cin, cout, 3, stride=2, padding=1, output_padding=1).cuda()
+    assert conv.convT_fewout_applies(x, ours.weight, ours.stride, ours.padding, ours.output_padding)
+    ref = nn.ConvTranspose3d(cin, cout, 3, stride=2, padding=1, output_padding=1).cuda()
+    ref.load_state_dict(ours.state_dict())
+    y = ours(x)
+    yr = ref(x)
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = ref.weight.detach().double().requires_grad_(True)
+    y64 = F.conv_transpose3d(x64, w64, ref.bias.double(), stride=2, padding=1, output_padding=1)
+    close64(y, yr, y64)
+    g = torch.randn_like(y)
+    gx, gw, gb = torch.autograd.grad(y, (x, ours.weight, ours.bias), g)
+    gxr, gwr, gbr = torch.autograd.grad(yr, (x, ref.weight, ref.bias), g)
+    gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
+    close64(gx, gxr, gx64)
+    close64(gw, gwr, gw64)
+    torch.testing.assert_close(gb, gbr, rtol=1e-4, atol=1e-4 * gbr.abs().max().item())
+
+
+def test_full_resolution_layers(conv):
+    """The bench shapes: Conv3d(4 -> 16, s2) on 2 x 4 x 240 x 240 x 160 and ConvTranspose3d(32 -> 3, s2)
+    from 2 x 32 x 120 x 120 x 80, forward and input gradient against PyTorch float32 (relative to the
+    largest value; the float64 comparison runs at the small shapes above)."""
+    torch.manual_seed(2)
+    x = torch.randn((2, 4, 240, 240, 160), device="cuda")
+    c = conv.Conv3d(4, 16, 3, stride=2, padding=1).cuda()
+    y = c(x)
+    yr = F.conv3d(x, c.weight, c.bias, stride=2, padding=1)
+    assert (y - yr).abs().max().item() <= 2e-5 * yr.abs().max().item()
+    xt = torch.randn((2, 32, 120, 120, 80), device="cuda", requires_grad=True)
+    t = conv.ConvTranspose3d(32, 3, 3, stride=2, padding=1, output_padding=1).cuda()
+    yt = t(xt)
+    ytr = F.conv_transpose3d(xt, t.weight, t.bias, stride=2, padding=1, output_padding=1)
+    assert (yt - ytr).abs().max().item() <= 2e-5 * ytr.abs().max().item()
+    g = torch.randn_like(yt)
+    gx, = torch.autograd.grad(yt, xt, g)
+    gxr, = torch.autograd.grad(ytr, xt, g)
+    assert (gx - gxr).abs().max().item() <= 2e-5 * gxr.abs().max().item()
