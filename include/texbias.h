@@ -227,6 +227,13 @@ int tb_conv3d_s2_fewin_f32(const float* in, const float* K, const float* bias, f
                            int Do, int Ho, int Wo, void* stream);
 int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, float* y, int N, int Cin, int Mout, int Di,
                           int Hi, int Wi, void* stream);
+/*
+ * Conv3d(16 -> 16, kernel 3, stride 1, padding 1) forward on the f32 matrix cores (csrc/conv_up.hip):
+ * x, y [N][16][D][H][W] (W % 16 == 0, W <= 128), weight [16][16][3][3][3], bias [16] or NULL.  The
+ * U-Net's 16-channel full-resolution units (forward, and input gradient with W'[c][m][t] = W[m][c][26-t]).
+ */
+int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
+                        void* stream);
 
 /*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous

@@ -27,6 +27,7 @@
 namespace {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Weights are wave-uniform: read through the constant address space they become scalar loads and
 // SGPR operands of the FMAs (as broadcast LDS reads they cost an LDS instruction per 2 FMAs: the
 // first version of these kernels was LDS-bound at 8 % of the FMA rate).
@@ -371,5 +372,166 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
       hipSuccess)
     return TB_ERR_HIP;
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+// ------------------------------------------------- stride-1 3x3x3 conv, 16 -> 16 channels, on MFMA
+// out[m][p] = b[m] + sum_{c, t} W[m][c][t] X[c][p + t - 1] (padding 1) as Out(16 m x 16 x) =
+// W(16 m x 432 k) . X(432 k x 16 x) on mfma_f32_16x16x4f32, k = (tap, channel quad): the block's whole
+// W lives in 108 A-fragment registers per lane for the kernel's life; B fragments are LDS reads of the
+// staged input planes (lane = (x, channel within the quad): bank-distinct at a channel pitch of 16 mod 32).
+// The block marches its (n, YB output rows, z segment) along z with a 4-slot plane ring (the next plane
+// in registers); each wave takes output tiles (row, 16 columns) two at a time (two accumulator chains
+// sharing every A fragment).  The input gradient of the same layer is this kernel with
+// W'[c][m][t] = W[m][c][26 - t].  Serves the 16-channel full-resolution units (120 x 120 x 80 at C3).
+namespace {
+struct F16Args {
+  const float* x;
+  const float* W;     // [16 m][16 c][27]
+  const float* bias;  // [16] or null
+  float* y;
+  int D, H, Wd;
+  int ZS, zlen, nyb;
+  int PX, RX;  // row pitch (data at column x + 4), channel pitch (= 16 mod 32)
+};
+
+template <int YB, int NXT>  // output rows per block; 16-column tiles per row (W = 16 NXT)
+__global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NR = YB + 2, W4 = 4 * NXT;  // staged rows; float4 per row
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int D = a.D, H = a.H, Wd = a.Wd, PX = a.PX, RX = a.RX, SS = 16 * RX;
+  float* ring = smem;  // [4][16 c][NR][PX]
+  for (int i = tid; i < 4 * SS; i += 256) ring[i] = 0.f;
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
+  // A fragments: lane (m = l & 15, ks = l >> 4); k-step kk = 4 t + cq covers channel 4 cq + ks at tap t
+  const int li = lane & 15, ks = lane >> 4;
+  float af[108];
+#pragma unroll
+  for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[(li * 16 + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
+  const int64_t plane = (int64_t)H * Wd, plane4 = plane / 4;
+  const float4* xb = reinterpret_cast<const float4*>(a.x + (int64_t)n * 16 * D * plane);
+  constexpr int NL = (16 * NR * W4 + 255) / 256;
+  int gof[NL], lof[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4, t = i / W4, r = t % NR, c = t / NR;
+    const int yi = y0 - 1 + r;
+    const bool ok = i < 16 * NR * W4 && yi >= 0 && yi < H;
+    gof[j] = ok ? (int)((int64_t)c * D * plane4 + ((int64_t)yi * Wd + 4 * q) / 4) : -1;
+    lof[j] = c * RX + r * PX + 4 + 4 * q;
+  }
+  float4 rg[NL];
+  auto load = [&](int zi) {
+    const bool in = zi >= 0 && zi < D;
+    const float4* src = xb + (int64_t)(in ? zi : 0) * plane4;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const float4 v = src[gof[j] < 0 ? 0 : gof[j]];
+      rg[j] = (in && gof[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int zi) {
+    float* d = ring + ((zi + 4) & 3) * SS;
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+  };
+  __syncthreads();
+  load(z0 - 1);
+  store(z0 - 1);
+  load(z0);
+  store(z0);
+  load(z0 + 1);
+  const float bm[4] = {a.bias ? a.bias[4 * ks] : 0.f, a.bias ? a.bias[4 * ks + 1] : 0.f,
+                       a.bias ? a.bias[4 * ks + 2] : 0.f, a.bias ? a.bias[4 * ks + 3] : 0.f};
+  // B lane base: channel 4 cq + ks (cq added per k-step), column x = li of the tile (+ tx - 1 at + 4)
+  const int bl = ks * RX + li + 3;
+  const int64_t oplane = plane;
+  float* yb0 = a.y + (int64_t)n * 16 * D * oplane;
+  constexpr int NT = YB * NXT;  // tiles per step
+  for (int z = z0; z < z1; ++z) {
+    store(z + 1);
+    __syncthreads();
+    if (z + 1 < z1) load(z + 2);
+    const float* s0 = ring + ((z + 3) & 3) * SS + bl;  // tz = 0: plane z - 1
+    const float* s1 = ring + (z & 3) * SS + bl;
+    const float* s2 = ring + ((z + 1) & 3) * SS + bl;
+    for (int t0 = wave; t0 < NT; t0 += 8) {  // tiles t0 and t0 + 4 of this wave
+      const int t1 = t0 + 4 < NT ? t0 + 4 : t0;
+      const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
+      const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
+      const int o0 = yy0 * PX + x00, o1 = yy1 * PX + x01;
+      f32x4 acc0 = {bm[0], bm[1], bm[2], bm[3]}, acc1 = acc0;
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz) {
+        const float* sl = tz == 0 ? s0 : tz == 1 ? s1 : s2;
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const int t = tz * 9 + ty * 3 + tx;
+#pragma unroll
+            for (int cq = 0; cq < 4; ++cq) {
+              const int off = 4 * cq * RX + ty * PX + tx;
+              const float b0 = sl[o0 + off], b1 = sl[o1 + off];
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], b0, acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], b1, acc1, 0, 0, 0);
+            }
+          }
+      }
+      // C: column x = li, rows m = 4 ks + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * ks + r;
+        if (y0 + yy0 < H) yb0[((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy0) * Wd + x00 + li] = acc0[r];
+        if (t1 != t0 && y0 + yy1 < H) yb0[((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy1) * Wd + x01 + li] = acc1[r];
+      }
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+// Conv3d(16 -> 16, 3, stride 1, padding 1) forward: x [N][16][D][H][W] -> y [N][16][D][H][W], W % 16 == 0,
+// W <= 128; weight [16][16][27], bias [16] or NULL.  (csrc/conv_up.hip, k_conv3d_fwd16)
+int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
+                        void* stream) {
+  if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
+  if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
+  constexpr int YB = 4;
+  F16Args a{};
+  a.x = x, a.W = W, a.bias = bias, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.PX = Wd + 8;
+  a.RX = (YB + 2) * a.PX;
+  while ((a.RX & 31) != 16) ++a.RX;
+  a.nyb = (H + YB - 1) / YB;
+  const size_t lds = (size_t)4 * 4 * 16 * a.RX;
+  if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
+  a.zlen = zseg(D, N * a.nyb, 1, 2);
+  a.ZS = (D + a.zlen - 1) / a.zlen;
+  void (*kern)(F16Args) = nullptr;
+  switch (Wd / 16) {
+    case 1: kern = k_conv3d_fwd16<YB, 1>; break;
+    case 2: kern = k_conv3d_fwd16<YB, 2>; break;
+    case 3: kern = k_conv3d_fwd16<YB, 3>; break;
+    case 4: kern = k_conv3d_fwd16<YB, 4>; break;
+    case 5: kern = k_conv3d_fwd16<YB, 5>; break;
+    case 6: kern = k_conv3d_fwd16<YB, 6>; break;
+    case 7: kern = k_conv3d_fwd16<YB, 7>; break;
+    case 8: kern = k_conv3d_fwd16<YB, 8>; break;
+    default: return TB_ERR_UNSUPPORTED_SIZE;
+  }
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
+      hipSuccess)
+    return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }

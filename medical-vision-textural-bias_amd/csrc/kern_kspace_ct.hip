@@ -170,6 +170,8 @@ static int kspace_occupancy(K kern, int nt, size_t lds) {
   return occ;
 }
 
+bool kspace_ct_persistent(int ncols) { return use_pair(ncols) && use_persist() && pair_tile() == 16; }
+
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t st) {
   const bool pair = use_pair(a.pl.W * (a.pl.D / 2 + 1));
   if (pair && use_persist() && pair_tile() == 16) {

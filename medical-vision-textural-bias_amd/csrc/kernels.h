@@ -76,6 +76,7 @@ hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st);
 bool kspace_ct_supported(int H);
 int kspace_ct_tile(int ncols);
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t st);
+bool kspace_ct_persistent(int ncols);  // launch_kspace_ct runs the persistent k_kspace_ct2p
 
 // Direct-DFT fallback (kern_generic.hip) for sizes the mixed-radix passes do not take: full complex
 // spectrum in two ping-pong buffers S[2][nbc][H][W][D] (gen_workspace_bytes).

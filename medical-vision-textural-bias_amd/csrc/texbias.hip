@@ -713,7 +713,10 @@ static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* 
       if (rc) return rc;
     }
     {
-      Timer t(1, st, 2.0 * spec, (g_compiled_plans && p->ct_tile) ? "k_kspace_ct2" : "k_kspace");
+      Timer t(1, st, 2.0 * spec,
+              (g_compiled_plans && p->ct_tile)
+                  ? (tb::kspace_ct_persistent(W * Dh) ? "k_kspace_ct2p" : "k_kspace_ct2")
+                  : "k_kspace");
       if (g_compiled_plans && p->ct_tile) {
         const int Tc = tb::kspace_ct_tile(W * Dh);
         KspaceArgs ka{p->dev, S, bc0, C, Tc, c0, bo, ng};

@@ -285,8 +285,55 @@ class _ConvTFewOutFn(torch.autograd.Function):
         return gx, gw, gb
 
 
+def conv_fwd16(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+    """Conv3d(16 -> 16, 3, stride 1, padding 1) forward on the f32 matrix cores (tb_conv3d_fwd16_f32)."""
+    x = x.contiguous()
+    N, _, D, H, W = x.shape
+    y = torch.empty_like(x)
+    with torch.cuda.device(x.device):
+        check(lib().tb_conv3d_fwd16_f32(x.data_ptr(), w.contiguous().data_ptr(), b.data_ptr() if b is not None else None,
+                                        y.data_ptr(), N, D, H, W, _stream(x)), "tb_conv3d_fwd16_f32")
+    return y
+
+
+def conv16_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
+    """Conv3d(16 -> 16, 3, stride 1, padding 1), rows of 16k <= 128 floats: k_conv3d_fwd16 (forward and
+    input gradient) + the z-marching weight gradient."""
+    return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape) == (16, 16, 3, 3, 3) and \
+        tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and x.shape[-1] % 16 == 0 and \
+        x.shape[-1] <= 80 and x.data_ptr() % 16 == 0 and os.environ.get("TEXBIAS_CONV16", "1") != "0"
+
+
+class _Conv16Fn(torch.autograd.Function):
+    """Conv3d(16 -> 16, stride 1): forward and input gradient (flipped, transposed weights) on the MFMA
+    kernel, weight gradient on the z-marching MFMA kernel, bias gradient on the channel-sum kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = conv_fwd16(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = conv_fwd16(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+        if ctx.needs_input_grad[1]:
+            gw = wgrad(gy, x, w.shape, 1, 1)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = channel_sum(gy)
+        return gx, gw, gb
+
+
 class Conv3d(nn.Conv3d):
     def forward(self, x):
+        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
+                conv16_applies(x, self.weight, self.stride, self.padding):
+            return _Conv16Fn.apply(x, self.weight, self.bias)
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
                 s2_fewin_applies(x, self.weight, self.stride, self.padding):
             return _ConvS2FewInFn.apply(x, self.weight, self.bias)

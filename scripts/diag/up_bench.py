@@ -36,3 +36,9 @@ gy = torch.randn((2, 3, 240, 240, 160), device="cuda")
 Kt = C.s2_pairs(wt)
 t = timeit(lambda: C.conv_s2_fewin(gy, Kt, None, 32))
 print(f"conv_s2_fewin 3->32 (exit convT dgrad)    {t:8.1f} us  {2 * 32 * 3 * 27 * 2 * 120 * 120 * 80 / t / 1e6:6.1f} TF/s")
+x16 = torch.randn((2, 16, 120, 120, 80), device="cuda")
+w16 = torch.randn((16, 16, 3, 3, 3), device="cuda")
+t = timeit(lambda: C.conv_fwd16(x16, w16, None))
+print(f"conv_fwd16 16->16 (120x120x80)            {t:8.1f} us  {2 * 16 * 16 * 27 * 2 * 120 * 120 * 80 / t / 1e6:6.1f} TF/s")
+t = timeit(lambda: torch.nn.functional.conv3d(x16, w16, None, padding=1))
+print(f"  MIOpen conv3d 16->16                    {t:8.1f} us")

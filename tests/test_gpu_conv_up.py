@@ -88,3 +88,25 @@ def test_full_resolution_layers(conv):
     gx, = torch.autograd.grad(yt, xt, g)
     gxr, = torch.autograd.grad(ytr, xt, g)
     assert (gx - gxr).abs().max().item() <= 2e-5 * gxr.abs().max().item()
+
+
+@pytest.mark.parametrize("shape", [(2, 6, 5, 32), (1, 9, 7, 80), (1, 3, 4, 16), (2, 12, 10, 48)])
+def test_conv16_mfma(conv, shape):
+    """Conv3d(16 -> 16, stride 1) forward and input gradient on k_conv3d_fwd16 (weight gradient: z-march)."""
+    torch.manual_seed(3)
+    x = torch.randn((shape[0], 16) + shape[1:], device="cuda", requires_grad=True)
+    ours = conv.Conv3d(16, 16, 3, padding=1).cuda()
+    assert conv.conv16_applies(x, ours.weight, ours.stride, ours.padding)
+    ref = nn.Conv3d(16, 16, 3, padding=1).cuda()
+    ref.load_state_dict(ours.state_dict())
+    y, yr = ours(x), ref(x)
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = ref.weight.detach().double().requires_grad_(True)
+    y64 = F.conv3d(x64, w64, ref.bias.double(), padding=1)
+    close64(y, yr, y64)
+    g = torch.randn_like(y)
+    gx, gw = torch.autograd.grad(y, (x, ours.weight), g)
+    gxr, gwr = torch.autograd.grad(yr, (x, ref.weight), g)
+    gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
+    close64(gx, gxr, gx64)
+    close64(gw, gwr, gw64)
