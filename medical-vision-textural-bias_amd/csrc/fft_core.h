@@ -36,6 +36,43 @@
 
 #define TB_MAX_STAGES 8
 
+// Loads of data a kernel reads once are nontemporal: a nontemporal read does not allocate in the
+// Infinity Cache, so one that follows a large write does not evict the written dirty lines and pay
+// their write-back (scripts/micro/read_bw.hip, 285.7 MB right after a 294 MB write: 86 us with plain
+// 16-B loads, 48 us nontemporal; 42-46 us both after a read).  TB_NT_LOADS: image reads (point,
+// wrap and slab forward passes); TB_NT_SPEC: the full route's spectrum reads (passes B and C).
+#ifndef TB_NT_LOADS
+#define TB_NT_LOADS 1
+#endif
+#ifndef TB_NT_SPEC
+#define TB_NT_SPEC 1
+#endif
+#ifndef TB_NT_WRAP  // the separable wrap pass (measured separately: it reads the clean input)
+#define TB_NT_WRAP 0
+#endif
+template <bool NT, class T>
+TB_HD T ld_stream(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (NT) return __builtin_nontemporal_load(p);
+#endif
+  return *p;
+}
+// TB_NT_STORES: the filtered image's stores nontemporal as well (point apply, wrap, slab inverse)
+#ifndef TB_NT_STORES
+#define TB_NT_STORES 0
+#endif
+template <bool NT, class T>
+TB_HD void st_stream(T* p, T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (NT) {
+    __builtin_nontemporal_store(v, p);
+    return;
+  }
+#endif
+  *p = v;
+}
+typedef float tb_f4v __attribute__((ext_vector_type(4)));
+
 namespace tb {
 
 struct alignas(8) cf {

@@ -5,6 +5,21 @@
 #include "kspace_ct.h"
 
 namespace tb {
+
+#ifdef TB_SLAB_PROF  // pass-B phase timestamps (as kern_slab_ct.hip)
+__device__ unsigned long long g_kspace_prof[256][16][8];
+#define TB_BSTAMP(U, I)                                                                        \
+  do {                                                                                         \
+    const int it_ = ((U) - (int)blockIdx.x) / (int)gridDim.x;                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && it_ < 16)                                      \
+      g_kspace_prof[blockIdx.x][it_][I] = __builtin_amdgcn_s_memtime();                        \
+  } while (0)
+#else
+#define TB_BSTAMP(U, I) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 using ct::v2;
 
@@ -73,7 +88,7 @@ __global__ __launch_bounds__(NT) void k_kspace_ct2(KspaceArgs) {
 // + gridDim.x, ...; each unit's stage-0 inputs are loaded into registers while the previous unit
 // runs its middle and inverse phases (one unit of HBM reads always in flight per workgroup, instead
 // of every short-lived workgroup paying the HBM latency before any of its arithmetic starts).
-template <int H, int T, int NT>
+template <int H, int T, int NT, int K>
 __global__ __launch_bounds__(NT) void k_kspace_ct2p(KspaceArgs) {
   using P = ct::TilePlan<H, T>;
   static_assert(P::N0 / 2 <= NT && P::NM % NT == 0 && NT % T == 0, "paired items");
@@ -101,7 +116,9 @@ __global__ __launch_bounds__(NT) void k_kspace_ct2p(KspaceArgs) {
     const int j0 = col0(u, bcl);
     v2* Sc = reinterpret_cast<v2*>(a.S) + (int64_t)(a.bc0 + bcl) * H * ncols + j0;
     const FreqCol fc = ct::tile_col(a.pl, j0 + tid % T);
+    TB_BSTAMP(u, 0);
     __syncthreads();  // the previous unit's inverse-stage reads of the tile are done (and the twiddles are in)
+    TB_BSTAMP(u, 1);
     if (ld) ct::b_s0_pair_regs<P>(lds, r, tid);
     {  // the next unit's inputs, in flight during the middle and inverse phases (clamped on the last pass)
       const int un = u + (int)gridDim.x < units ? u + (int)gridDim.x : u;
@@ -110,15 +127,30 @@ __global__ __launch_bounds__(NT) void k_kspace_ct2p(KspaceArgs) {
       if (ld) ct::b_load_pair<P>(r, reinterpret_cast<const v2*>(a.S) + (int64_t)(a.bc0 + bn) * H * ncols + jn, ncols, tid);
     }
     __syncthreads();
+    TB_BSTAMP(u, 2);
     const int sl = a.cofs + bcl;
+    if constexpr (K == ct::MASK_GENERIC) {
 #pragma unroll 1
-    for (int s = 0; s < P::NM / NT; ++s) ct::b_mid_lds<P>(lds, a.ops.s[sl / a.C], sl % a.C, fc, tid + s * NT);
+      for (int s = 0; s < P::NM / NT; ++s) ct::b_mid_lds<P>(lds, a.ops.s[sl / a.C], sl % a.C, fc, tid + s * NT);
+    } else {
+#pragma unroll 1
+      for (int s = 0; s < P::NM / NT; ++s) ct::b_mid_mask<P, K>(lds, a.ops.s[sl / a.C], sl % a.C, fc, tid + s * NT);
+    }
     __syncthreads();
+    TB_BSTAMP(u, 3);
     if (ld) ct::b_s1_pair<P>(lds, Sc, ncols, tid);
+    TB_BSTAMP(u, 4);
   }
 }
 
 }  // namespace
+
+#ifdef TB_SLAB_PROF
+extern "C" int tb_debug_kspace_prof(void* host, size_t bytes) {
+  if (bytes > sizeof(g_kspace_prof)) bytes = sizeof(g_kspace_prof);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kspace_prof), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 bool kspace_ct_supported(int H) {
 #define TB_X(h) if (H == h) return true;
@@ -172,18 +204,35 @@ static int kspace_occupancy(K kern, int nt, size_t lds) {
 
 bool kspace_ct_persistent(int ncols) { return use_pair(ncols) && use_persist() && pair_tile() == 16; }
 
+// the launch's programs all of one mask-op kind -> pass B's unrolled middle phase
+// (TEXBIAS_KSPACE_MASK=0: always the generic one)
+static int launch_mask_kind(const KspaceArgs& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_KSPACE_MASK");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (!on || a.nbc < 1) return ct::MASK_GENERIC;
+  const int s0 = a.cofs / a.C, s1 = (a.cofs + a.nbc - 1) / a.C;
+  return ct::mask_kind(a.ops.s + s0, s1 - s0 + 1);
+}
+
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t st) {
   const bool pair = use_pair(a.pl.W * (a.pl.D / 2 + 1));
   if (pair && use_persist() && pair_tile() == 16) {
+    const int mk = launch_mask_kind(a);
 #define TB_X(h)                                                                           \
     if (a.pl.H == h) {                                                                    \
       constexpr size_t lds = ct::TilePlan<h, 16>::LDS_BYTES;                              \
-      hipError_t e = allow_lds(k_kspace_ct2p<h, 16, 128>, lds);                           \
+      auto kern = mk == ct::MASK_GIBBS ? k_kspace_ct2p<h, 16, 128, ct::MASK_GIBBS>        \
+                : mk == ct::MASK_LAYER ? k_kspace_ct2p<h, 16, 128, ct::MASK_LAYER>        \
+                : mk == ct::MASK_DISK  ? k_kspace_ct2p<h, 16, 128, ct::MASK_DISK>         \
+                                       : k_kspace_ct2p<h, 16, 128, ct::MASK_GENERIC>;     \
+      hipError_t e = allow_lds(kern, lds);                                                \
       if (e != hipSuccess) return e;                                                      \
       const int units = (int)(grid.x * grid.y);                                           \
-      int g = ncu * kspace_occupancy(k_kspace_ct2p<h, 16, 128>, 128, lds);                \
+      int g = ncu * kspace_occupancy(kern, 128, lds);                                     \
       g = g < units ? g : units;                                                          \
-      hipLaunchKernelGGL((k_kspace_ct2p<h, 16, 128>), dim3(g), dim3(128), lds, st, a);    \
+      hipLaunchKernelGGL(kern, dim3(g), dim3(128), lds, st, a);                           \
       return hipGetLastError();                                                           \
     }
     TB_CT_TILE_H(TB_X)

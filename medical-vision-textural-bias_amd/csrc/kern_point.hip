@@ -75,7 +75,11 @@ typedef float f32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ void load_quad(const float* row, int d0, int D, bool ok, float (&v)[4]) {
   const int dl = d0 + 4 <= D ? d0 : D - 4, sh = ok ? d0 - dl : 4;  // sh 4: nothing
+#if TB_NT_LOADS  // (the builtin directly: ld_stream's template parameter would drop the 4-B alignment)
+  const f32x4_a4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4_a4*>(row + dl));
+#else
   const f32x4_a4 q = *reinterpret_cast<const f32x4_a4*>(row + dl);
+#endif
   const float e[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -390,7 +394,7 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
         }
       float* yr = yb + ((uint32_t)h * (uint32_t)a.ysh + (uint32_t)w * (uint32_t)a.ysw);
       if (vout && d0 + 4 <= ncol) {
-        *reinterpret_cast<float4*>(yr + d0) = make_float4(v[0], v[1], v[2], v[3]);
+        st_stream<TB_NT_STORES>(reinterpret_cast<tb_f4v*>(yr + d0), tb_f4v{v[0], v[1], v[2], v[3]});
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)

@@ -11,6 +11,23 @@
 #include "slab_ct.h"
 
 namespace tb {
+
+// Phase timestamps (measurement builds only: -DTB_SLAB_PROF, scripts/build_variant.sh): thread 0 of
+// workgroups < 256 stamps the shader clock after each barrier of its first 16 units.
+#ifdef TB_SLAB_PROF
+__device__ unsigned long long g_slab_prof[2][256][16][12];
+#define TB_STAMP(K, U, I)                                                                      \
+  do {                                                                                         \
+    const int it_ = ((U) - (int)blockIdx.x) / (int)gridDim.x;                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && it_ < 16)                                      \
+      g_slab_prof[K][blockIdx.x][it_][I] = __builtin_amdgcn_s_memtime();                       \
+  } while (0)
+#else
+#define TB_STAMP(K, U, I) \
+  do {                    \
+  } while (0)
+#endif
+
 namespace {
 using ct::v2;
 
@@ -109,10 +126,12 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct16(SlabFwdArgs) {
     const f4* xb = reinterpret_cast<const f4*>(a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh);
 #pragma unroll
     for (int s = 0; s < SV; ++s)
-      if (tid + s * NT < NV) rv[s] = xb[tid + s * NT];
+      if (tid + s * NT < NV) rv[s] = ld_stream<TB_NT_LOADS>(xb + tid + s * NT);
   }
   for (; u < units; u += (int)gridDim.x) {
+    TB_STAMP(0, u, 0);
     __syncthreads();  // the previous unit's W1 reads are done (and the twiddles are visible)
+    TB_STAMP(0, u, 1);
     {
       f4* raw4 = reinterpret_cast<f4*>(smem);
 #pragma unroll
@@ -120,16 +139,20 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct16(SlabFwdArgs) {
         if (tid + s * NT < NV) raw4[tid + s * NT] = rv[s];
     }
     __syncthreads();
+    TB_STAMP(0, u, 2);
     v2 rf[SF][P::R0];
 #pragma unroll
     for (int s = 0; s < SF; ++s)
       if (tid + s * NT < P::N_F0) ct::a_load_raw<P>(reinterpret_cast<const float*>(smem), rf[s], tid + s * NT);
     __syncthreads();  // every raw read is done before Z (the same bytes) is written
+    TB_STAMP(0, u, 3);
 #pragma unroll
     for (int s = 0; s < SF; ++s)
       if (tid + s * NT < P::N_F0) ct::a_f0<P>(lds, rf[s], tid + s * NT);
     // next unit's raw slab (clamped on the last pass, as in k_slab_fwd_ct): EARLY issues it here,
     // in flight during D1 / U / W0 / W1, else after U (in flight during W0 / W1 only)
+    // (issuing these loads spread over F0 / D1 / U / W0 instead measured no faster: the F0 phase
+    // shrank by what the later phases grew, and the kernel spilled)
     auto prefetch = [&]() {
       const int un = u + (int)gridDim.x;
       const int uc = un < units ? un : u;
@@ -137,29 +160,37 @@ __global__ __launch_bounds__(NT) void k_slab_fwd_ct16(SlabFwdArgs) {
       const f4* xb = reinterpret_cast<const f4*>(a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh);
 #pragma unroll
       for (int s = 0; s < SV; ++s)
-        if (tid + s * NT < NV) rv[s] = xb[tid + s * NT];
+        if (tid + s * NT < NV) rv[s] = ld_stream<TB_NT_LOADS>(xb + tid + s * NT);
     };
     if constexpr (EARLY) prefetch();
     __syncthreads();
+    TB_STAMP(0, u, 4);
     _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::a_d1<P>(lds, it);
     __syncthreads();
+    TB_STAMP(0, u, 5);
     {
       v2 ru[SU][2];
 #pragma unroll
       for (int s = 0; s < SU; ++s)
         if (tid + s * NT < P::N_U) ct::a_u_read<P>(lds, ru[s], tid + s * NT);
       __syncthreads();
+      TB_STAMP(0, u, 6);
 #pragma unroll
       for (int s = 0; s < SU; ++s)
         if (tid + s * NT < P::N_U) ct::a_u_write<P>(lds, ru[s], tid + s * NT);
     }
     if constexpr (!EARLY) prefetch();
     __syncthreads();
+    TB_STAMP(0, u, 7);
     _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::a_w0<P>(lds, it);
     __syncthreads();
+    TB_STAMP(0, u, 8);
     const int bcl = u / H, h = u - bcl * H;
     v2* Sb = reinterpret_cast<v2*>(a.S) + ((int64_t)(a.bc0 + bcl) * H + h) * (int64_t)(W * P::Dh);
+    // (W1 in place in LDS + one contiguous 16-B sweep of the slab's spectrum, every line written
+    // whole, measured 13 us slower per C3 launch than these strided 8-B stores)
     _Pragma("unroll 1") for (int it = tid; it < P::N_W1; it += NT) ct::a_w1<P>(lds, Sb, it);
+    TB_STAMP(0, u, 9);
   }
 }
 
@@ -187,13 +218,17 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
       if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
   }
   for (; u < units; u += (int)gridDim.x) {
+    TB_STAMP(1, u, 0);
     __syncthreads();  // the previous unit's E0 reads are done
+    TB_STAMP(1, u, 1);
 #pragma unroll
     for (int s = 0; s < SG; ++s)
       if (tid + s * NT < P::N_W1) ct::c_g0<P>(lds, rg[s], tid + s * NT);
     __syncthreads();
+    TB_STAMP(1, u, 2);
     _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::c_g1<P>(lds, it);
     __syncthreads();
+    TB_STAMP(1, u, 3);
     if constexpr (FUSE && P::FUSED_DU) {  // repack + inverse D stage 1 in one phase (slab_ct.h c_re_*)
       constexpr int SD = ct::Slots<P::N_DU, NT>::value;
       v2 rd[SD][2 * P::R1];
@@ -201,6 +236,7 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
       for (int s = 0; s < SD; ++s)
         if (tid + s * NT < P::N_DU) ct::c_re_load<P>(lds, rd[s], tid + s * NT);
       __syncthreads();
+      TB_STAMP(1, u, 4);
 #pragma unroll
       for (int s = 0; s < SD; ++s)
         if (tid + s * NT < P::N_DU) ct::c_re_compute<P>(lds, rd[s], tid + s * NT);
@@ -224,9 +260,11 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
         if (tid + s * NT < P::N_W1) ct::c_load<P>(rg[s], Sb, tid + s * NT);
     }
     __syncthreads();
+    TB_STAMP(1, u, 5);
     const int bcl = u / H, h = u - bcl * H, bc = a.bc0 + bcl;
     float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh;
     _Pragma("unroll 1") for (int it = tid; it < P::N_F0; it += NT) ct::c_e0<P>(lds, yb, a.sw, a.scale, it, lo, hi);
+    TB_STAMP(1, u, 6);
     if (a.ypad > 0) {
       const FastDiv fp = FastDiv::make(a.ypad);
       for (int t = tid; t < W * a.ypad; t += NT) {
@@ -241,6 +279,7 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
       lo = 3.402823466e38f;
       hi = -3.402823466e38f;
     }
+    TB_STAMP(1, u, 7);
   }
 }
 
@@ -260,6 +299,17 @@ hipError_t launch_ct(K kern, int nt, size_t lds, int units, int ncu, const A& a,
 }
 
 }  // namespace
+
+#ifdef TB_SLAB_PROF
+extern "C" int tb_debug_slab_prof(void* host, size_t bytes) {
+  if (bytes > sizeof(g_slab_prof)) bytes = sizeof(g_slab_prof);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_slab_prof), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int tb_debug_slab_prof_clear() {
+  static unsigned long long z[2][256][16][12];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_slab_prof), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 // threads per workgroup: 768 (3 waves per SIMD) by default; TEXBIAS_CT_NT=512 selects 512 (tuning).
 // TEXBIAS_CT_FUSE (bit 1: forward, bit 2: inverse; default 2) selects the fused DU / RE phase
@@ -294,7 +344,7 @@ static bool raw16_ok(const SlabFwdArgs& a) {
     return !(e && std::atoi(e) == 0);
   }();
   return on && a.sw == a.pl.D && a.sh % 4 == 0 && a.sbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
-         (a.pl.W * a.pl.D) % 4 == 0;
+         (a.pl.W * a.pl.D) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.S) & 15) == 0;
 }
 
 static bool raw16_early() {

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
   const int n = lane & 15, role = n >> 2, g = n & 3, kb = lane >> 4;
   const int cpy = (-lane) & 7;
   const _Float16* thp = tab + cpy * L + (OFF - cpy + 8 * kb - n) - 16 * (NTO - 1);  // + 32 s + 16 (NTO - 1 - t)
-  const float* xrd = stg + role * a.RS + ((a.radj >> (8 * role)) & 255) + g * D + 8 * kb;  // + 32 s + j
+  const float* xrd = stg + role * a.RS + g * D + 8 * kb;                            // + 32 s + j
   int cur = -1;
   float lo = FLT_MAX, hi = -FLT_MAX;
   // the quad's four role chunks (rows 4 gq + rw W/2 + g of slabs hq + rh H/2) of unit u into v
@@ -223,8 +223,7 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
         const int f = lane + 64 * i;
         if (f < D) {  // 4 f < 4 D: inside the role's 4-row chunk
           const float4 s4 = v[r][i];
-          *reinterpret_cast<float4*>(stg + r * a.RS + ((a.radj >> (8 * r)) & 255) + 4 * f) =
-              make_float4(s4.x * sx, s4.y * sx, s4.z * sx, s4.w * sx);
+          *reinterpret_cast<float4*>(stg + r * a.RS + 4 * f) = make_float4(s4.x * sx, s4.y * sx, s4.z * sx, s4.w * sx);
         }
       }
     // the wave's next unit: its loads fly during this unit's products and stores
@@ -463,31 +462,7 @@ hipError_t launch_dgemm(WrapArgs& a, int ncu, hipStream_t st) {
   constexpr int L = (32 * KS + 16 * NTO + 8 + 15) & ~15;
   const bool vec = a.vec & 1;
   a.RS = (4 * a.D + 3) & ~3;
-  // per-role offsets (non-decreasing multiples of 4 below 32, so the chunks never overlap) putting the
-  // 32 lanes of a read group -- (role, row g, k-half kb) at role chunk + g D + 8 kb -- on as few
-  // shared banks as possible (D = 155: 0, 4, 4, 8 -- conflict-free)
-  int last = 0;
-  {
-    int best = 1 << 30, pick = 0;
-    for (int c = 0; c < 8 * 8 * 8 && best > 1; ++c) {
-      const int adj[4] = {0, 4 * (c & 7), 4 * ((c >> 3) & 7), 4 * (c >> 6)};
-      if (adj[1] > adj[2] || adj[2] > adj[3]) continue;
-      int cnt[32] = {0}, worst = 0;
-      for (int r = 0; r < 4; ++r)
-        for (int g = 0; g < 4; ++g)
-          for (int kb = 0; kb < 2; ++kb) {
-            const int b = (r * a.RS + adj[r] + g * a.D + 8 * kb) & 31;
-            worst = ++cnt[b] > worst ? cnt[b] : worst;
-          }
-      if (worst < best) {
-        best = worst;
-        pick = adj[1] << 8 | adj[2] << 16 | adj[3] << 24;
-        last = adj[3];
-      }
-    }
-    a.radj = pick;
-  }
-  a.region = (3 * a.RS + last + 3 * a.D + 32 * KS + 3) & ~3;
+  a.region = (3 * a.RS + 3 * a.D + 32 * KS + 3) & ~3;
   const size_t lds = (size_t)32 * L + (size_t)4 * a.region * (WRAP_NT / 64);
   auto kern = vec ? k_wrap_dgemm<NTO, KS, true> : k_wrap_dgemm<NTO, KS, false>;
   const hipError_t e = allow_lds(kern, lds);

@@ -175,6 +175,71 @@ TB_HD void b_mid_lds(v2* lds, const SO& so, int chan, const FreqCol& fc, int it)
   for (int q = 0; q < P::Q1; ++q) t[q * P::T] = a[q];
 }
 
+// Programs made of one mask-op kind (every op GIBBS, or every op LAYER, or every op DISK): the
+// ops scale or zero the butterfly's Q1 coefficients in registers between the two DFTs, fully
+// unrolled (b_mid_lds's rolled per-coefficient apply_ops made pass B latency-bound: 34 K of a
+// 44 K-cycle unit).  Each op is applied in program order exactly as apply_ops does (scale by
+// 0 / 0.5 / 1, or select), so the results are the generic path's bit for bit.
+enum { MASK_GENERIC = 0, MASK_GIBBS = 1, MASK_LAYER = 2, MASK_DISK = 3 };
+template <class SO>
+TB_HD int mask_kind(const SO* s, int n) {
+  int k = -1;
+  for (int i = 0; i < n; ++i) {
+    if (s[i].n < 1) return MASK_GENERIC;
+    for (int o = 0; o < s[i].n; ++o) {
+      const int kd = s[i].op[o].kind;
+      const int m = kd == TB_OP_GIBBS ? MASK_GIBBS : kd == TB_OP_LAYER ? MASK_LAYER : kd == TB_OP_DISK ? MASK_DISK : 0;
+      if (m == 0 || (k >= 0 && m != k)) return MASK_GENERIC;
+      k = m;
+    }
+  }
+  return k < 0 ? MASK_GENERIC : k;
+}
+template <class P, int K, class SO>
+TB_HD void b_mid_mask(v2* lds, const SO& so, int chan, const FreqCol& fc, int it) {
+  const int blk = it / P::T, c = it - blk * P::T;
+  v2* t = lds + (blk * P::L) * P::T + c;
+  v2 a[P::Q1];
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) a[q] = t[q * P::T];
+  Dv<P::Q1, true>::run(a);
+  int g0[P::Q1], g1[P::Q1];  // per coefficient: (ef, en) for GIBBS / LAYER, dsq for DISK
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) {  // slot blk*L + q holds kh = blk + Q0*q
+    const AxisGeo h = axis_geo(blk + P::Q0 * q, P::H);
+    g0[q] = K == MASK_DISK ? h.dsq + fc.dsq : h.ef + fc.ef;
+    g1[q] = h.en + fc.en;
+  }
+  for (int o = 0; o < so.n; ++o) {
+    const tb_op& op = so.op[o];
+    if (op.chan >= 0 && op.chan != chan) continue;
+    if constexpr (K == MASK_GIBBS) {
+      TB_UNROLL
+      for (int q = 0; q < P::Q1; ++q) {
+        const float m = 0.5f * (((int64_t)g0[q] <= op.l ? 1.f : 0.f) + ((int64_t)g1[q] <= op.l ? 1.f : 0.f));
+        a[q] = m * a[q];
+      }
+    } else if constexpr (K == MASK_LAYER) {
+      TB_UNROLL
+      for (int q = 0; q < P::Q1; ++q) {
+        const float m = 0.5f * ((layer_in(op, g0[q]) ? 1.f : 0.f) + (layer_in(op, g1[q]) ? 1.f : 0.f));
+        a[q] = m * a[q];
+      }
+    } else {
+      const bool ir = op.i[0] != 0, off = op.i[1] != 0;
+      TB_UNROLL
+      for (int q = 0; q < P::Q1; ++q) {
+        bool in = ir ? ((int64_t)g0[q] < op.l) : ((float)g0[q] < op.f[0]);
+        if (off) in = !in;
+        a[q] = in ? a[q] : V(0.f, 0.f);
+      }
+    }
+  }
+  Dv<P::Q1, false>::run(a);
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) t[q * P::T] = a[q];
+}
+
 template <class P>
 TB_HD void b_s1(const v2* lds, v2* __restrict__ Sc, int64_t ncols, int it) {
   const int j = it / P::T, c = it - j * P::T;
@@ -229,7 +294,7 @@ TB_HD void b_load_pair(f4* r, const v2* __restrict__ Sc, int64_t ncols, int it) 
   const f4* s = reinterpret_cast<const f4*>(Sc + (int64_t)j * ncols + c);
   const int64_t st = (int64_t)P::L * (ncols / 2);
   TB_UNROLL
-  for (int q = 0; q < P::Q0; ++q) r[q] = s[q * st];
+  for (int q = 0; q < P::Q0; ++q) r[q] = ld_stream<TB_NT_SPEC>(s + q * st);
 }
 template <class P>
 TB_HD void b_s0_pair_regs(v2* lds, const f4* r, int it) {

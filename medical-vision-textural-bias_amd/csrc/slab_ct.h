@@ -370,8 +370,12 @@ template <class P>
 TB_HD void c_load(v2* r, const v2* __restrict__ Sb, int it) {
   const int blk = it / P::Dh, k = it - blk * P::Dh;
   const v2* s = Sb + (blk * P::LW) * P::Dh + k;
+  typedef float f2v __attribute__((ext_vector_type(2)));
   TB_UNROLL
-  for (int q = 0; q < P::Q1; ++q) r[q] = s[q * P::Dh];
+  for (int q = 0; q < P::Q1; ++q) {
+    const f2v t = ld_stream<TB_NT_SPEC>(reinterpret_cast<const f2v*>(s + q * P::Dh));
+    r[q] = V(t.x, t.y);
+  }
 }
 
 template <class P>
@@ -493,8 +497,8 @@ TB_HD void c_e0(const v2* lds, float* __restrict__ yb, int64_t sw, float scale, 
   TB_UNROLL
   for (int q = 0; q < P::R0; ++q) {
     const v2 v = a[q] * scale;
-    r0[q * P::L0] = v.x;
-    r1[q * P::L0] = v.y;
+    st_stream<TB_NT_STORES>(r0 + q * P::L0, v.x);
+    st_stream<TB_NT_STORES>(r1 + q * P::L0, v.y);
     lo = v.x < lo ? v.x : lo;
     hi = v.x > hi ? v.x : hi;
     lo = v.y < lo ? v.y : lo;

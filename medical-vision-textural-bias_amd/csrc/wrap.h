@@ -41,9 +41,7 @@ struct WrapArgs {
   float ah[TB_MAX_BATCH], bh[TB_MAX_BATCH], aw[TB_MAX_BATCH], bw[TB_MAX_BATCH], ad[TB_MAX_BATCH], bd[TB_MAX_BATCH];
   float alpha;            // D odd: the launch's (uniform) D-axis alpha for the circulant table
   const double* q;        // D odd: q[j], j < D (plan table)
-  int RS;                 // D odd: floats between the staged role chunks of a unit (>= 4 D, multiple of 32)
-  int radj;               // D odd: role r's chunk at r RS + byte r of radj (floats, multiple of 4): the
-                          // lanes' (role, row, k-half) reads of a k-step on 32 distinct banks
+  int RS;                 // D odd: floats between the staged role chunks of a unit (>= 4 D, multiple of 4)
   int region;             // D odd: floats of one wave's staging region
   int vec;                // 16-B loads / stores (alignment checked on the host)
   uint32_t* mm;           // per-sample min/max keys, or null

@@ -100,9 +100,14 @@ void ct_tile(const tb_plan_dev& pl, v2* lds, v2* S, int bc, int tile, const tb_s
     if (it % T < nc) ct::b_load<P>(r, Sc, ncols, it);
     ct::b_s0<P>(lds, r, it);
   }
+  const int mk = ct::mask_kind(&so, 1);  // the device's unrolled middle phase for mask-only programs
   for (int it = 0; it < P::NM; ++it) {
     const int c = it % T;
-    ct::b_mid<P>(lds, so, chan, ct::tile_col(pl, j0 + (c < nc ? c : 0)), it);
+    const FreqCol fc = ct::tile_col(pl, j0 + (c < nc ? c : 0));
+    if (mk == ct::MASK_GIBBS) ct::b_mid_mask<P, ct::MASK_GIBBS>(lds, so, chan, fc, it);
+    else if (mk == ct::MASK_LAYER) ct::b_mid_mask<P, ct::MASK_LAYER>(lds, so, chan, fc, it);
+    else if (mk == ct::MASK_DISK) ct::b_mid_mask<P, ct::MASK_DISK>(lds, so, chan, fc, it);
+    else ct::b_mid<P>(lds, so, chan, fc, it);
   }
   for (int it = 0; it < P::N0; ++it)
     if (it % T < nc) ct::b_s1<P>(lds, Sc, ncols, it);
