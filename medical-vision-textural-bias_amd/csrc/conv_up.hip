@@ -380,8 +380,8 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
 // W(16 m x 432 k) . X(432 k x 16 x) on mfma_f32_16x16x4f32, k = (tap, channel quad): the block's whole
 // W lives in 108 A-fragment registers per lane for the kernel's life; B fragments are LDS reads of the
 // staged input planes (lane = (x, channel within the quad): bank-distinct at a channel pitch of 16 mod 32).
-// The block marches its (n, YB output rows, z segment) along z with a 4-slot plane ring (the next plane
-// in registers); each wave takes output tiles (row, 16 columns) two at a time (two accumulator chains
+// The block marches its (n, YB output rows, z segment) along z with a 3-slot plane ring (the next plane
+// in registers, stored over the slot the previous step read last); each wave takes output tiles (row, 16 columns) two at a time (two accumulator chains
 // sharing every A fragment).  The input gradient of the same layer is this kernel with
 // W'[c][m][t] = W[m][c][26 - t].  Serves the 16-channel full-resolution units (120 x 120 x 80 at C3).
 namespace {
@@ -402,8 +402,8 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int D = a.D, H = a.H, Wd = a.Wd, PX = a.PX, RX = a.RX, SS = 16 * RX;
-  float* ring = smem;  // [4][16 c][NR][PX]
-  for (int i = tid; i < 4 * SS; i += 256) ring[i] = 0.f;
+  float* ring = smem;  // [3][16 c][NR][PX]
+  for (int i = tid; i < 3 * SS; i += 256) ring[i] = 0.f;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
     }
   };
   auto store = [&](int zi) {
-    float* d = ring + ((zi + 4) & 3) * SS;
+    float* d = ring + ((zi + 3) % 3) * SS;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
       if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
@@ -461,9 +461,9 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
     store(z + 1);
     __syncthreads();
     if (z + 1 < z1) load(z + 2);
-    const float* s0 = ring + ((z + 3) & 3) * SS + bl;  // tz = 0: plane z - 1
-    const float* s1 = ring + (z & 3) * SS + bl;
-    const float* s2 = ring + ((z + 1) & 3) * SS + bl;
+    const float* s0 = ring + ((z + 2) % 3) * SS + bl;  // tz = 0: plane z - 1
+    const float* s1 = ring + (z % 3) * SS + bl;
+    const float* s2 = ring + ((z + 1) % 3) * SS + bl;
     for (int t0 = wave; t0 < NT; t0 += 8) {  // tiles t0 and t0 + 4 of this wave
       const int t1 = t0 + 4 < NT ? t0 + 4 : t0;
       const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
@@ -506,29 +506,41 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
                         void* stream) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
-  constexpr int YB = 4;
+  // output rows per block (TEXBIAS_CONV16_YB 2..4; C3, W = 80: YB 2 / 3 / 4 = 478 / 419 / 482 us -- the
+  // YB x 5 tiles of a step over 4 waves x 2 chains: 10 of 16, 15 of 16, 20 of 24 slots used; YB = 2's
+  // second block per CU did not make up for it)
+  static const int YBv = [] {
+    const char* e = std::getenv("TEXBIAS_CONV16_YB");
+    const int v = e ? std::atoi(e) : 3;
+    return v >= 2 && v <= 4 ? v : 3;
+  }();
+  const int YB = YBv;
   F16Args a{};
   a.x = x, a.W = W, a.bias = bias, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.PX = Wd + 8;
   a.RX = (YB + 2) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;
   a.nyb = (H + YB - 1) / YB;
-  const size_t lds = (size_t)4 * 4 * 16 * a.RX;
+  const size_t lds = (size_t)3 * 4 * 16 * a.RX;
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
-  a.zlen = zseg(D, N * a.nyb, 1, 2);
+  const int per_cu = 163840 / (int)lds >= 2 ? 2 : 1;
+  a.zlen = zseg(D, N * a.nyb, per_cu, 2);
   a.ZS = (D + a.zlen - 1) / a.zlen;
   void (*kern)(F16Args) = nullptr;
-  switch (Wd / 16) {
-    case 1: kern = k_conv3d_fwd16<YB, 1>; break;
-    case 2: kern = k_conv3d_fwd16<YB, 2>; break;
-    case 3: kern = k_conv3d_fwd16<YB, 3>; break;
-    case 4: kern = k_conv3d_fwd16<YB, 4>; break;
-    case 5: kern = k_conv3d_fwd16<YB, 5>; break;
-    case 6: kern = k_conv3d_fwd16<YB, 6>; break;
-    case 7: kern = k_conv3d_fwd16<YB, 7>; break;
-    case 8: kern = k_conv3d_fwd16<YB, 8>; break;
-    default: return TB_ERR_UNSUPPORTED_SIZE;
-  }
+#define TB_F16(Y)                                        \
+  if (YB == Y) switch (Wd / 16) {                        \
+      case 1: kern = k_conv3d_fwd16<Y, 1>; break;        \
+      case 2: kern = k_conv3d_fwd16<Y, 2>; break;        \
+      case 3: kern = k_conv3d_fwd16<Y, 3>; break;        \
+      case 4: kern = k_conv3d_fwd16<Y, 4>; break;        \
+      case 5: kern = k_conv3d_fwd16<Y, 5>; break;        \
+      case 6: kern = k_conv3d_fwd16<Y, 6>; break;        \
+      case 7: kern = k_conv3d_fwd16<Y, 7>; break;        \
+      case 8: kern = k_conv3d_fwd16<Y, 8>; break;        \
+      default: return TB_ERR_UNSUPPORTED_SIZE;           \
+    }
+  TB_F16(2) TB_F16(3) TB_F16(4)
+#undef TB_F16
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;
