@@ -235,6 +235,14 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
 int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
                         void* stream);
 
+/* ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward on the f32 matrix cores
+ * (sub-pixel form, all 27 taps real): x [N][64][Di][Hi][Wi] -> y [N][16][2Di][2Hi][2Wi], weight
+ * [64][16][3][3][3] as torch's module holds it, bias [16] or NULL; Wi % 4 == 0, Wi <= 64, x 16-B
+ * aligned.  Replaces the col2im path torch.nn.functional.conv_transpose3d takes for the U-Net's up1
+ * layer of the train step (10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-243, MONAI UNet). */
+int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, float* y, int N, int Di, int Hi, int Wi,
+                          void* stream);
+
 /*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
  * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution

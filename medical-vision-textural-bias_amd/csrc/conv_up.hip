@@ -547,3 +547,182 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
   hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
+
+// ------------------------------------------------- ConvTranspose3d(64 -> 16, 3, s2, p1, op1) on MFMA
+// Sub-pixel form (as k_convT_fewout): input position i = (z, y, x) gives the 8 outputs 2 i + p, p in
+// {0, 1}^3; per axis parity 0 takes tap 1 at offset 0, parity 1 takes tap 2 at offset 0 and tap 0 at
+// offset +1, so the 27 taps split over the 8 parities and each is a real multiply-add.  As products:
+// Out_p(16 m x 16 positions) = sum over p's taps and the 64 channels of W[c][m][t] X[c][i + delta(t)],
+// on mfma_f32_16x16x4f32 with k = (tap, channel quad).  Wave g holds the A fragments of channel group
+// g (channels 16 g .. 16 g + 15: 108 registers) and accumulates all 8 parities of a 16-position tile
+// (positions = flattened (row, column) of the block's YB input rows); the four groups' partial tiles
+// meet in LDS (double-buffered, one barrier per tile), where wave w sums parities (w >> 1, w & 1, 0 / 1)
+// and writes them as (px = 0, 1) float2 pairs.  The block marches (n, YB rows, z segment) along z with
+// a 2-slot input plane ring (plane z and z + 1; the next plane in registers).  Replaces MIOpen's
+// col2im GEMM pair for the U-Net's up1 ConvTranspose3d (64 -> 16, 60 x 60 x 40 -> 120 x 120 x 80 at C3).
+namespace {
+struct T64Args {
+  const float* x;     // [N][64][Di][Hi][Wi]
+  const float* W;     // [64 c][16 m][27]
+  const float* bias;  // [16] or null
+  float* y;           // [N][16][2 Di][2 Hi][2 Wi]
+  int Di, Hi, Wi;
+  int ZS, zlen, nyb;
+  int PX, RX;         // staged row pitch (data at columns 0 .. Wi - 1, zeros after), channel pitch (16 mod 32)
+};
+
+template <int YB, int NL>  // NL: float4 staging pieces per thread (64 (YB + 1) Wi / 4 <= 256 NL)
+__global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NR = YB + 1;  // staged rows: y0 .. y0 + YB
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // channel group of this wave
+  const int Di = a.Di, Hi = a.Hi, Wi = a.Wi, PX = a.PX, RX = a.RX, SS = 64 * RX;
+  float* ring = smem;                   // [2][64 c][NR][PX]
+  float* part = smem + 2 * SS;          // [2 buf][4 waves][8 parities][16 m][16 pos]
+  for (int i = tid; i < 2 * SS; i += 256) ring[i] = 0.f;
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(Di, z0 + a.zlen);
+  const int li = lane & 15, ks = lane >> 4;
+  float af[108];  // k-step 4 t + cq: channel 16 g + 4 cq + ks, tap t, output channel li
+#pragma unroll
+  for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[((16 * g + 4 * (kk & 3) + ks) * 16 + li) * 27 + (kk >> 2)];
+  const int64_t plane = (int64_t)Hi * Wi;
+  const float* xb = a.x + (int64_t)n * 64 * Di * plane;
+  // staging: float4 pieces of (channel, row, column quad); Wi % 4 == 0.  gof: offset in the
+  // channel-plane's floats (-1: a row past Hi, staged as zeros), lof: LDS offset (-1: no piece)
+  const int W4 = Wi >> 2, per_c = NR * W4, total = 64 * per_c;
+  const int64_t cstride = (int64_t)Di * plane;
+  int gof[NL], lof[NL], gch[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + 256 * j;
+    const int c = i / per_c, r2 = i - c * per_c, r = r2 / W4, q = r2 - r * W4;
+    const int yi = y0 + r;
+    lof[j] = i < total ? c * RX + r * PX + 4 * q : -1;
+    gof[j] = (i < total && yi < Hi) ? yi * Wi + 4 * q : -1;
+    gch[j] = i < total ? c : 0;
+  }
+  float4 rg[NL];
+  auto load = [&](int zi) {
+    const bool in = zi < Di;
+    const float* src = xb + (int64_t)(in ? zi : 0) * plane;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const bool ok = in && gof[j] >= 0;
+      const float4 v = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
+      rg[j] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int zi) {
+    float* d = ring + (zi & 1) * SS;
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+      if (lof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+  };
+  __syncthreads();
+  load(z0);
+  store(z0);
+  load(z0 + 1);
+  const int npos = YB * Wi, ntile = (npos + 15) / 16;
+  const int pz = g >> 1, py = g & 1;  // the two parities this wave reduces and stores: (pz, py, 0 / 1)
+  float bm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bm[r] = a.bias ? a.bias[4 * ks + r] : 0.f;
+  const int64_t oplane = 4 * plane, orow = 2 * Wi;
+  float* yb0 = a.y + (int64_t)n * 16 * (2 * Di) * oplane;
+  int buf = 0;
+  for (int z = z0; z < z1; ++z) {
+    store(z + 1);  // slot (z + 1) & 1 last held plane z - 1, read before the previous step's last barrier
+    __syncthreads();
+    if (z + 1 < z1) load(z + 2);
+    const float* sz[2] = {ring + (z & 1) * SS, ring + ((z + 1) & 1) * SS};
+    for (int tI = 0; tI < ntile; ++tI) {
+      const int p = 16 * tI + li, pc = p < npos ? p : npos - 1;
+      const int yy = pc / Wi, xx = pc - yy * Wi;
+      const int bl = (4 * 0 + ks) * RX + yy * PX + xx + 16 * g * RX;
+      f32x4 acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz)
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const int t = tz * 9 + ty * 3 + tx;
+            const int par = (tz != 1) * 4 + (ty != 1) * 2 + (tx != 1);
+            const float* s = sz[tz == 0] + bl + (ty == 0) * PX + (tx == 0);
+#pragma unroll
+            for (int cq = 0; cq < 4; ++cq)
+              acc[par] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], s[4 * cq * RX], acc[par], 0, 0, 0);
+          }
+      // partial tiles: C layout column = position li, rows m = 4 ks + r
+      float* pw = part + (buf * 4 + g) * 8 * 256;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[q * 256 + (4 * ks + r) * 16 + li] = acc[q][r];
+      __syncthreads();
+      // wave g: parities (pz, py, 0) and (pz, py, 1) summed over the 4 groups
+      const float* pr = part + buf * 4 * 8 * 256;
+      const int q0 = pz * 4 + py * 2;
+      const bool okp = p < npos && y0 + yy < Hi;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * ks + r, e = m * 16 + li;
+        float v0 = bm[r], v1 = bm[r];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          v0 += pr[(v * 8 + q0) * 256 + e];
+          v1 += pr[(v * 8 + q0 + 1) * 256 + e];
+        }
+        if (okp)
+          *reinterpret_cast<float2*>(yb0 + ((int64_t)m * (2 * Di) + 2 * z + pz) * oplane +
+                                     (int64_t)(2 * (y0 + yy) + py) * orow + 2 * xx) = make_float2(v0, v1);
+      }
+      buf ^= 1;
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+// ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward:
+// x [N][64][Di][Hi][Wi] -> y [N][16][2Di][2Hi][2Wi]; weight [64][16][3][3][3] as the module holds it,
+// bias [16] or NULL; Wi % 4 == 0, Wi <= 64.  (csrc/conv_up.hip, k_convT_mfma64)
+int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, float* y, int N, int Di, int Hi, int Wi,
+                          void* stream) {
+  if (!x || !W || !y || N < 1 || Di < 1 || Hi < 1 || Wi < 1) return TB_ERR_INVALID_ARG;
+  if (Wi % 4 != 0 || Wi > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0 || (reinterpret_cast<uintptr_t>(y) & 7) != 0)
+    return TB_ERR_UNSUPPORTED_SIZE;
+  constexpr int YB = 2;
+  T64Args a{};
+  a.x = x, a.W = W, a.bias = bias, a.y = y, a.Di = Di, a.Hi = Hi, a.Wi = Wi;
+  a.PX = Wi + 4;
+  a.RX = (YB + 1) * a.PX;
+  while ((a.RX & 31) != 16) ++a.RX;
+  a.nyb = (Hi + YB - 1) / YB;
+  const size_t lds = (size_t)4 * (2 * 64 * a.RX + 2 * 4 * 8 * 256);
+  if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
+  a.zlen = zseg(Di, N * a.nyb, 1, 1);
+  a.ZS = (Di + a.zlen - 1) / a.zlen;
+  const int nl = (64 * (YB + 1) * (Wi / 4) + 255) / 256;
+  void (*kern)(T64Args) = nullptr;
+  switch (nl) {
+#define TB_NL(k) \
+  case k: kern = k_convT_mfma64<YB, k>; break;
+    TB_NL(1) TB_NL(2) TB_NL(3) TB_NL(4) TB_NL(5) TB_NL(6) TB_NL(7) TB_NL(8) TB_NL(9) TB_NL(10) TB_NL(11) TB_NL(12)
+#undef TB_NL
+    default: return TB_ERR_UNSUPPORTED_SIZE;
+  }
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
+      hipSuccess)
+    return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}

@@ -24,6 +24,7 @@ from ._lib import check, lib
 # TEXBIAS_WGRAD=0 leaves every layer to MIOpen (e.g. to compare with MIOpen's Find choice)
 MIN_K_PER_OUTPUT = 64
 ENABLED = os.environ.get("TEXBIAS_WGRAD", "1") != "0"
+CONVT64 = os.environ.get("TEXBIAS_CONVT64", "1") != "0"
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -103,7 +104,9 @@ def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, pa
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, padding, output_padding, transposed, fast_w):
-        if transposed:
+        if transposed and convT64_applies(x, w, stride, padding, output_padding):
+            y = convT_mfma64(x, w, b)
+        elif transposed:
             y = F.conv_transpose3d(x, w, b, stride, padding, output_padding)
         else:
             y = F.conv3d(x, w, b, stride, padding)
@@ -283,6 +286,27 @@ class _ConvTFewOutFn(torch.autograd.Function):
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = channel_sum(gy)
         return gx, gw, gb
+
+
+def convT_mfma64(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+    """ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward on the f32 matrix cores
+    (tb_convT3d_mfma64_f32; w as the module holds it, [64, 16, 3, 3, 3])."""
+    x = x.contiguous()
+    N, _, D, H, W = x.shape
+    y = torch.empty((N, 16, 2 * D, 2 * H, 2 * W), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device):
+        check(lib().tb_convT3d_mfma64_f32(x.data_ptr(), w.contiguous().data_ptr(),
+                                          b.data_ptr() if b is not None else None, y.data_ptr(), N, D, H, W,
+                                          _stream(x)), "tb_convT3d_mfma64_f32")
+    return y
+
+
+def convT64_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, output_padding) -> bool:
+    """ConvTranspose3d(64 -> 16, 3, 2, 1, output_padding 1), rows of 4k <= 64 floats: forward on
+    k_convT_mfma64 (TEXBIAS_CONVT64=0: ATen).  Input and weight gradients stay where _ConvFn puts them."""
+    return CONVT64 and custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape) == (64, 16, 3, 3, 3) and \
+        tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and tuple(output_padding) == (1, 1, 1) and \
+        x.shape[-1] % 4 == 0 and x.shape[-1] <= 64 and x.data_ptr() % 16 == 0
 
 
 def conv_fwd16(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:

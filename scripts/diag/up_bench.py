@@ -42,3 +42,9 @@ t = timeit(lambda: C.conv_fwd16(x16, w16, None))
 print(f"conv_fwd16 16->16 (120x120x80)            {t:8.1f} us  {2 * 16 * 16 * 27 * 2 * 120 * 120 * 80 / t / 1e6:6.1f} TF/s")
 t = timeit(lambda: torch.nn.functional.conv3d(x16, w16, None, padding=1))
 print(f"  MIOpen conv3d 16->16                    {t:8.1f} us")
+x64 = torch.randn((2, 64, 60, 60, 40), device="cuda")
+w64 = torch.randn((64, 16, 3, 3, 3), device="cuda")
+t = timeit(lambda: C.convT_mfma64(x64, w64, None))
+print(f"convT_mfma64 64->16 (up1 convT fwd)       {t:8.1f} us  {2 * 64 * 16 * 27 * 2 * 60 * 60 * 40 / t / 1e6:6.1f} TF/s")
+t = timeit(lambda: torch.nn.functional.conv_transpose3d(x64, w64, None, stride=2, padding=1, output_padding=1))
+print(f"  MIOpen conv_transpose3d 64->16          {t:8.1f} us")

@@ -110,3 +110,28 @@ def test_conv16_mfma(conv, shape):
     gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
     close64(gx, gxr, gx64)
     close64(gw, gwr, gw64)
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 4, 8), (2, 5, 6, 40), (1, 4, 3, 16), (2, 60, 60, 40)])
+def test_convT64_mfma(conv, shape):
+    """ConvTranspose3d(64 -> 16, stride 2) forward on k_convT_mfma64 (sub-pixel, f32 matrix cores) vs
+    ATen and float64; the C3 up1 shape is the last case."""
+    torch.manual_seed(4)
+    x = torch.randn((shape[0], 64) + shape[1:], device="cuda", requires_grad=True)
+    ours = conv.ConvTranspose3d(64, 16, 3, stride=2, padding=1, output_padding=1).cuda()
+    assert conv.convT64_applies(x, ours.weight, ours.stride, ours.padding, ours.output_padding)
+    ref = nn.ConvTranspose3d(64, 16, 3, stride=2, padding=1, output_padding=1).cuda()
+    ref.load_state_dict(ours.state_dict())
+    y, yr = ours(x), ref(x)
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = ref.weight.detach().double().requires_grad_(True)
+    y64 = F.conv_transpose3d(x64, w64, ref.bias.double(), stride=2, padding=1, output_padding=1)
+    close64(y, yr, y64)
+    if shape[1] > 10:
+        return  # the gradients are _ConvFn's (ATen input gradient, z-march weight gradient), tested elsewhere
+    g = torch.randn_like(y)
+    gx, gw = torch.autograd.grad(y, (x, ours.weight), g)
+    gxr, gwr = torch.autograd.grad(yr, (x, ref.weight), g)
+    gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
+    close64(gx, gxr, gx64)
+    close64(gw, gwr, gw64)
