@@ -243,6 +243,14 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
 int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, float* y, int N, int Di, int Hi, int Wi,
                           void* stream);
 
+/* Conv3d(C -> C, 3, stride 1, padding 1) forward for C = 32 or 64 on the f32 matrix cores (the input
+ * channels split over the block's waves, partial tiles summed in LDS): x [N][C][D][H][W] -> y,
+ * weight [C][C][3][3][3], bias [C] or NULL; W % 4 == 0, W <= 64 (C = 64: W <= 48), x 16-B aligned.
+ * The input gradient of the layer is the same call with the flipped, transposed weight.  The U-Net's
+ * 32- and 64-channel units of the train step (stylized_gibbs12p5.py:192-243, MONAI UNet). */
+int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float* y, int N, int C, int D, int H, int Wd,
+                       void* stream);
+
 /*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
  * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution

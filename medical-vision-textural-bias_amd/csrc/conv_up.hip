@@ -726,3 +726,187 @@ int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, flo
   hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
+
+// ------------------------------------------------- stride-1 3x3x3 conv, C -> C channels (C = 32, 64), on MFMA
+// The k_conv3d_fwd16 product with the input channels split over the block's waves: wave w holds the A
+// fragments (108 registers) of channel group g = w % G (16 channels) for output tile m = w / G of the
+// block's 4 / G; it accumulates NC position tiles at once (NC independent chains; positions = the
+// flattened (row, column) of the block's YB rows, so rows need not be a multiple of 16) and the G
+// groups' partial tiles meet in LDS, where the waves sum them and store.  A 3-slot plane ring as in
+// k_conv3d_fwd16.  The input gradient of the same layer is this kernel with W'[c][m][t] = W[m][c][26 - t].
+// Serves the U-Net's 32- and 64-channel units (60 x 60 x 40 and 30 x 30 x 20 at C3).
+namespace {
+struct S1Args {
+  const float* x;     // [N][C][D][H][W]
+  const float* W;     // [C m][C c][27]
+  const float* bias;  // [C] or null
+  float* y;
+  int D, H, Wd, YB;
+  int ZS, zlen, nyb, MG;  // z segments, row blocks, output-tile groups
+  int PX, RX;             // row pitch (data at column x + 4), channel pitch (16 mod 32)
+};
+
+template <int G, int NC, int NL>
+__global__ __launch_bounds__(256) void k_conv3d_mfma_s1(S1Args a) {
+  constexpr int CIN = 16 * G, MTB = 4 / G;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w % G, mt = w / G;
+  const int D = a.D, H = a.H, Wd = a.Wd, YB = a.YB, PX = a.PX, RX = a.RX, SS = CIN * RX;
+  const int NR = YB + 2;
+  float* ring = smem;            // [3][CIN][NR rows][PX]
+  float* part = smem + 3 * SS;   // [4 waves][NC][16 m][16 pos]
+  for (int i = tid; i < 3 * SS; i += 256) ring[i] = 0.f;
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int mg = b % a.MG;
+  b /= a.MG;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int COUT = 16 * MTB * a.MG;
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
+  const int li = lane & 15, ks = lane >> 4;
+  const int m0 = (mg * MTB + mt) * 16;
+  float af[108];
+#pragma unroll
+  for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[((m0 + li) * CIN + 16 * g + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
+  const int64_t plane = (int64_t)H * Wd, cstride = (int64_t)D * plane;
+  const float* xb = a.x + (int64_t)n * CIN * cstride;
+  const int W4 = Wd >> 2, per_c = NR * W4, total = CIN * per_c;
+  int gof[NL], lof[NL], gch[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + 256 * j;
+    const int c = i / per_c, r2 = i - c * per_c, r = r2 / W4, q = r2 - r * W4;
+    const int yi = y0 - 1 + r;
+    lof[j] = i < total ? c * RX + r * PX + 4 + 4 * q : -1;
+    gof[j] = (i < total && yi >= 0 && yi < H) ? yi * Wd + 4 * q : -1;
+    gch[j] = i < total ? c : 0;
+  }
+  float4 rg[NL];
+  auto load = [&](int zi) {
+    const bool in = zi >= 0 && zi < D;
+    const float* src = xb + (int64_t)(in ? zi : 0) * plane;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const bool ok = in && gof[j] >= 0;
+      const float4 v = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
+      rg[j] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int zi) {
+    float* d = ring + ((zi + 3) % 3) * SS;
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+      if (lof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+  };
+  __syncthreads();
+  load(z0 - 1);
+  store(z0 - 1);
+  load(z0);
+  store(z0);
+  load(z0 + 1);
+  const int npos = YB * Wd, ntile = (npos + 15) / 16;
+  float* ybase = a.y + (int64_t)n * COUT * cstride;
+  for (int z = z0; z < z1; ++z) {
+    store(z + 1);  // over plane z - 2, last read before the previous step's final barrier
+    __syncthreads();
+    if (z + 1 < z1) load(z + 2);
+    const float* sp[3] = {ring + ((z + 2) % 3) * SS, ring + (z % 3) * SS, ring + ((z + 1) % 3) * SS};
+    for (int t0 = 0; t0 < ntile; t0 += NC) {
+      int bl[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int p = 16 * (t0 + c) + li, pc = p < npos ? p : npos - 1;
+        const int yy = pc / Wd, xx = pc - yy * Wd;
+        bl[c] = (16 * g + ks) * RX + yy * PX + xx + 3;
+      }
+      f32x4 acc[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz)
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const int t = tz * 9 + ty * 3 + tx;
+            const float* s = sp[tz] + ty * PX + tx;
+#pragma unroll
+            for (int cq = 0; cq < 4; ++cq)
+#pragma unroll
+              for (int c = 0; c < NC; ++c)
+                acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], s[bl[c] + 4 * cq * RX], acc[c], 0, 0, 0);
+          }
+      float* pw = part + w * NC * 256;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[c * 256 + (4 * ks + r) * 16 + li] = acc[c][r];
+      __syncthreads();
+      // (output tile mt', chain c) combos over the 4 waves: the G groups' partials summed + bias
+      for (int k = w; k < MTB * NC; k += 4) {
+        const int mq = k / NC, c = k - mq * NC;
+        const int p = 16 * (t0 + c) + li;
+        const int yy = p / Wd, xx = p - yy * Wd;
+        const bool ok = t0 + c < ntile && p < npos && y0 + yy < H;
+        const int mb = (mg * MTB + mq) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 4 * ks + r;
+          float v = a.bias ? a.bias[mb + m] : 0.f;
+#pragma unroll
+          for (int gg = 0; gg < G; ++gg) v += part[((mq * G + gg) * NC + c) * 256 + m * 16 + li];
+          if (ok) ybase[(int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx] = v;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+}  // namespace
+
+// Conv3d(C -> C, 3, stride 1, padding 1) forward for C = 32 or 64: x [N][C][D][H][W] -> y, W % 4 == 0,
+// W <= 64; weight [C][C][27], bias [C] or NULL.  (csrc/conv_up.hip, k_conv3d_mfma_s1)
+int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float* y, int N, int C, int D, int H, int Wd,
+                       void* stream) {
+  if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
+  if ((C != 32 && C != 64) || Wd % 4 != 0 || Wd > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
+    return TB_ERR_UNSUPPORTED_SIZE;
+  constexpr int NC = 5;
+  const int G = C / 16;
+  S1Args a{};
+  a.x = x, a.W = W, a.bias = bias, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.PX = Wd + 8;
+  a.MG = G == 2 ? 1 : 4;  // 32: both output tiles in the block; 64: one tile per block, 4 block groups
+  size_t lds = 0;
+  int YB = (16 * NC + Wd - 1) / Wd;  // about NC tiles of positions per step
+  for (; YB >= 1; --YB) {
+    a.RX = (YB + 2) * a.PX;
+    while ((a.RX & 31) != 16) ++a.RX;
+    lds = (size_t)4 * (3 * C * a.RX + 4 * NC * 256);
+    if (lds <= 163840) break;
+  }
+  if (YB < 1) return TB_ERR_UNSUPPORTED_SIZE;
+  a.YB = YB > H ? H : YB;
+  a.nyb = (H + a.YB - 1) / a.YB;
+  a.zlen = zseg(D, N * a.nyb * a.MG, 1, 2);
+  a.ZS = (D + a.zlen - 1) / a.zlen;
+  const int nl = (C * (a.YB + 2) * (Wd / 4) + 255) / 256;
+  void (*kern)(S1Args) = nullptr;
+#define TB_NL(k)                                                  \
+  case k: kern = G == 2 ? k_conv3d_mfma_s1<2, NC, k> : k_conv3d_mfma_s1<4, NC, k>; break;
+  switch (nl) {
+    TB_NL(1) TB_NL(2) TB_NL(3) TB_NL(4) TB_NL(5) TB_NL(6) TB_NL(7) TB_NL(8) TB_NL(9) TB_NL(10) TB_NL(11) TB_NL(12)
+    default: return TB_ERR_UNSUPPORTED_SIZE;
+  }
+#undef TB_NL
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
+      hipSuccess)
+    return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.MG * a.ZS)), dim3(256), lds,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}

@@ -25,6 +25,7 @@ from ._lib import check, lib
 MIN_K_PER_OUTPUT = 64
 ENABLED = os.environ.get("TEXBIAS_WGRAD", "1") != "0"
 CONVT64 = os.environ.get("TEXBIAS_CONVT64", "1") != "0"
+CONVMFMA = os.environ.get("TEXBIAS_CONVMFMA", "1") != "0"
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -353,11 +354,63 @@ class _Conv16Fn(torch.autograd.Function):
         return gx, gw, gb
 
 
+def conv_mfma(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+    """Conv3d(C -> C, 3, stride 1, padding 1), C = 32 or 64, forward on the f32 matrix cores
+    (tb_conv3d_mfma_f32)."""
+    x = x.contiguous()
+    N, C, D, H, W = x.shape
+    y = torch.empty_like(x)
+    with torch.cuda.device(x.device):
+        check(lib().tb_conv3d_mfma_f32(x.data_ptr(), w.contiguous().data_ptr(), b.data_ptr() if b is not None else None,
+                                       y.data_ptr(), N, C, D, H, W, _stream(x)), "tb_conv3d_mfma_f32")
+    return y
+
+
+def conv_mfma_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
+    """Conv3d(32 -> 32) with rows of 4k <= 64 floats, or Conv3d(64 -> 64) with rows <= 48, stride 1,
+    padding 1: k_conv3d_mfma_s1 (forward and input gradient) + the z-marching weight gradient
+    (TEXBIAS_CONVMFMA=0: _ConvFn)."""
+    if not (custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3)):
+        return False
+    C = w.shape[0]
+    return C in (32, 64) and w.shape[1] == C and tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and \
+        x.shape[-1] % 4 == 0 and x.shape[-1] <= (64 if C == 32 else 48) and x.data_ptr() % 16 == 0 and CONVMFMA
+
+
+class _ConvMfmaFn(torch.autograd.Function):
+    """Conv3d(C -> C, stride 1), C = 32 or 64: forward and input gradient (flipped, transposed weights)
+    on the channel-split MFMA kernel, weight gradient on the z-marching MFMA kernel, bias gradient on
+    the channel-sum kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = conv_mfma(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = conv_mfma(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+        if ctx.needs_input_grad[1]:
+            gw = wgrad(gy, x, w.shape, 1, 1)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = channel_sum(gy)
+        return gx, gw, gb
+
+
 class Conv3d(nn.Conv3d):
     def forward(self, x):
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
                 conv16_applies(x, self.weight, self.stride, self.padding):
             return _Conv16Fn.apply(x, self.weight, self.bias)
+        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
+                conv_mfma_applies(x, self.weight, self.stride, self.padding):
+            return _ConvMfmaFn.apply(x, self.weight, self.bias)
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
                 s2_fewin_applies(x, self.weight, self.stride, self.padding):
             return _ConvS2FewInFn.apply(x, self.weight, self.bias)

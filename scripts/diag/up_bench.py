@@ -48,3 +48,11 @@ t = timeit(lambda: C.convT_mfma64(x64, w64, None))
 print(f"convT_mfma64 64->16 (up1 convT fwd)       {t:8.1f} us  {2 * 64 * 16 * 27 * 2 * 60 * 60 * 40 / t / 1e6:6.1f} TF/s")
 t = timeit(lambda: torch.nn.functional.conv_transpose3d(x64, w64, None, stride=2, padding=1, output_padding=1))
 print(f"  MIOpen conv_transpose3d 64->16          {t:8.1f} us")
+for ch, sh in ((32, (2, 32, 60, 60, 40)), (64, (2, 64, 30, 30, 20))):
+    xc = torch.randn(sh, device="cuda")
+    wc = torch.randn((ch, ch, 3, 3, 3), device="cuda")
+    fl = 2 * ch * ch * 27 * 2 * sh[2] * sh[3] * sh[4]
+    t = timeit(lambda: C.conv_mfma(xc, wc, None))
+    print(f"conv_mfma {ch}->{ch} {sh[2:]}        {t:8.1f} us  {fl / t / 1e6:6.1f} TF/s")
+    t = timeit(lambda: torch.nn.functional.conv3d(xc, wc, None, padding=1))
+    print(f"  MIOpen conv3d {ch}->{ch}                    {t:8.1f} us")

@@ -135,3 +135,28 @@ def test_convT64_mfma(conv, shape):
     gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
     close64(gx, gxr, gx64)
     close64(gw, gwr, gw64)
+
+
+@pytest.mark.parametrize("C,shape", [(32, (1, 5, 4, 40)), (32, (2, 3, 7, 12)), (64, (1, 4, 5, 20)), (64, (2, 3, 3, 8)),
+                                     (32, (2, 60, 60, 40)), (64, (2, 30, 30, 20)), (32, (1, 4, 3, 64)),
+                                     (64, (1, 3, 4, 48))])
+def test_conv_mfma(conv, C, shape):
+    """Conv3d(C -> C, stride 1), C = 32 / 64: forward and input gradient on k_conv3d_mfma_s1 (weight
+    gradient: z-march) vs ATen and float64; the C3 shapes of the 32- and 64-channel units included."""
+    torch.manual_seed(5)
+    x = torch.randn((shape[0], C) + shape[1:], device="cuda", requires_grad=True)
+    ours = conv.Conv3d(C, C, 3, padding=1).cuda()
+    assert conv.conv_mfma_applies(x, ours.weight, ours.stride, ours.padding)
+    ref = nn.Conv3d(C, C, 3, padding=1).cuda()
+    ref.load_state_dict(ours.state_dict())
+    y, yr = ours(x), ref(x)
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = ref.weight.detach().double().requires_grad_(True)
+    y64 = F.conv3d(x64, w64, ref.bias.double(), padding=1)
+    close64(y, yr, y64)
+    g = torch.randn_like(y)
+    gx, gw = torch.autograd.grad(y, (x, ours.weight), g)
+    gxr, gwr = torch.autograd.grad(yr, (x, ref.weight), g)
+    gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
+    close64(gx, gxr, gx64)
+    close64(gw, gwr, gw64)
