@@ -242,6 +242,10 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
  * layer of the train step (10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-243, MONAI UNet). */
 int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, float* y, int N, int Di, int Hi, int Wi,
                           void* stream);
+/* The same for Cin = 32 or 64 (Cin -> 16); with a Conv3d(16 -> Cin, 3, s2, p1) layer's weight it is
+ * that layer's input gradient (dX = conv_transpose3d(dY, W)). */
+int tb_convT3d_mfma_f32(const float* x, const float* W, const float* bias, float* y, int N, int Cin, int Di, int Hi,
+                        int Wi, void* stream);
 
 /* Conv3d(C -> C, 3, stride 1, padding 1) forward for C = 32 or 64 on the f32 matrix cores (the input
  * channels split over the block's waves, partial tiles summed in LDS): x [N][C][D][H][W] -> y,

@@ -571,14 +571,17 @@ struct T64Args {
   int PX, RX;         // staged row pitch (data at columns 0 .. Wi - 1, zeros after), channel pitch (16 mod 32)
 };
 
-template <int YB, int NL>  // NL: float4 staging pieces per thread (64 (YB + 1) Wi / 4 <= 256 NL)
+// G channel groups (Cin = 16 G): with G = 2 the waves (g, h) also split the position tiles (h = tile parity).
+template <int G, int YB, int NL>  // NL: float4 staging pieces per thread (Cin (YB + 1) Wi / 4 <= 256 NL)
 __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NR = YB + 1;  // staged rows: y0 .. y0 + YB
+  constexpr int CIN = 16 * G, HT = 4 / G;
   const int tid = (int)threadIdx.x, lane = tid & 63;
-  const int g = __builtin_amdgcn_readfirstlane(tid >> 6);  // channel group of this wave
-  const int Di = a.Di, Hi = a.Hi, Wi = a.Wi, PX = a.PX, RX = a.RX, SS = 64 * RX;
-  float* ring = smem;                   // [2][64 c][NR][PX]
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w % G, h = w / G;  // channel group, tile phase of this wave
+  const int Di = a.Di, Hi = a.Hi, Wi = a.Wi, PX = a.PX, RX = a.RX, SS = CIN * RX;
+  float* ring = smem;                   // [2][Cin][NR][PX]
   float* part = smem + 2 * SS;          // [2 buf][4 waves][8 parities][16 m][16 pos]
   for (int i = tid; i < 2 * SS; i += 256) ring[i] = 0.f;
   int b = (int)blockIdx.x;
@@ -592,10 +595,10 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
 #pragma unroll
   for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[((16 * g + 4 * (kk & 3) + ks) * 16 + li) * 27 + (kk >> 2)];
   const int64_t plane = (int64_t)Hi * Wi;
-  const float* xb = a.x + (int64_t)n * 64 * Di * plane;
+  const float* xb = a.x + (int64_t)n * CIN * Di * plane;
   // staging: float4 pieces of (channel, row, column quad); Wi % 4 == 0.  gof: offset in the
   // channel-plane's floats (-1: a row past Hi, staged as zeros), lof: LDS offset (-1: no piece)
-  const int W4 = Wi >> 2, per_c = NR * W4, total = 64 * per_c;
+  const int W4 = Wi >> 2, per_c = NR * W4, total = CIN * per_c;
   const int64_t cstride = (int64_t)Di * plane;
   int gof[NL], lof[NL], gch[NL];
 #pragma unroll
@@ -629,7 +632,6 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
   store(z0);
   load(z0 + 1);
   const int npos = YB * Wi, ntile = (npos + 15) / 16;
-  const int pz = g >> 1, py = g & 1;  // the two parities this wave reduces and stores: (pz, py, 0 / 1)
   float bm[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bm[r] = a.bias ? a.bias[4 * ks + r] : 0.f;
@@ -641,10 +643,11 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
     __syncthreads();
     if (z + 1 < z1) load(z + 2);
     const float* sz[2] = {ring + (z & 1) * SS, ring + ((z + 1) & 1) * SS};
-    for (int tI = 0; tI < ntile; ++tI) {
+    for (int t0 = 0; t0 < ntile; t0 += HT) {
+      const int tI = t0 + h;
       const int p = 16 * tI + li, pc = p < npos ? p : npos - 1;
       const int yy = pc / Wi, xx = pc - yy * Wi;
-      const int bl = (4 * 0 + ks) * RX + yy * PX + xx + 16 * g * RX;
+      const int bl = (16 * g + ks) * RX + yy * PX + xx;
       f32x4 acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -662,28 +665,31 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
               acc[par] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], s[4 * cq * RX], acc[par], 0, 0, 0);
           }
       // partial tiles: C layout column = position li, rows m = 4 ks + r
-      float* pw = part + (buf * 4 + g) * 8 * 256;
+      float* pw = part + (buf * 4 + w) * 8 * 256;
 #pragma unroll
       for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int r = 0; r < 4; ++r) pw[q * 256 + (4 * ks + r) * 16 + li] = acc[q][r];
       __syncthreads();
-      // wave g: parities (pz, py, 0) and (pz, py, 1) summed over the 4 groups
+      // (tile phase h', parity pair (pz, py, 0 / 1)) combos over the waves: the G groups' partials summed
       const float* pr = part + buf * 4 * 8 * 256;
-      const int q0 = pz * 4 + py * 2;
-      const bool okp = p < npos && y0 + yy < Hi;
+      for (int k = w; k < 4 * HT; k += 4) {
+        const int hq = k >> 2, pz = (k >> 1) & 1, py = k & 1, q0 = pz * 4 + py * 2;
+        const int pq = 16 * (t0 + hq) + li, yq = pq / Wi, xq = pq - yq * Wi;
+        const bool okp = t0 + hq < ntile && pq < npos && y0 + yq < Hi;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 4 * ks + r, e = m * 16 + li;
-        float v0 = bm[r], v1 = bm[r];
+        for (int r = 0; r < 4; ++r) {
+          const int m = 4 * ks + r, e = m * 16 + li;
+          float v0 = bm[r], v1 = bm[r];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          v0 += pr[(v * 8 + q0) * 256 + e];
-          v1 += pr[(v * 8 + q0 + 1) * 256 + e];
+          for (int v = 0; v < G; ++v) {
+            v0 += pr[((hq * G + v) * 8 + q0) * 256 + e];
+            v1 += pr[((hq * G + v) * 8 + q0 + 1) * 256 + e];
+          }
+          if (okp)
+            *reinterpret_cast<float2*>(yb0 + ((int64_t)m * (2 * Di) + 2 * z + pz) * oplane +
+                                       (int64_t)(2 * (y0 + yq) + py) * orow + 2 * xq) = make_float2(v0, v1);
         }
-        if (okp)
-          *reinterpret_cast<float2*>(yb0 + ((int64_t)m * (2 * Di) + 2 * z + pz) * oplane +
-                                     (int64_t)(2 * (y0 + yy) + py) * orow + 2 * xx) = make_float2(v0, v1);
       }
       buf ^= 1;
     }
@@ -697,7 +703,15 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
 // bias [16] or NULL; Wi % 4 == 0, Wi <= 64.  (csrc/conv_up.hip, k_convT_mfma64)
 int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, float* y, int N, int Di, int Hi, int Wi,
                           void* stream) {
+  return tb_convT3d_mfma_f32(x, W, bias, y, N, 64, Di, Hi, Wi, stream);
+}
+
+// ConvTranspose3d(Cin -> 16, 3, s2, p1, op1) forward for Cin = 32 or 64 (also the input gradient of
+// Conv3d(16 -> Cin, s2, p1) with that layer's weight); as tb_convT3d_mfma64_f32 otherwise.
+int tb_convT3d_mfma_f32(const float* x, const float* W, const float* bias, float* y, int N, int Cin, int Di, int Hi,
+                        int Wi, void* stream) {
   if (!x || !W || !y || N < 1 || Di < 1 || Hi < 1 || Wi < 1) return TB_ERR_INVALID_ARG;
+  if (Cin != 32 && Cin != 64) return TB_ERR_UNSUPPORTED_SIZE;
   if (Wi % 4 != 0 || Wi > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0 || (reinterpret_cast<uintptr_t>(y) & 7) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
   constexpr int YB = 2;
@@ -707,15 +721,15 @@ int tb_convT3d_mfma64_f32(const float* x, const float* W, const float* bias, flo
   a.RX = (YB + 1) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;
   a.nyb = (Hi + YB - 1) / YB;
-  const size_t lds = (size_t)4 * (2 * 64 * a.RX + 2 * 4 * 8 * 256);
+  const size_t lds = (size_t)4 * (2 * Cin * a.RX + 2 * 4 * 8 * 256);
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
   a.zlen = zseg(Di, N * a.nyb, 1, 1);
   a.ZS = (Di + a.zlen - 1) / a.zlen;
-  const int nl = (64 * (YB + 1) * (Wi / 4) + 255) / 256;
+  const int nl = (Cin * (YB + 1) * (Wi / 4) + 255) / 256;
   void (*kern)(T64Args) = nullptr;
   switch (nl) {
 #define TB_NL(k) \
-  case k: kern = k_convT_mfma64<YB, k>; break;
+  case k: kern = Cin == 64 ? k_convT_mfma64<4, YB, k> : k_convT_mfma64<2, YB, k>; break;
     TB_NL(1) TB_NL(2) TB_NL(3) TB_NL(4) TB_NL(5) TB_NL(6) TB_NL(7) TB_NL(8) TB_NL(9) TB_NL(10) TB_NL(11) TB_NL(12)
 #undef TB_NL
     default: return TB_ERR_UNSUPPORTED_SIZE;

@@ -51,6 +51,7 @@ def _proto(L):
         "tb_convT3d_fewout_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
         "tb_conv3d_fwd16_f32": (I, [P, P, P, P] + [I] * 4 + [P]),
         "tb_convT3d_mfma64_f32": (I, [P, P, P, P] + [I] * 4 + [P]),
+        "tb_convT3d_mfma_f32": (I, [P, P, P, P] + [I] * 5 + [P]),
         "tb_conv3d_mfma_f32": (I, [P, P, P, P] + [I] * 5 + [P]),
         "tb_dice_sums_f32": (I, [P, P, P, I64, I64, I, I, P]),
         "tb_dice_sums_bwd_f32": (I, [P, P, P, P, I64, I64, I, I, P]),

@@ -106,7 +106,7 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, padding, output_padding, transposed, fast_w):
         if transposed and convT64_applies(x, w, stride, padding, output_padding):
-            y = convT_mfma64(x, w, b)
+            y = convT_mfma(x, w, b)
         elif transposed:
             y = F.conv_transpose3d(x, w, b, stride, padding, output_padding)
         else:
@@ -123,10 +123,14 @@ class _ConvFn(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         gx = gb = gw = None
         lib_w = need_w and not fast_w
+        if need_x and not transposed and s2_dgrad_applies(gy, x, w, stride, padding):
+            gx = convT_mfma(gy, w, None)  # Conv3d(16 -> 32, s2)'s input gradient on k_convT_mfma64
+            need_x = False
         if need_x or lib_w:
-            gx, gw, _ = torch.ops.aten.convolution_backward(
+            gxl, gw, _ = torch.ops.aten.convolution_backward(
                 gy, x, w, None, list(stride), list(padding), [1, 1, 1], transposed, list(output_padding), 1,
                 [need_x, lib_w, False])
+            gx = gxl if need_x else gx
         if need_w and fast_w:
             if transposed:   # dW[ci][co] = corr(x, gy)
                 gw = wgrad(x, gy, w.shape, stride[0], padding[0])
@@ -289,17 +293,28 @@ class _ConvTFewOutFn(torch.autograd.Function):
         return gx, gw, gb
 
 
-def convT_mfma64(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
-    """ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward on the f32 matrix cores
-    (tb_convT3d_mfma64_f32; w as the module holds it, [64, 16, 3, 3, 3])."""
+def convT_mfma(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+    """ConvTranspose3d(Cin -> 16, 3, stride 2, padding 1, output_padding 1), Cin = 32 or 64, forward on the
+    f32 matrix cores (tb_convT3d_mfma_f32; w [Cin, 16, 3, 3, 3] as the module holds it)."""
     x = x.contiguous()
-    N, _, D, H, W = x.shape
+    N, Cin, D, H, W = x.shape
     y = torch.empty((N, 16, 2 * D, 2 * H, 2 * W), dtype=torch.float32, device=x.device)
     with torch.cuda.device(x.device):
-        check(lib().tb_convT3d_mfma64_f32(x.data_ptr(), w.contiguous().data_ptr(),
-                                          b.data_ptr() if b is not None else None, y.data_ptr(), N, D, H, W,
-                                          _stream(x)), "tb_convT3d_mfma64_f32")
+        check(lib().tb_convT3d_mfma_f32(x.data_ptr(), w.contiguous().data_ptr(),
+                                        b.data_ptr() if b is not None else None, y.data_ptr(), N, Cin, D, H, W,
+                                        _stream(x)), "tb_convT3d_mfma_f32")
     return y
+
+
+convT_mfma64 = convT_mfma
+
+
+def s2_dgrad_applies(gy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
+    """Conv3d(16 -> 32, 3, stride 2, padding 1) on even extents: its input gradient is
+    conv_transpose3d(dY, W) with output_padding 1, i.e. k_convT_mfma64 with 32 input channels."""
+    return CONVT64 and tuple(w.shape) == (32, 16, 3, 3, 3) and tuple(stride) == (2, 2, 2) and \
+        tuple(padding) == (1, 1, 1) and gy.dim() == 5 and all(2 * a == b for a, b in zip(gy.shape[2:], x.shape[2:])) and \
+        gy.shape[-1] % 4 == 0 and gy.shape[-1] <= 64 and gy.data_ptr() % 16 == 0
 
 
 def convT64_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, output_padding) -> bool:

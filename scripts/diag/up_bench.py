@@ -56,3 +56,9 @@ for ch, sh in ((32, (2, 32, 60, 60, 40)), (64, (2, 64, 30, 30, 20))):
     print(f"conv_mfma {ch}->{ch} {sh[2:]}        {t:8.1f} us  {fl / t / 1e6:6.1f} TF/s")
     t = timeit(lambda: torch.nn.functional.conv3d(xc, wc, None, padding=1))
     print(f"  MIOpen conv3d {ch}->{ch}                    {t:8.1f} us")
+gy32 = torch.randn((2, 32, 60, 60, 40), device="cuda")
+w32 = torch.randn((32, 16, 3, 3, 3), device="cuda")
+t = timeit(lambda: C.convT_mfma(gy32, w32, None))
+print(f"convT_mfma 32->16 (down1 s2 dgrad)        {t:8.1f} us  {2 * 32 * 16 * 27 * 2 * 60 * 60 * 40 / t / 1e6:6.1f} TF/s")
+t = timeit(lambda: torch.nn.functional.conv_transpose3d(gy32, w32, None, stride=2, padding=1, output_padding=1))
+print(f"  MIOpen conv_transpose3d 32->16          {t:8.1f} us")

@@ -160,3 +160,23 @@ def test_conv_mfma(conv, C, shape):
     gx64, gw64 = torch.autograd.grad(y64, (x64, w64), g.double())
     close64(gx, gxr, gx64)
     close64(gw, gwr, gw64)
+
+
+@pytest.mark.parametrize("shape", [(1, 6, 8, 16), (2, 10, 6, 24), (2, 120, 120, 80)])
+def test_s2_dgrad_mfma(conv, shape):
+    """Conv3d(16 -> 32, stride 2): its input gradient on k_convT_mfma64 with 32 input channels vs ATen
+    and float64 (the C3 down1 shape last)."""
+    torch.manual_seed(6)
+    x = torch.randn((shape[0], 16) + shape[1:], device="cuda", requires_grad=True)
+    ours = conv.Conv3d(16, 32, 3, stride=2, padding=1).cuda()
+    ref = nn.Conv3d(16, 32, 3, stride=2, padding=1).cuda()
+    ref.load_state_dict(ours.state_dict())
+    y, yr = ours(x), ref(x)
+    g = torch.randn_like(y)
+    assert conv.s2_dgrad_applies(g, x, ours.weight, ours.stride, ours.padding)
+    gx, = torch.autograd.grad(y, (x,), g)
+    gxr, = torch.autograd.grad(yr, (x,), g)
+    x64 = x.detach().double().requires_grad_(True)
+    y64 = F.conv3d(x64, ref.weight.double(), ref.bias.double(), stride=2, padding=1)
+    gx64, = torch.autograd.grad(y64, (x64,), g.double())
+    close64(gx, gxr, gx64)
