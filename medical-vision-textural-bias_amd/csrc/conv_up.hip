@@ -395,15 +395,16 @@ struct F16Args {
   int PX, RX;  // row pitch (data at column x + 4), channel pitch (= 16 mod 32)
 };
 
-template <int YB, int NXT>  // output rows per block; 16-column tiles per row (W = 16 NXT)
-__global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
+template <int YB, int NXT, int NTH>  // output rows per block; 16-column tiles per row (W = 16 NXT); threads
+__global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {
+  constexpr int NWV = NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NR = YB + 2, W4 = 4 * NXT;  // staged rows; float4 per row
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int D = a.D, H = a.H, Wd = a.Wd, PX = a.PX, RX = a.RX, SS = 16 * RX;
   float* ring = smem;  // [3][16 c][NR][PX]
-  for (int i = tid; i < 3 * SS; i += 256) ring[i] = 0.f;
+  for (int i = tid; i < 3 * SS; i += NTH) ring[i] = 0.f;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -417,11 +418,11 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
   for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[(li * 16 + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
   const int64_t plane = (int64_t)H * Wd, plane4 = plane / 4;
   const float4* xb = reinterpret_cast<const float4*>(a.x + (int64_t)n * 16 * D * plane);
-  constexpr int NL = (16 * NR * W4 + 255) / 256;
+  constexpr int NL = (16 * NR * W4 + NTH - 1) / NTH;
   int gof[NL], lof[NL];
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NTH * j;
     const int q = i % W4, t = i / W4, r = t % NR, c = t / NR;
     const int yi = y0 - 1 + r;
     const bool ok = i < 16 * NR * W4 && yi >= 0 && yi < H;
@@ -464,8 +465,8 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd16(F16Args a) {
     const float* s0 = ring + ((z + 2) % 3) * SS + bl;  // tz = 0: plane z - 1
     const float* s1 = ring + (z % 3) * SS + bl;
     const float* s2 = ring + ((z + 1) % 3) * SS + bl;
-    for (int t0 = wave; t0 < NT; t0 += 8) {  // tiles t0 and t0 + 4 of this wave
-      const int t1 = t0 + 4 < NT ? t0 + 4 : t0;
+    for (int t0 = wave; t0 < NT; t0 += 2 * NWV) {  // tiles t0 and t0 + NWV of this wave
+      const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
       const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
       const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
       const int o0 = yy0 * PX + x00, o1 = yy1 * PX + x01;
@@ -527,24 +528,30 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
   a.zlen = zseg(D, N * a.nyb, per_cu, 2);
   a.ZS = (D + a.zlen - 1) / a.zlen;
   void (*kern)(F16Args) = nullptr;
-#define TB_F16(Y)                                        \
-  if (YB == Y) switch (Wd / 16) {                        \
-      case 1: kern = k_conv3d_fwd16<Y, 1>; break;        \
-      case 2: kern = k_conv3d_fwd16<Y, 2>; break;        \
-      case 3: kern = k_conv3d_fwd16<Y, 3>; break;        \
-      case 4: kern = k_conv3d_fwd16<Y, 4>; break;        \
-      case 5: kern = k_conv3d_fwd16<Y, 5>; break;        \
-      case 6: kern = k_conv3d_fwd16<Y, 6>; break;        \
-      case 7: kern = k_conv3d_fwd16<Y, 7>; break;        \
-      case 8: kern = k_conv3d_fwd16<Y, 8>; break;        \
-      default: return TB_ERR_UNSUPPORTED_SIZE;           \
+  // threads per block (TEXBIAS_CONV16_NT 256 | 512): 8 waves, 2 per SIMD sharing the matrix core, hide
+  // the B-fragment LDS reads the compiler issues only 1-3 ahead (YB = 3: 421 -> 365 us per C3 call)
+  static const int NTv = [] {
+    const char* e = std::getenv("TEXBIAS_CONV16_NT");
+    return e && std::atoi(e) == 256 ? 256 : 512;
+  }();
+#define TB_F16(Y, T)                                        \
+  if (YB == Y && NTv == T) switch (Wd / 16) {               \
+      case 1: kern = k_conv3d_fwd16<Y, 1, T>; break;        \
+      case 2: kern = k_conv3d_fwd16<Y, 2, T>; break;        \
+      case 3: kern = k_conv3d_fwd16<Y, 3, T>; break;        \
+      case 4: kern = k_conv3d_fwd16<Y, 4, T>; break;        \
+      case 5: kern = k_conv3d_fwd16<Y, 5, T>; break;        \
+      case 6: kern = k_conv3d_fwd16<Y, 6, T>; break;        \
+      case 7: kern = k_conv3d_fwd16<Y, 7, T>; break;        \
+      case 8: kern = k_conv3d_fwd16<Y, 8, T>; break;        \
+      default: return TB_ERR_UNSUPPORTED_SIZE;              \
     }
-  TB_F16(2) TB_F16(3) TB_F16(4)
+  TB_F16(2, 256) TB_F16(3, 256) TB_F16(4, 256) TB_F16(2, 512) TB_F16(3, 512) TB_F16(4, 512)
 #undef TB_F16
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(256), lds, reinterpret_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(NTv), lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
