@@ -767,18 +767,18 @@ struct S1Args {
   int PX, RX;             // row pitch (data at column x + 4), channel pitch (16 mod 32)
 };
 
-template <int G, int NC, int NL>
-__global__ __launch_bounds__(256) void k_conv3d_mfma_s1(S1Args a) {
-  constexpr int CIN = 16 * G, MTB = 4 / G;
+template <int G, int NC, int NL, int NTH>  // NTH 512: two waves per role, alternate tiles (NWG phases)
+__global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {
+  constexpr int CIN = 16 * G, MTB = 4 / G, NWG = NTH / 256;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = w % G, mt = w / G;
+  const int g = w % G, mt = (w / G) % MTB, h = w / 4;
   const int D = a.D, H = a.H, Wd = a.Wd, YB = a.YB, PX = a.PX, RX = a.RX, SS = CIN * RX;
   const int NR = YB + 2;
   float* ring = smem;            // [3][CIN][NR rows][PX]
-  float* part = smem + 3 * SS;   // [4 waves][NC][16 m][16 pos]
-  for (int i = tid; i < 3 * SS; i += 256) ring[i] = 0.f;
+  float* part = smem + 3 * SS;   // [NTH / 64 waves][NC][16 m][16 pos]
+  for (int i = tid; i < 3 * SS; i += NTH) ring[i] = 0.f;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -799,7 +799,7 @@ __global__ __launch_bounds__(256) void k_conv3d_mfma_s1(S1Args a) {
   int gof[NL], lof[NL], gch[NL];
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NTH * j;
     const int c = i / per_c, r2 = i - c * per_c, r = r2 / W4, q = r2 - r * W4;
     const int yi = y0 - 1 + r;
     lof[j] = i < total ? c * RX + r * PX + 4 + 4 * q : -1;
@@ -836,11 +836,11 @@ __global__ __launch_bounds__(256) void k_conv3d_mfma_s1(S1Args a) {
     __syncthreads();
     if (z + 1 < z1) load(z + 2);
     const float* sp[3] = {ring + ((z + 2) % 3) * SS, ring + (z % 3) * SS, ring + ((z + 1) % 3) * SS};
-    for (int t0 = 0; t0 < ntile; t0 += NC) {
+    for (int t0 = 0; t0 < ntile; t0 += NWG * NC) {  // chain c of this wave: tile t0 + NWG c + h
       int bl[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const int p = 16 * (t0 + c) + li, pc = p < npos ? p : npos - 1;
+        const int p = 16 * (t0 + NWG * c + h) + li, pc = p < npos ? p : npos - 1;
         const int yy = pc / Wd, xx = pc - yy * Wd;
         bl[c] = (16 * g + ks) * RX + yy * PX + xx + 3;
       }
@@ -867,19 +867,20 @@ __global__ __launch_bounds__(256) void k_conv3d_mfma_s1(S1Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) pw[c * 256 + (4 * ks + r) * 16 + li] = acc[c][r];
       __syncthreads();
-      // (output tile mt', chain c) combos over the 4 waves: the G groups' partials summed + bias
-      for (int k = w; k < MTB * NC; k += 4) {
-        const int mq = k / NC, c = k - mq * NC;
-        const int p = 16 * (t0 + c) + li;
+      // (output tile mt', phase h', chain c) combos over the waves: the G groups' partials summed + bias
+      for (int k = w; k < MTB * NWG * NC; k += NTH / 64) {
+        const int mq = k / (NWG * NC), r2 = k - mq * (NWG * NC), hq = r2 / NC, c = r2 - hq * NC;
+        const int tq = t0 + NWG * c + hq;
+        const int p = 16 * tq + li;
         const int yy = p / Wd, xx = p - yy * Wd;
-        const bool ok = t0 + c < ntile && p < npos && y0 + yy < H;
+        const bool ok = tq < ntile && p < npos && y0 + yy < H;
         const int mb = (mg * MTB + mq) * 16;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 4 * ks + r;
           float v = a.bias ? a.bias[mb + m] : 0.f;
 #pragma unroll
-          for (int gg = 0; gg < G; ++gg) v += part[((mq * G + gg) * NC + c) * 256 + m * 16 + li];
+          for (int gg = 0; gg < G; ++gg) v += part[((hq * 4 + mq * G + gg) * NC + c) * 256 + m * 16 + li];
           if (ok) ybase[(int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx] = v;
         }
       }
@@ -896,18 +897,24 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if ((C != 32 && C != 64) || Wd % 4 != 0 || Wd > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
-  constexpr int NC = 5;
+  // 4 waves with 5 chains each (TEXBIAS_CONVMFMA_NT=512: 8 waves, two per role on alternate tiles with
+  // 3 chains -- measured slower here, 245 vs 211 us at 32 -> 32, unlike k_conv3d_fwd16)
+  static const int NTv = [] {
+    const char* e = std::getenv("TEXBIAS_CONVMFMA_NT");
+    return e && std::atoi(e) == 512 ? 512 : 256;
+  }();
+  const int NC = NTv == 512 ? 3 : 5;
   const int G = C / 16;
   S1Args a{};
   a.x = x, a.W = W, a.bias = bias, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.PX = Wd + 8;
   a.MG = G == 2 ? 1 : 4;  // 32: both output tiles in the block; 64: one tile per block, 4 block groups
   size_t lds = 0;
-  int YB = (16 * NC + Wd - 1) / Wd;  // about NC tiles of positions per step
+  int YB = (16 * 5 + Wd - 1) / Wd;  // about 5 tiles of positions per step
   for (; YB >= 1; --YB) {
     a.RX = (YB + 2) * a.PX;
     while ((a.RX & 31) != 16) ++a.RX;
-    lds = (size_t)4 * (3 * C * a.RX + 4 * NC * 256);
+    lds = (size_t)4 * (3 * C * a.RX + (NTv / 64) * NC * 256);
     if (lds <= 163840) break;
   }
   if (YB < 1) return TB_ERR_UNSUPPORTED_SIZE;
@@ -915,10 +922,13 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
   a.nyb = (H + a.YB - 1) / a.YB;
   a.zlen = zseg(D, N * a.nyb * a.MG, 1, 2);
   a.ZS = (D + a.zlen - 1) / a.zlen;
-  const int nl = (C * (a.YB + 2) * (Wd / 4) + 255) / 256;
+  const int nl = (C * (a.YB + 2) * (Wd / 4) + NTv - 1) / NTv;
   void (*kern)(S1Args) = nullptr;
-#define TB_NL(k)                                                  \
-  case k: kern = G == 2 ? k_conv3d_mfma_s1<2, NC, k> : k_conv3d_mfma_s1<4, NC, k>; break;
+#define TB_NL(k)                                                                                           \
+  case k:                                                                                                  \
+    kern = NTv == 512 ? (G == 2 ? k_conv3d_mfma_s1<2, 3, k, 512> : k_conv3d_mfma_s1<4, 3, k, 512>)         \
+                      : (G == 2 ? k_conv3d_mfma_s1<2, 5, k, 256> : k_conv3d_mfma_s1<4, 5, k, 256>);        \
+    break;
   switch (nl) {
     TB_NL(1) TB_NL(2) TB_NL(3) TB_NL(4) TB_NL(5) TB_NL(6) TB_NL(7) TB_NL(8) TB_NL(9) TB_NL(10) TB_NL(11) TB_NL(12)
     default: return TB_ERR_UNSUPPORTED_SIZE;
@@ -927,7 +937,7 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.MG * a.ZS)), dim3(256), lds,
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.MG * a.ZS)), dim3(NTv), lds,
                      reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
