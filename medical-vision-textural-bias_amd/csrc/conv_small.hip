@@ -119,6 +119,13 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 #endif
 constexpr int ZB = TB_SMALL_ZB;  // output planes per block
 
+// weights of the z-march as scalar loads from the constant address space (SGPR operands of the FMAs)
+// instead of per-FMA-group LDS broadcast reads (TB_SMALL_SW=0: LDS)
+#ifndef TB_SMALL_SW
+#define TB_SMALL_SW 0
+#endif
+typedef const __attribute__((address_space(4))) float* cfloat_sp;
+
 template <int CI, int CO>
 __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__ x, const float* __restrict__ wt,
                                                        const float* __restrict__ bias, float* __restrict__ y, int D,
@@ -189,7 +196,8 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
           for (int co = 0; co < CO; ++co) {
 #pragma unroll
             for (int tx = 0; tx < 3; ++tx) {
-              const float wv = ws[(((co * CI + ci) * 3 + tz) * 3 + ty) * 3 + tx];
+              const int wi = (((co * CI + ci) * 3 + tz) * 3 + ty) * 3 + tx;
+              const float wv = TB_SMALL_SW ? ((cfloat_sp)wt)[wi] : ws[wi];
 #pragma unroll
               for (int k = 0; k < WPT; ++k) acc[co][k] = fmaf(wv, v[k + tx], acc[co][k]);
             }
