@@ -256,6 +256,33 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
                        void* stream);
 
 /*
+ * The U-Net's channel-deep convolutions as implicit GEMMs on the f32 matrix cores (csrc/conv_gemm.hip;
+ * train step of 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-243, MONAI UNet module tree
+ * source_code/test.ipynb:754-1010 -- the stride-2 entries 16 -> 32 .. 64 -> 128, the 128/256-channel
+ * bottom unit, the ConvTranspose3d ups and every one of their input gradients, which MIOpen/CK ran at
+ * 23-51 TFLOP/s plus layout transposes).  x [N][Cin][D][H][Wd] with batch stride xsn (0: contiguous),
+ * channel stride D H Wd; y likewise with batch stride ysn (0: contiguous); bias [M] or NULL; add (or
+ * NULL) is summed into y (same layout as y, batch stride addsn; may alias y).  mode:
+ *   TB_CG_CONV  (0): Conv3d(Cin -> M, ksize 3 (padding 1) or 1 (padding 0), stride 1 or 2), W [M][Cin][k^3];
+ *   TB_CG_DGRAD (1): the input gradient of a stride-1 Conv3d(M -> Cin): x = dY [N][Cin][..], y = dX
+ *                    [N][M][..], W = that layer's weight [Cin][M][k^3] (flipped and transposed inside);
+ *   TB_CG_CONVT (2): ConvTranspose3d(Cin -> M, 3, stride 2, padding 1, output_padding 1) forward,
+ *                    W [Cin][M][27] as the module holds it, y [N][M][2D][2H][2Wd] -- also the input
+ *                    gradient of a stride-2 Conv3d(M -> Cin) with that layer's weight (x = dY, y = dX).
+ * Cin % 4 == 0, W 16-B aligned, every tensor < 2^31 elements.  ws: device scratch of
+ * tb_conv3d_gemm_workspace_bytes(...) bytes (packed weights, split-k partials; stream-ordered reuse).
+ * tb_conv3d_gemm_config: cfg[0..5] = BM, BP, k slices, k per slice, blocks, positions (host only).
+ */
+#define TB_CG_CONV 0
+#define TB_CG_DGRAD 1
+#define TB_CG_CONVT 2
+size_t tb_conv3d_gemm_workspace_bytes(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride, int ksize);
+int tb_conv3d_gemm_f32(int mode, const float* x, int64_t xsn, const float* W, const float* bias, const float* add,
+                       int64_t addsn, float* y, int64_t ysn, int N, int Cin, int M, int D, int H, int Wd, int stride,
+                       int ksize, void* ws, size_t ws_bytes, void* stream);
+int tb_conv3d_gemm_config(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride, int ksize, int64_t* cfg);
+
+/*
  * Fused InstanceNorm3d(affine=False, eps) + PReLU(one weight a) over NC instances of S contiguous
  * voxels (x as [N][C][D][H][W], NC = N*C) -- the "ADN" block after every U-Net convolution
  * (MONAI Convolution, used by 10_scripts/20_Gibbs_filters/stylized_gibbs12p5.py:192-199).

@@ -649,8 +649,8 @@ static bool band_plan(const tb_plan* p, const tb_sample_ops* ops, int s0, int s1
 
 enum { RUN_COPY = 0, RUN_FULL = 1, RUN_BAND = 2, RUN_POINT = 3, RUN_WRAP = 4 };
 
-// The run [s0, s1) takes the separable wrap route: every program wrap-only with the same alpha
-// product (one circulant table per launch), a shape the route takes, room for its partials.
+// The run [s0, s1) takes the separable wrap route: every program wrap-only (with the same alpha
+// product when D is odd: one circulant table per launch), a shape the route takes, room for its partials.
 static bool wrap_run(const tb_plan* p, const tb_sample_ops* ops, int s, int y_pad, size_t ws_bytes, float* alpha) {
   if (!g_wrap || ws_bytes < tb::wrap_ws_bytes()) return false;
   if (!tb::wrap_shape_ok(p->dev.H, p->dev.W, p->dev.D, y_pad)) return false;
@@ -937,7 +937,9 @@ static int kspace_filter(const tb_plan* p, const float* x, const int64_t* xs, fl
       Run run;
       run.route = route(b0 + i, &al0);
       int j = i + 1;
-      while (j < nb && route(b0 + j, &al) == run.route && (run.route != RUN_WRAP || al == al0)) ++j;
+      // odd D: one circulant table per launch (k_wrap_dgemm builds it from one alpha); even D: k_wrap_even
+      // carries every sample's 2-tap weights, so mixed alphas share the launch
+      while (j < nb && route(b0 + j, &al) == run.route && (run.route != RUN_WRAP || al == al0 || !(p->dev.D & 1))) ++j;
       run.s0 = b0 + i;
       run.s1 = b0 + j;
       if (run.route == RUN_FULL && g_point && ws_bytes >= tb::point_ws(B * C).total &&

@@ -53,6 +53,9 @@ def _proto(L):
         "tb_convT3d_mfma64_f32": (I, [P, P, P, P] + [I] * 4 + [P]),
         "tb_convT3d_mfma_f32": (I, [P, P, P, P] + [I] * 5 + [P]),
         "tb_conv3d_mfma_f32": (I, [P, P, P, P] + [I] * 5 + [P]),
+        "tb_conv3d_gemm_workspace_bytes": (SZ, [I] * 9),
+        "tb_conv3d_gemm_f32": (I, [I, P, I64, P, P, P, I64, P, I64] + [I] * 8 + [P, SZ, P]),
+        "tb_conv3d_gemm_config": (I, [I] * 9 + [P]),
         "tb_dice_sums_f32": (I, [P, P, P, I64, I64, I, I, P]),
         "tb_dice_sums_bwd_f32": (I, [P, P, P, P, I64, I64, I, I, P]),
         "tb_dice_metric_sums_f32": (I, [P, P, P, I64, I64, P]),

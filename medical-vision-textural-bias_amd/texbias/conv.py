@@ -85,6 +85,20 @@ def _wgrad_tiles(g_shape, x_shape, stride: int) -> bool:
     return lib().tb_conv3d_wgrad_config(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, 1, cfg) == 0
 
 
+def weight_grad(gy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, transposed: bool = False,
+                output_padding=(0, 0, 0)) -> torch.Tensor:
+    """The 3x3x3, padding-1 weight gradient of a layer whose forward ran on a texbias kernel: the
+    texbias MFMA kernels when tb_conv3d_wgrad_config finds a tiling for the shapes, else ATen's
+    (``aten.convolution_backward`` with only the weight output), never an error for a shape the
+    forward accepted."""
+    G, X = (x, gy) if transposed else (gy, x)
+    if _wgrad_tiles(tuple(G.shape), tuple(X.shape), stride):
+        return wgrad(G, X, w.shape, stride, 1)
+    _, gw, _ = torch.ops.aten.convolution_backward(gy.contiguous(), x, w, None, [stride] * 3, [1, 1, 1], [1, 1, 1],
+                                                   transposed, list(output_padding), 1, [False, True, False])
+    return gw
+
+
 def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, padding, transposed: bool,
                        output_padding=(0, 0, 0)) -> bool:
     if not custom_backward_applies(x, w):
@@ -102,43 +116,50 @@ def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, pa
     return _wgrad_tiles((x.shape[0], w.shape[0]) + tuple(out_spatial), tuple(x.shape), s)
 
 
-class _ConvFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, b, stride, padding, output_padding, transposed, fast_w):
-        if transposed and convT64_applies(x, w, stride, padding, output_padding):
-            y = convT_mfma(x, w, b)
-        elif transposed:
-            y = F.conv_transpose3d(x, w, b, stride, padding, output_padding)
-        else:
-            y = F.conv3d(x, w, b, stride, padding)
-        ctx.save_for_backward(x, w)
-        ctx.cfg = (stride, padding, output_padding, transposed, b is not None, fast_w)
-        return y
+GEMM = os.environ.get("TEXBIAS_CONVGEMM", "1") != "0"
 
-    @staticmethod
-    def backward(ctx, gy):
-        x, w = ctx.saved_tensors
-        stride, padding, output_padding, transposed, has_b, fast_w = ctx.cfg
-        gy = gy.contiguous()
-        need_x, need_w, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
-        gx = gb = gw = None
-        lib_w = need_w and not fast_w
-        if need_x and not transposed and s2_dgrad_applies(gy, x, w, stride, padding):
-            gx = convT_mfma(gy, w, None)  # Conv3d(16 -> 32, s2)'s input gradient on k_convT_mfma64
-            need_x = False
-        if need_x or lib_w:
-            gxl, gw, _ = torch.ops.aten.convolution_backward(
-                gy, x, w, None, list(stride), list(padding), [1, 1, 1], transposed, list(output_padding), 1,
-                [need_x, lib_w, False])
-            gx = gxl if need_x else gx
-        if need_w and fast_w:
-            if transposed:   # dW[ci][co] = corr(x, gy)
-                gw = wgrad(x, gy, w.shape, stride[0], padding[0])
-            else:            # dW[co][ci] = corr(gy, x)
-                gw = wgrad(gy, x, w.shape, stride[0], padding[0])
-        if need_b and has_b:
-            gb = channel_sum(gy)
-        return gx, gw, gb, None, None, None, None, None
+
+def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:
+    """Shapes tb_conv3d_gemm_f32 takes: 3x3x3 (padding 1, stride 1 / 2) or 1x1x1 (padding 0, stride 1)
+    Conv3d, or ConvTranspose3d(3, stride 2, padding 1, output_padding 1); float32 HIP tensors, input
+    channels a multiple of 8, every tensor < 2^31 elements."""
+    if not (GEMM and custom_backward_applies(x, w) and x.dim() == 5 and len(set(stride)) == 1 and
+            len(set(padding)) == 1):
+        return False
+    k = tuple(w.shape[2:])
+    s, p = stride[0], padding[0]
+    if transposed:
+        ok = k == (3, 3, 3) and s == 2 and p == 1 and tuple(output_padding) == (1, 1, 1) and x.shape[1] == w.shape[0]
+    else:
+        ok = x.shape[1] == w.shape[1] and ((k == (3, 3, 3) and p == 1 and s in (1, 2)) or
+                                           (k == (1, 1, 1) and p == 0 and s == 1))
+    return ok and x.shape[1] % 8 == 0 and x.numel() // x.shape[1] * 8 * max(w.shape[0], w.shape[1], x.shape[1]) < 2 ** 31
+
+
+def gemm_applies(x, w, stride, padding, transposed: bool, output_padding=(0, 0, 0)) -> bool:
+    """Forward on the implicit-GEMM kernel (csrc/conv_gemm.hip)."""
+    return _gemm_geom_ok(x, w, stride, padding, transposed, output_padding)
+
+
+def gemm_dgrad_applies(gy, x, w, stride, padding, transposed: bool, output_padding=(0, 0, 0)) -> bool:
+    """The input gradient on the implicit-GEMM kernel: stride-1 Conv3d ("dgrad"), stride-2 Conv3d on even
+    extents ("convT" with the layer's weight), ConvTranspose3d (a stride-2 Conv3d of dY with its weight)."""
+    if not (_gemm_geom_ok(x, w, stride, padding, transposed, output_padding) and gy.is_cuda and
+            gy.dtype == torch.float32):
+        return False
+    if transposed:
+        return gy.shape[1] % 8 == 0
+    if stride[0] == 2:
+        return gy.shape[1] % 8 == 0 and all(2 * a == b for a, b in zip(gy.shape[2:], x.shape[2:]))
+    return gy.shape[1] % 8 == 0
+
+
+def gemm_dgrad(gy: torch.Tensor, w: torch.Tensor, stride: int, transposed: bool) -> torch.Tensor:
+    if transposed:   # ConvTranspose3d(Cin -> M, s2): dX = Conv3d(dY, W as [Cin][M], stride 2)
+        return conv_gemm(gy, w, None, "conv", 2, 3)
+    if stride == 2:  # Conv3d(s2): dX = ConvTranspose3d(dY, W as [M][Cin])
+        return conv_gemm(gy, w, None, "convT", 2, 3)
+    return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2])
 
 
 def small_conv(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
@@ -156,33 +177,9 @@ def small_conv(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
 
 def small_conv_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and \
-        tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and w.shape[0] <= 4 and w.shape[1] <= 4 and \
+        x.shape[1] == w.shape[1] and tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and \
+        w.shape[0] <= 4 and w.shape[1] <= 4 and \
         x.shape[-1] <= 168
-
-
-class _SmallConvFn(torch.autograd.Function):
-    """Few-channel stride-1 3x3x3 Conv3d: forward and input gradient on the direct kernel, weight
-    gradient on the split-K MFMA kernel, bias gradient on the channel-sum kernel."""
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        y = small_conv(x, w, b)
-        ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, w = ctx.saved_tensors
-        gy = gy.contiguous()
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
-        if ctx.needs_input_grad[1]:
-            gw = wgrad(gy, x, w.shape, 1, 1)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = channel_sum(gy)
-        return gx, gw, gb
 
 
 # ---------------------------------------------------------------- full-resolution stride-2 layers
@@ -227,7 +224,7 @@ def _s2_shape_ok(spatial) -> bool:
 def s2_fewin_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     """Conv3d(Cin <= 4 -> 16 or 32, 3, stride 2, padding 1) on even spatial dims: k_conv_s2_fewin."""
     return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and \
-        tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and w.shape[1] <= 4 and \
+        x.shape[1] == w.shape[1] and tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and w.shape[1] <= 4 and \
         w.shape[0] in (16, 32) and _s2_shape_ok(x.shape[2:]) and x.data_ptr() % 16 == 0
 
 
@@ -235,62 +232,9 @@ def convT_fewout_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, outp
     """ConvTranspose3d(Cin <= 32 -> Cout <= 4, 3, 2, 1, output_padding 1): forward on k_convT_fewout and
     input gradient on k_conv_s2_fewin (needs Cin 16 or 32)."""
     return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and \
-        tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and tuple(output_padding) == (1, 1, 1) and \
-        w.shape[1] <= 4 and w.shape[0] in (16, 32) and x.shape[-1] % 4 == 0 and x.shape[-1] <= 80 and \
+        x.shape[1] == w.shape[0] and tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and \
+        tuple(output_padding) == (1, 1, 1) and w.shape[1] <= 4 and w.shape[0] in (16, 32) and x.shape[-1] % 4 == 0 and x.shape[-1] <= 80 and \
         _s2_shape_ok(tuple(2 * n for n in x.shape[2:]))
-
-
-class _ConvS2FewInFn(torch.autograd.Function):
-    """Conv3d(Cin <= 4, stride 2): forward on the direct stride-2 kernel; weight gradient on the
-    z-marching MFMA kernel, bias gradient on the channel-sum kernel, input gradient (rarely needed:
-    the first layer's input is data) on ATen."""
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        y = conv_s2_fewin(x, s2_pairs(w), b, w.shape[0])
-        ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, w = ctx.saved_tensors
-        gy = gy.contiguous()
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx, _, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [2, 2, 2], [1, 1, 1], [1, 1, 1], False,
-                                                           [0, 0, 0], 1, [True, False, False])
-        if ctx.needs_input_grad[1]:
-            gw = wgrad(gy, x, w.shape, 2, 1)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = channel_sum(gy)
-        return gx, gw, gb
-
-
-class _ConvTFewOutFn(torch.autograd.Function):
-    """ConvTranspose3d(Cin -> Cout <= 4, stride 2): forward on the sub-pixel kernel, input gradient (a
-    stride-2 convolution of dY with Cout input channels) on the direct stride-2 kernel, weight gradient
-    on the z-marching MFMA kernel, bias gradient on the channel-sum kernel."""
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        y = convT_fewout(x, w, b)
-        ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, w = ctx.saved_tensors
-        gy = gy.contiguous()
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:  # dX[m][i] = sum_{c, t} W[m][c][t] dY[c][2 i + t - 1]
-            gx = conv_s2_fewin(gy, s2_pairs(w), None, w.shape[0])
-        if ctx.needs_input_grad[1]:  # dW[ci][co] = corr(x, dY)
-            gw = wgrad(x, gy, w.shape, 2, 1)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = channel_sum(gy)
-        return gx, gw, gb
 
 
 def convT_mfma(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
@@ -312,7 +256,8 @@ convT_mfma64 = convT_mfma
 def s2_dgrad_applies(gy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     """Conv3d(16 -> 32, 3, stride 2, padding 1) on even extents: its input gradient is
     conv_transpose3d(dY, W) with output_padding 1, i.e. k_convT_mfma64 with 32 input channels."""
-    return CONVT64 and tuple(w.shape) == (32, 16, 3, 3, 3) and tuple(stride) == (2, 2, 2) and \
+    return CONVT64 and gy.is_cuda and gy.dtype == torch.float32 and w.dtype == torch.float32 and \
+        tuple(w.shape) == (32, 16, 3, 3, 3) and tuple(stride) == (2, 2, 2) and gy.shape[1] == 32 and \
         tuple(padding) == (1, 1, 1) and gy.dim() == 5 and all(2 * a == b for a, b in zip(gy.shape[2:], x.shape[2:])) and \
         gy.shape[-1] % 4 == 0 and gy.shape[-1] <= 64 and gy.data_ptr() % 16 == 0
 
@@ -321,6 +266,7 @@ def convT64_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, output_pa
     """ConvTranspose3d(64 -> 16, 3, 2, 1, output_padding 1), rows of 4k <= 64 floats: forward on
     k_convT_mfma64 (TEXBIAS_CONVT64=0: ATen).  Input and weight gradients stay where _ConvFn puts them."""
     return CONVT64 and custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape) == (64, 16, 3, 3, 3) and \
+        x.shape[1] == 64 and \
         tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and tuple(output_padding) == (1, 1, 1) and \
         x.shape[-1] % 4 == 0 and x.shape[-1] <= 64 and x.data_ptr() % 16 == 0
 
@@ -340,33 +286,8 @@ def conv16_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     """Conv3d(16 -> 16, 3, stride 1, padding 1), rows of 16k <= 128 floats: k_conv3d_fwd16 (forward and
     input gradient) + the z-marching weight gradient."""
     return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape) == (16, 16, 3, 3, 3) and \
-        tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and x.shape[-1] % 16 == 0 and \
+        x.shape[1] == 16 and tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and x.shape[-1] % 16 == 0 and \
         x.shape[-1] <= 80 and x.data_ptr() % 16 == 0 and os.environ.get("TEXBIAS_CONV16", "1") != "0"
-
-
-class _Conv16Fn(torch.autograd.Function):
-    """Conv3d(16 -> 16, stride 1): forward and input gradient (flipped, transposed weights) on the MFMA
-    kernel, weight gradient on the z-marching MFMA kernel, bias gradient on the channel-sum kernel."""
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        y = conv_fwd16(x, w, b)
-        ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, w = ctx.saved_tensors
-        gy = gy.contiguous()
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = conv_fwd16(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
-        if ctx.needs_input_grad[1]:
-            gw = wgrad(gy, x, w.shape, 1, 1)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = channel_sum(gy)
-        return gx, gw, gb
 
 
 def conv_mfma(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
@@ -385,70 +306,213 @@ def conv_mfma_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool
     """Conv3d(32 -> 32) with rows of 4k <= 64 floats, or Conv3d(64 -> 64) with rows <= 48, stride 1,
     padding 1: k_conv3d_mfma_s1 (forward and input gradient) + the z-marching weight gradient
     (TEXBIAS_CONVMFMA=0: _ConvFn)."""
-    if not (custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3)):
+    if not (custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and
+            x.shape[1] == w.shape[1]):
         return False
     C = w.shape[0]
     return C in (32, 64) and w.shape[1] == C and tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and \
         x.shape[-1] % 4 == 0 and x.shape[-1] <= (64 if C == 32 else 48) and x.data_ptr() % 16 == 0 and CONVMFMA
 
 
-class _ConvMfmaFn(torch.autograd.Function):
-    """Conv3d(C -> C, stride 1), C = 32 or 64: forward and input gradient (flipped, transposed weights)
-    on the channel-split MFMA kernel, weight gradient on the z-marching MFMA kernel, bias gradient on
-    the channel-sum kernel."""
+# ---------------------------------------------------------------- implicit-GEMM convolutions
+CG_MODES = {"conv": 0, "dgrad": 1, "convT": 2}
 
+
+def gemm_out_shape(x_shape, w_shape, mode: str, stride: int, ksize: int):
+    N, _, D, H, Wd = x_shape
+    if mode == "conv":
+        p = 1 if ksize == 3 else 0
+        return (N, w_shape[0]) + tuple((n + 2 * p - ksize) // stride + 1 for n in (D, H, Wd))
+    if mode == "dgrad":
+        return (N, w_shape[1], D, H, Wd)
+    return (N, w_shape[1], 2 * D, 2 * H, 2 * Wd)
+
+
+def conv_gemm(x: torch.Tensor, w: torch.Tensor, b=None, mode: str = "conv", stride: int = 1, ksize: int = 3,
+              add=None, out=None) -> torch.Tensor:
+    """tb_conv3d_gemm_f32 (csrc/conv_gemm.hip): mode "conv" = Conv3d(x, w, b, stride, padding (k-1)/2);
+    "dgrad" = the input gradient of a stride-1 Conv3d whose weight is ``w`` (x = dY); "convT" =
+    ConvTranspose3d(x, w, b, stride 2, padding 1, output_padding 1), which with a stride-2 Conv3d's
+    weight is that layer's input gradient.  ``add`` (same shape as the output) is summed in; ``out`` may be
+    given (batch stride free: a channel slice of a larger buffer) and may alias ``add``."""
+    N, Cin, D, H, Wd = x.shape
+    if x.stride(1) != D * H * Wd or x.stride(4) != 1 or x.stride(3) != Wd or x.stride(2) != H * Wd:
+        x = x.contiguous()
+    w = w.contiguous()
+    md = CG_MODES[mode]
+    M = w.shape[0] if mode == "conv" else w.shape[1]
+    oshape = gemm_out_shape(x.shape, w.shape, mode, stride, ksize)
+    y = torch.empty(oshape, dtype=torch.float32, device=x.device) if out is None else out
+    sp = math.prod(oshape[2:])
+    assert y.shape == oshape and y.stride(1) == sp and y.stride(4) == 1, "conv_gemm: out layout"
+    if add is not None:
+        assert add.shape == oshape and add.stride(1) == sp and add.stride(4) == 1, "conv_gemm: add layout"
+    nb = int(lib().tb_conv3d_gemm_workspace_bytes(md, N, Cin, M, D, H, Wd, stride, ksize))
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        check(lib().tb_conv3d_gemm_f32(md, x.data_ptr(), x.stride(0), w.data_ptr(),
+                                       b.data_ptr() if b is not None else None,
+                                       add.data_ptr() if add is not None else None,
+                                       add.stride(0) if add is not None else 0, y.data_ptr(), y.stride(0), N, Cin, M,
+                                       D, H, Wd, stride, ksize, ws.data_ptr(), nb, _stream(x)), "tb_conv3d_gemm_f32")
+    return y
+
+
+def conv_gemm_config(x_shape, M: int, mode: str = "conv", stride: int = 1, ksize: int = 3) -> dict:
+    import ctypes
+    cfg = (ctypes.c_int64 * 6)()
+    N, Cin, D, H, Wd = x_shape
+    check(lib().tb_conv3d_gemm_config(CG_MODES[mode], N, Cin, M, D, H, Wd, stride, ksize, cfg), "tb_conv3d_gemm_config")
+    return dict(zip(("BM", "BP", "nsplit", "kper", "blocks", "positions"), list(cfg)))
+
+
+# ---------------------------------------------------------------- routing: one kernel choice per call
+class Route:
+    """The kernels one Conv3d / ConvTranspose3d call runs on -- forward, input gradient, weight gradient,
+    bias gradient -- chosen once from the shapes (the gates above), so that the layer's autograd function
+    and the fused U-Net blocks (``texbias.unet``) share one dispatch.  Kinds: ``fwd16`` (k_conv3d_fwd16),
+    ``mfma`` (k_conv3d_mfma_s1), ``fewin`` (k_conv_s2_fewin), ``small`` (k_conv3d_small_z), ``fewout``
+    (k_convT_fewout), ``convT64`` (k_convT_mfma64), ``gemm`` (k_conv_gemm), ``aten`` (MIOpen / CK)."""
+
+    __slots__ = ("kind", "dx", "stride", "padding", "output_padding", "transposed", "fast_w", "k")
+
+    def __init__(self, x: torch.Tensor, w: torch.Tensor, stride, padding, output_padding, transposed: bool):
+        self.stride, self.padding = tuple(stride), tuple(padding)
+        self.output_padding, self.transposed = tuple(output_padding), transposed
+        self.k = w.shape[2]
+        st, pd, op = self.stride, self.padding, self.output_padding
+        if not custom_backward_applies(x, w):
+            self.kind = "aten"
+        elif transposed:
+            self.kind = ("fewout" if convT_fewout_applies(x, w, st, pd, op) else
+                         "convT64" if convT64_applies(x, w, st, pd, op) else
+                         "gemm" if gemm_applies(x, w, st, pd, True, op) else "aten")
+        else:
+            self.kind = ("fwd16" if conv16_applies(x, w, st, pd) else
+                         "mfma" if conv_mfma_applies(x, w, st, pd) else
+                         "fewin" if s2_fewin_applies(x, w, st, pd) else
+                         "small" if small_conv_applies(x, w, st, pd) else
+                         "gemm" if gemm_applies(x, w, st, pd, False) else "aten")
+        # input gradient kernel
+        if self.kind in ("fwd16", "mfma", "small", "fewout"):
+            self.dx = self.kind
+        else:
+            self.dx = "aten"
+            if self.kind != "aten" and not transposed and st[0] == 2 and tuple(w.shape) == (32, 16, 3, 3, 3) and CONVT64 \
+                    and x.shape[-1] % 8 == 0 and x.shape[-1] // 2 <= 64 and all(n % 2 == 0 for n in x.shape[2:]):
+                self.dx = "convT64"   # Conv3d(16 -> 32, s2)'s input gradient on k_convT_mfma64
+            elif self.kind != "aten" and _gemm_geom_ok(x, w, st, pd, transposed, op) and w.shape[0] % 8 == 0 and \
+                    (transposed or st[0] == 1 or all(n % 2 == 0 for n in x.shape[2:])) and \
+                    (w.shape[1] % 8 == 0 if transposed else w.shape[0] % 8 == 0):
+                self.dx = "gemm"
+        # weight gradient: the texbias MFMA kernels where a tiling exists and the reduction is long
+        if self.kind in ("fwd16", "mfma", "fewin", "small", "fewout"):
+            self.fast_w = True
+        elif self.kind == "aten" and not custom_backward_applies(x, w):
+            self.fast_w = False
+        else:
+            osp = None if transposed else [(n + 2 * p - kk) // s + 1
+                                          for n, p, s, kk in zip(x.shape[2:], pd, st, w.shape[2:])]
+            self.fast_w = fast_wgrad_applies(x, w, osp, st, pd, transposed, op)
+
+    # -- forward
+    def forward(self, x, w, b):
+        k = self.kind
+        if k == "fwd16":
+            return conv_fwd16(x, w, b)
+        if k == "mfma":
+            return conv_mfma(x, w, b)
+        if k == "fewin":
+            return conv_s2_fewin(x, s2_pairs(w), b, w.shape[0])
+        if k == "small":
+            return small_conv(x, w, b)
+        if k == "fewout":
+            return convT_fewout(x, w, b)
+        if k == "convT64":
+            return convT_mfma(x, w, b)
+        if k == "gemm":
+            return conv_gemm(x, w, b, "convT" if self.transposed else "conv", self.stride[0], self.k)
+        if self.transposed:
+            return F.conv_transpose3d(x, w, b, self.stride, self.padding, self.output_padding)
+        return F.conv3d(x, w, b, self.stride, self.padding)
+
+    # -- input gradient (x only for its shape on the ATen path)
+    def input_grad(self, gy, x, w):
+        k = self.dx
+        if k == "fwd16":
+            return conv_fwd16(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+        if k == "mfma":
+            return conv_mfma(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+        if k == "small":
+            return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+        if k == "fewout":   # dX[m][i] = sum_{c, t} W[m][c][t] dY[c][2 i + t - 1]
+            return conv_s2_fewin(gy, s2_pairs(w), None, w.shape[0])
+        if k == "convT64":
+            return convT_mfma(gy if gy.data_ptr() % 16 == 0 else gy.clone(), w, None)
+        if k == "gemm":
+            return gemm_dgrad(gy, w, self.stride[0], self.transposed)
+        gx, _, _ = torch.ops.aten.convolution_backward(
+            gy, x, w, None, list(self.stride), list(self.padding), [1, 1, 1], self.transposed,
+            list(self.output_padding), 1, [True, False, False])
+        return gx
+
+    # -- weight gradient
+    def weight_grad(self, gy, x, w):
+        if self.fast_w and tuple(w.shape[2:]) == (3, 3, 3) and self.padding[0] == 1:
+            return weight_grad(gy, x, w, self.stride[0], self.transposed, self.output_padding)
+        _, gw, _ = torch.ops.aten.convolution_backward(
+            gy, x, w, None, list(self.stride), list(self.padding), [1, 1, 1], self.transposed,
+            list(self.output_padding), 1, [False, True, False])
+        return gw
+
+    def backward(self, gy, x, w, need_x: bool, need_w: bool, need_b: bool, gb=None):
+        gy = gy.contiguous()
+        gx = self.input_grad(gy, x, w) if need_x else None
+        gw = self.weight_grad(gy, x, w) if need_w else None
+        if need_b and gb is None:
+            gb = channel_sum(gy) if self.kind != "aten" else gy.sum(dim=(0, 2, 3, 4))
+        return gx, gw, gb if need_b else None
+
+
+class _RouteFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
-        y = conv_mfma(x, w, b)
+    def forward(ctx, x, w, b, route):
+        y = route.forward(x.contiguous() if route.kind != "aten" else x, w, b)
         ctx.save_for_backward(x, w)
-        ctx.has_b = b is not None
+        ctx.route, ctx.has_b = route, b is not None
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        gy = gy.contiguous()
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = conv_mfma(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
-        if ctx.needs_input_grad[1]:
-            gw = wgrad(gy, x, w.shape, 1, 1)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = channel_sum(gy)
-        return gx, gw, gb
+        n = ctx.needs_input_grad
+        gx, gw, gb = ctx.route.backward(gy, x, w, n[0], n[1], n[2] and ctx.has_b)
+        return gx, gw, gb, None
+
+
+def route_of(mod, x: torch.Tensor) -> "Route":
+    """The layer's route for this input (cached per shape / alignment / dtype / device)."""
+    key = (tuple(x.shape), x.dtype, x.device, x.data_ptr() % 16 == 0, x.is_contiguous())
+    cache = mod.__dict__.setdefault("_tb_routes", {})
+    r = cache.get(key)
+    if r is None:
+        tr = isinstance(mod, nn.ConvTranspose3d)
+        r = Route(x, mod.weight, mod.stride, mod.padding, mod.output_padding if tr else (0, 0, 0), tr)
+        cache[key] = r
+    return r
 
 
 class Conv3d(nn.Conv3d):
     def forward(self, x):
         if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
-                conv16_applies(x, self.weight, self.stride, self.padding):
-            return _Conv16Fn.apply(x, self.weight, self.bias)
-        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
-                conv_mfma_applies(x, self.weight, self.stride, self.padding):
-            return _ConvMfmaFn.apply(x, self.weight, self.bias)
-        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
-                s2_fewin_applies(x, self.weight, self.stride, self.padding):
-            return _ConvS2FewInFn.apply(x, self.weight, self.bias)
-        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
-                small_conv_applies(x, self.weight, self.stride, self.padding):
-            return _SmallConvFn.apply(x, self.weight, self.bias)
-        if self.groups == 1 and self.dilation == (1, 1, 1) and self.padding_mode == "zeros" and \
                 custom_backward_applies(x, self.weight):
-            k = self.weight.shape[2:]
-            out_sp = [(n + 2 * p - kk) // s + 1 for n, p, s, kk in zip(x.shape[2:], self.padding, self.stride, k)]
-            fast = fast_wgrad_applies(x, self.weight, out_sp, self.stride, self.padding, False)
-            return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, (0, 0, 0), False, fast)
+            return _RouteFn.apply(x, self.weight, self.bias, route_of(self, x))
         return super().forward(x)
 
 
 class ConvTranspose3d(nn.ConvTranspose3d):
     def forward(self, x, output_size=None):
         if output_size is None and self.groups == 1 and self.dilation == (1, 1, 1) and \
-                convT_fewout_applies(x, self.weight, self.stride, self.padding, self.output_padding):
-            return _ConvTFewOutFn.apply(x, self.weight, self.bias)
-        if output_size is None and self.groups == 1 and self.dilation == (1, 1, 1) and \
                 custom_backward_applies(x, self.weight):
-            fast = fast_wgrad_applies(x, self.weight, None, self.stride, self.padding, True, self.output_padding)
-            return _ConvFn.apply(x, self.weight, self.bias, self.stride, self.padding, self.output_padding, True,
-                                 fast)
+            return _RouteFn.apply(x, self.weight, self.bias, route_of(self, x))
         return super().forward(x, output_size)

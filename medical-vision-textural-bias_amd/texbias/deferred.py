@@ -44,11 +44,25 @@ def active() -> bool:
     return torch.utils.data.get_worker_info() is not None
 
 
+try:  # xxh3-128 hashes ~15 GB/s on one core (a 143 MB BraTS sample in ~10 ms); BLAKE2b ~1 GB/s
+    import xxhash as _xx
+
+    def _digest(buf) -> int:
+        return _xx.xxh3_128_intdigest(buf)
+except ImportError:  # pragma: no cover - xxhash ships with this image
+    def _digest(buf) -> int:
+        return int.from_bytes(hashlib.blake2b(buf, digest_size=16).digest(), "little")
+
+
 def _checksum(t: torch.Tensor) -> int:
-    """Position-dependent digest (BLAKE2b) of a float32 tensor's bits: a transform that only moves
-    voxels (a flip, a transpose, a rot90) changes it as surely as one that changes values."""
-    x = torch.as_tensor(t).detach().to(device="cpu", dtype=torch.float32).contiguous()
-    return int.from_bytes(hashlib.blake2b(x.numpy().tobytes(), digest_size=16).digest(), "little")
+    """Position-dependent 128-bit digest of a float32 tensor's bits: a transform that only moves
+    voxels (a flip, a transpose, a rot90) changes it as surely as one that changes values.  The
+    bytes are hashed in place (no ``tobytes`` copy); a tensor already contiguous float32 on the CPU
+    (the collated batch's samples) is not copied at all."""
+    x = torch.as_tensor(t).detach()
+    if x.device.type != "cpu" or x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.to(device="cpu", dtype=torch.float32).contiguous()
+    return _digest(memoryview(x.numpy()).cast("B"))
 
 
 class TexbiasPlan:

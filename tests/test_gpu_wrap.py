@@ -123,3 +123,23 @@ def test_wrap_route_mixed_batch(rt):
     rt.kspace_filter(z, 3, [[K.wrap_op(0.75)]] * 2, 3, out=z)
     torch.cuda.synchronize()
     assert relerr(z[0].cpu().numpy(), O.wrap_artifact(z0[0], 0.75)) < 1e-5
+
+
+def test_wrap_route_mixed_alpha_even_d_one_launch(rt):
+    """Even D: k_wrap_even carries per-sample 2-tap weights, so a batch with different alphas per
+    sample runs as ONE launch (odd D still splits where the circulant table changes)."""
+    torch.manual_seed(5)
+    shape = (4, 2, 16, 12, 10)
+    x = torch.randn(shape, device="cuda")
+    alphas = [0.0, 0.25, 0.5, 0.75]
+    progs = [[K.wrap_op(a)] for a in alphas]
+    rt.set_pass_timing(True)
+    yw = rt.kspace_filter(x, 3, progs, 2, pad=2)
+    _, cnt, _, names = rt.pass_stats()
+    rt.set_pass_timing(False)
+    torch.cuda.synchronize()
+    assert names[2] == "k_wrap_even" and cnt[2] == 1
+    xh = x.cpu().numpy()
+    for b, al in enumerate(alphas):
+        assert relerr(yw[b, ..., :10].cpu().numpy(), O.wrap_artifact(xh[b], al)) < 1e-5
+    assert torch.all(yw[..., 10:] == 0)
