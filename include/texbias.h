@@ -299,6 +299,26 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
                               size_t ws_bytes, void* stream);
 
 /*
+ * The same ADN block (InstanceNorm3d(affine=False) + PReLU) for the fused U-Net units of round 5:
+ * per-sample batch strides (a channel slice of a wider tensor: *sn = floats between samples, 0 =
+ * contiguous C S), the ResidualUnit's sum fused into the forward store (y = prelu(norm(x)) + res; res
+ * may be NULL), and in the backward the preceding convolution's bias gradient dbias[c] = sum over n and
+ * voxels of dx (NULL: not computed) and the PReLU weight gradient dw (NULL: not computed).  No
+ * accumulator memsets and no float atomics: every block publishes partial sums, the last block of an
+ * instance (channel) reduces them in block order -- results are deterministic.  `counters`: DEVICE
+ * uint32[tb_adn_counters(N, C)], zero before the first call, left zero by every call (one set per
+ * stream); ws: tb_adn_workspace_bytes(N, C, S) bytes of device scratch.
+ */
+size_t tb_adn_workspace_bytes(int64_t N, int64_t C, int64_t S);
+int64_t tb_adn_counters(int64_t N, int64_t C);
+int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const float* res, int64_t rsn, float* mean,
+                   float* rstd, const float* prelu_w, int64_t N, int64_t C, int64_t S, float eps, void* ws,
+                   size_t ws_bytes, uint32_t* counters, void* stream);
+int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, float* dx, int64_t dxsn,
+                   const float* mean, const float* rstd, const float* prelu_w, float* dw, float* dbias, int64_t N,
+                   int64_t C, int64_t S, void* ws, size_t ws_bytes, uint32_t* counters, void* stream);
+
+/*
  * GPU-side BraTS preprocessing of B resident raw volumes img [B][C][H0][W0][D0] and
  * label maps lab [B][H0][W0][D0] (float class ids, as LoadImaged gives them; may be NULL when
  * out_lab is NULL), per sample b with params[b] drawn on the host:

@@ -47,7 +47,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int KC = 32;    // k rows per stage
 constexpr int NTH = 256;  // threads per block
-constexpr int RS = 36;    // LDS floats per tile row: [k parity 0..1][16 steps] + 4 pad
+constexpr int RS = 36;    // LDS floats per tile row: 32 k + 4 pad (16-B reads of 16 rows hit distinct banks)
 
 struct CGArgs {
   const float* x;
@@ -57,6 +57,7 @@ struct CGArgs {
   float* y;
   float* part;
   int64_t xsn, ysn, addsn;  // batch strides (floats); channel strides below
+  int64_t xbytes;           // bytes of x from its base (the gather's buffer range)
   int xsc, ysc;
   int Cin, M;
   int IDm, IH, IW;  // input extents
@@ -100,7 +101,8 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
   constexpr int NPOS = BP / 64;          // gather positions per lane
   constexpr int AQ = BM * KC / 4 / NTH;  // A float4 per thread per stage
   static_assert(TM >= 1 && TN >= 1 && NPOS >= 1 && AQ >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BP) * RS];
+  extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
+  constexpr int LBUF = (BM + BP) * RS;   // floats per stage buffer
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   int b = xcd_remap((int)blockIdx.x, (int)gridDim.x);
@@ -117,7 +119,8 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
   const int m0 = mt * BM, p0 = pt * BP;
   const int IHW = a.IH * a.IW;
 
-  // gather positions: lane + 64 i of the tile
+  // gather positions: lane + 64 i of the tile; byte offset of the tap-(0,0,0) voxel of channel 0 and the
+  // per-tap validity bits
   int xo[NPOS];
   uint32_t vm[NPOS];
 #pragma unroll
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
     t /= a.OH;
     const int oz = t % a.OD, n = t / a.OD;
     const int bz = a.S * oz, by = a.S * oy, bx = a.S * ox;
-    xo[i] = (int)(n * a.xsn) + bz * IHW + by * a.IW + bx;
+    xo[i] = 4 * ((int)(n * a.xsn) + bz * IHW + by * a.IW + bx);
     uint32_t m = 0;
     for (int j = 0; j < T; ++j) {
       int dz, dy, dx, wi;
@@ -142,9 +145,15 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
     }
     vm[i] = m;
   }
+  // the input through a buffer descriptor: an out-of-range offset reads 0 (the zero padding and the
+  // k rows past k_end), so the gather needs no selects
+  const uint32_t xbytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.xbytes);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, (int)xbytes, 0x00020000);
+  const int xsc4 = 4 * a.xsc;
 
   // two register slots: the loads of stage s + 2 are in flight while stage s runs from LDS and stage
-  // s + 1 (loaded one stage earlier) is written to the other LDS buffer
+  // s + 1 (loaded one stage earlier) is written to the other LDS buffer.  LDS rows hold k in natural
+  // order; the MFMA step st pairs k = st (lanes 0-31) with k = 16 + st (lanes 32-63).
   float rb[2][NPOS][8];
   f32x4 ra[2][AQ];
   auto gather = [&](auto SL, int k0) {
@@ -155,23 +164,22 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
     const bool kin = k < k_end;
     int dz, dy, dx, wi;
     tap_of(a.kind, cls, kin ? t : 0, dz, dy, dx, wi);
-    const int off = c * a.xsc + (dz * a.IH + dy) * a.IW + dx;
+    const int off = 4 * ((dz * a.IH + dy) * a.IW + dx);
+    const int soff = c * xsc4;
 #pragma unroll
     for (int i = 0; i < NPOS; ++i) {
       const bool v = kin && ((vm[i] >> t) & 1u);
-      const float* src = a.x + (v ? xo[i] + off : 0);
+      const int vo = v ? xo[i] + off : (int)0x80000000;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float val = src[r * a.xsc];
-        rb[sl][i][r] = v ? val : 0.f;
-      }
+      for (int r = 0; r < 8; ++r)
+        rb[sl][i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, soff + r * xsc4, 0));
     }
   };
   auto aload = [&](auto SL, int k0) {
     constexpr int sl = decltype(SL)::value;
 #pragma unroll
     for (int u = 0; u < AQ; ++u) {
-      const int q4 = tid + NTH * u, row = q4 >> 3, kq = k0 + 4 * (q4 & 7);
+      const int q4 = tid + NTH * u, row = q4 % BM, kq = k0 + 4 * (q4 / BM);
       const int m = m0 + row;
       const bool ok = m < a.M && kq < k_end;
       const f32x4 v = *reinterpret_cast<const f32x4*>(A + (ok ? (int64_t)m * Kld + kq : 0));
@@ -180,19 +188,17 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
   };
   auto stage_store = [&](auto SL) {  // slot sl -> LDS buffer sl (stage s uses slot and buffer s & 1)
     constexpr int sl = decltype(SL)::value;
-    float* L = lds[sl];
+    float* L = lds_dyn + sl * LBUF;
 #pragma unroll
     for (int u = 0; u < AQ; ++u) {
-      const int q4 = tid + NTH * u, row = q4 >> 3, c4 = q4 & 7;
-      float* d = L + row * RS + 2 * c4;
-      *reinterpret_cast<float2*>(d) = make_float2(ra[sl][u][0], ra[sl][u][2]);
-      *reinterpret_cast<float2*>(d + 16) = make_float2(ra[sl][u][1], ra[sl][u][3]);
+      const int q4 = tid + NTH * u, row = q4 % BM, c4 = q4 / BM;
+      *reinterpret_cast<f32x4*>(L + row * RS + 4 * c4) = ra[sl][u];
     }
 #pragma unroll
     for (int i = 0; i < NPOS; ++i) {
-      float* d = L + (BM + lane + 64 * i) * RS + 4 * w;
-      *reinterpret_cast<f32x4*>(d) = f32x4{rb[sl][i][0], rb[sl][i][2], rb[sl][i][4], rb[sl][i][6]};
-      *reinterpret_cast<f32x4*>(d + 16) = f32x4{rb[sl][i][1], rb[sl][i][3], rb[sl][i][5], rb[sl][i][7]};
+      float* d = L + (BM + lane + 64 * i) * RS + 8 * w;
+      *reinterpret_cast<f32x4*>(d) = f32x4{rb[sl][i][0], rb[sl][i][1], rb[sl][i][2], rb[sl][i][3]};
+      *reinterpret_cast<f32x4*>(d + 4) = f32x4{rb[sl][i][4], rb[sl][i][5], rb[sl][i][6], rb[sl][i][7]};
     }
   };
 
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
   const int kk = lane >> 5, l32 = lane & 31;
   auto compute = [&](auto SL) {
     constexpr int sl = decltype(SL)::value;
-    const float* L = lds[sl];
+    const float* L = lds_dyn + sl * LBUF;
     f32x4 af[TM][4], bf[TN][4];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -369,6 +375,7 @@ struct Plan {
 };
 
 inline size_t align_floats(size_t n) { return (n + 63) & ~size_t(63); }
+inline size_t lds_bytes(int BM, int BP) { return (size_t)2 * (BM + BP) * RS * sizeof(float); }
 
 // Fill the geometry and tiling of a call (no device pointers).  Returns TB_OK or an error code.
 int make_plan(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride, int ksize, Plan& pl) {
@@ -404,26 +411,35 @@ int make_plan(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride,
   a.ysc = a.ymul == 2 ? 8 * a.OD * a.OH * a.OW : a.OD * a.OH * a.OW;
   if ((int64_t)N * M * a.ysc >= (int64_t)1 << 31) return TB_ERR_UNSUPPORTED_SIZE;
   a.P = N * a.OD * a.OH * a.OW;
-  // tile: M <= 32 -> 32 x 128; M <= 64 -> 64 x 64; else 128 x 64 (TEXBIAS_CG_TILE=a,b,c overrides)
+  // tile: M <= 32 -> 32 x 128; M <= 64 -> 64 x 64; else 128 x 128 (TEXBIAS_CG_TILE=1..5 overrides)
   static const int tile_env = [] {
     const char* e = std::getenv("TEXBIAS_CG_TILE");
     return e ? std::atoi(e) : 0;
   }();
   int tile = tile_env;
-  if (tile < 1 || tile > 4) tile = M <= 32 ? 1 : (M <= 64 ? 2 : 3);
-  static const int cfg[5][3] = {{0, 0, 0}, {32, 128, 1}, {64, 64, 2}, {128, 64, 2}, {64, 128, 2}};
+  if (tile < 1 || tile > 5) tile = M <= 32 ? 1 : (M <= 64 ? 2 : 5);
+  static const int cfg[6][3] = {{0, 0, 0}, {32, 128, 1}, {64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2}};
   pl.BM = cfg[tile][0], pl.BP = cfg[tile][1], pl.WGM = cfg[tile][2];
   a.mtiles = (M + pl.BM - 1) / pl.BM;
   a.ptiles = (a.P + pl.BP - 1) / pl.BP;
   int Kmax = 0;
   for (int c = 0; c < a.ncls; ++c) Kmax = a.Kc[c] > Kmax ? a.Kc[c] : Kmax;
-  // split k until about 4 blocks per CU exist (each slice >= 4 stages)
+  // split k so that the blocks fill whole rounds of the chip's block slots (LDS-bound occupancy), each
+  // slice >= 4 stages; among splits within 3 % of the best fill the smallest (less partial traffic)
   const int64_t base = (int64_t)a.mtiles * a.ptiles * a.ncls;
-  const int64_t want = 4LL * num_cu();
-  int ns = base >= want ? 1 : (int)((want + base - 1) / base);
-  const int maxs = Kmax / (4 * KC) > 1 ? Kmax / (4 * KC) : 1;
-  ns = ns > maxs ? maxs : ns;
-  ns = ns > 16 ? 16 : (ns < 1 ? 1 : ns);
+  int occ = (int)(163840 / lds_bytes(pl.BM, pl.BP));
+  occ = occ > 4 ? 4 : (occ < 1 ? 1 : occ);
+  const int64_t slots = (int64_t)occ * num_cu();
+  const int stages = (Kmax + KC - 1) / KC;
+  double best = 0.0;
+  int ns = 1;
+  for (int s = 1; s <= 16; ++s) {
+    if (s > 1 && stages / s < 4) break;
+    const int64_t blocks = base * s;
+    const int64_t rounds = (blocks + slots - 1) / slots;
+    const double eff = (double)blocks / (double)(rounds * slots);
+    if (eff > best * 1.03) best = eff, ns = s;
+  }
   a.kper = ((Kmax + ns - 1) / ns + KC - 1) / KC * KC;
   a.nsplit = (Kmax + a.kper - 1) / a.kper;
   pl.part_floats = a.nsplit > 1 ? (size_t)a.ncls * a.nsplit * M * a.P : 0;
@@ -433,7 +449,15 @@ int make_plan(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride,
 template <int BM, int BP, int WGM>
 hipError_t launch_tile(const CGArgs& a, hipStream_t st) {
   const int64_t nb = (int64_t)a.mtiles * a.ptiles * a.nsplit * a.ncls;
-  hipLaunchKernelGGL((k_conv_gemm<BM, BP, WGM>), dim3((unsigned)nb), dim3(NTH), 0, st, a);
+  const size_t lds = lds_bytes(BM, BP);
+  static std::once_flag once;
+  static hipError_t attr = hipSuccess;
+  std::call_once(once, [&] {
+    attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv_gemm<BM, BP, WGM>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  });
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_conv_gemm<BM, BP, WGM>), dim3((unsigned)nb), dim3(NTH), lds, st, a);
   return hipGetLastError();
 }
 
@@ -460,7 +484,8 @@ int tb_conv3d_gemm_f32(int mode, const float* x, int64_t xsn, const float* W, co
   a.xsn = xsn > 0 ? xsn : (int64_t)Cin * a.xsc;
   a.ysn = ysn > 0 ? ysn : (int64_t)M * a.ysc;
   a.addsn = addsn > 0 ? addsn : a.ysn;
-  if ((int64_t)(N - 1) * a.xsn + (int64_t)Cin * a.xsc >= (int64_t)1 << 31) return TB_ERR_UNSUPPORTED_SIZE;
+  a.xbytes = 4 * ((int64_t)(N - 1) * a.xsn + (int64_t)Cin * a.xsc);
+  if (a.xbytes >= (int64_t)1 << 31) return TB_ERR_UNSUPPORTED_SIZE;
   float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
   {
     const int64_t total = (int64_t)pl.pack_floats;
@@ -472,7 +497,8 @@ int tb_conv3d_gemm_f32(int mode, const float* x, int64_t xsn, const float* W, co
   if (pl.BM == 32) e = launch_tile<32, 128, 1>(a, st);
   else if (pl.BM == 64 && pl.BP == 64) e = launch_tile<64, 64, 2>(a, st);
   else if (pl.BM == 64) e = launch_tile<64, 128, 2>(a, st);
-  else e = launch_tile<128, 64, 2>(a, st);
+  else if (pl.BP == 64) e = launch_tile<128, 64, 2>(a, st);
+  else e = launch_tile<128, 128, 2>(a, st);
   if (e != hipSuccess) return TB_ERR_HIP;
   if (a.nsplit > 1) {
     const int64_t tot = (int64_t)a.ncls * a.M * a.P;

@@ -363,6 +363,305 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_apply(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ strided, memset-free ADN (round 5)
+// The same arithmetic as K1-K4 with (a) per-sample batch strides, so that an ADN can read a channel slice
+// of a wider tensor (the stacked unit + residual convolution of a strided ResidualUnit) and write into
+// one; (b) the residual sum fused into the forward store; (c) the preceding convolution's bias gradient
+// (dx summed over n and the voxels) out of the backward's store pass; (d) no accumulator memsets: every
+// block stores its partial sums, counts itself in on a per-instance counter, and the last block of the
+// instance reduces the partials in block order (deterministic) and resets the counter -- the counters
+// live in a caller-owned buffer that is zero before the first call and is left zero by every call.
+struct AdnArgs {
+  const float* x;
+  const float* dy;
+  const float* res;
+  float* y;  // forward output / backward dx
+  int64_t xsn, dysn, rsn, ysn;
+  float* mean;
+  float* rstd;
+  const float* aw;
+  float* dw;
+  float* dbias;
+  double* part;   // [NC][nblk][3]
+  double* inst;   // [NC][4]: per-instance results (backward: mg, mgz, sa)
+  uint32_t* cnt;  // [2 NC + C + 1]
+  int64_t S;
+  int C, NC, nblk;
+  float eps;
+  int vec;
+};
+
+__device__ __forceinline__ void store_d(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_d(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// block-reduce K doubles (fixed order) into red[k] (valid in every thread after the call)
+template <int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double (&out)[K]) {
+  __shared__ double red[K][NT / 64];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[k][wid] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) s += red[k][w];
+    out[k] = s;
+  }
+}
+
+// Publish this block's K sums as partial `slot` of group `g` (stride K doubles) and return true in every
+// thread of the block that arrives last of `total` on counter cnt[g] (the counter is reset to zero then).
+template <int K>
+__device__ __forceinline__ bool publish_last(const double (&sums)[K], double* part, int slot, uint32_t* cnt,
+                                             uint32_t total) {
+  __shared__ int last;
+  if (threadIdx.x < K) store_d(part + (int64_t)slot * K + threadIdx.x, sums[threadIdx.x]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    const uint32_t prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == total - 1;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// sum over `n` partials (stride K) of component k, in partial order (threads stride, fixed tree)
+template <int K>
+__device__ __forceinline__ void reduce_partials(const double* part, int n, double (&out)[K]) {
+  double v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = 0.0;
+  for (int i = threadIdx.x; i < n; i += NT)
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += load_d(part + (int64_t)i * K + k);
+  block_sum<K>(v, out);
+}
+
+__device__ __forceinline__ int64_t inst_base(int nc, int C, int64_t sn, int64_t S) {
+  return (int64_t)(nc / C) * sn + (int64_t)(nc % C) * S;
+}
+
+__global__ __launch_bounds__(NT) void k_adn_stats(const AdnArgs a) {
+  double s1 = 0.0, s2 = 0.0;
+  const int64_t b = (int64_t)blockIdx.x * CHUNK;
+  const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
+  const int nc = blockIdx.y;
+  const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
+  if (a.vec) {
+    const int n4 = (int)((e - b) >> 2);
+    float4 v[VPT];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int i = threadIdx.x + k * NT;
+      v[k] = i < n4 ? reinterpret_cast<const float4*>(xp)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const double p = v[k].x, q = v[k].y, r = v[k].z, t = v[k].w;
+      s1 += (p + q) + (r + t);
+      s2 += (p * p + q * q) + (r * r + t * t);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < e - b; i += NT) {
+      const double v = xp[i];
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  double in[2] = {s1, s2}, tot[2];
+  block_sum<2>(in, tot);
+  if (!publish_last<2>(tot, a.part + (int64_t)nc * a.nblk * 2, blockIdx.x, a.cnt + nc, a.nblk)) return;
+  double all[2];
+  reduce_partials<2>(a.part + (int64_t)nc * a.nblk * 2, a.nblk, all);
+  if (threadIdx.x == 0) {
+    float mean, rstd;
+    stats_of(all[0], all[1], a.S, a.eps, mean, rstd);
+    a.mean[nc] = mean;
+    a.rstd[nc] = rstd;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_adn_apply(const AdnArgs a) {
+  const int nc = blockIdx.y;
+  const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
+  const int64_t b = (int64_t)blockIdx.x * CHUNK;
+  const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
+  const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
+  float* yp = a.y + inst_base(nc, a.C, a.ysn, a.S) + b;
+  const float* rp = a.res ? a.res + inst_base(nc, a.C, a.rsn, a.S) + b : nullptr;
+  if (a.vec) {
+    const int n4 = (int)((e - b) >> 2);
+    float4 v[VPT];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int i = threadIdx.x + k * NT;
+      if (i < n4) v[k] = reinterpret_cast<const float4*>(xp)[i];
+    }
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int i = threadIdx.x + k * NT;
+      if (i < n4) {
+        float4 o;
+        o.x = prelu((v[k].x - mean) * rstd, aw);
+        o.y = prelu((v[k].y - mean) * rstd, aw);
+        o.z = prelu((v[k].z - mean) * rstd, aw);
+        o.w = prelu((v[k].w - mean) * rstd, aw);
+        if (rp) {
+          const float4 r = reinterpret_cast<const float4*>(rp)[i];
+          o.x += r.x, o.y += r.y, o.z += r.z, o.w += r.w;
+        }
+        reinterpret_cast<float4*>(yp)[i] = o;
+      }
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < e - b; i += NT) {
+      float o = prelu((xp[i] - mean) * rstd, aw);
+      if (rp) o += rp[i];
+      yp[i] = o;
+    }
+  }
+}
+
+// backward statistics: per instance mg = mean(g), mgz = mean(g z); globally sa = sum dy z [z <= 0]
+__global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
+  const int nc = blockIdx.y;
+  const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
+  const double md = mean, rd = rstd;
+  double s1 = 0.0, s2 = 0.0, sa = 0.0;
+  auto visit = [&](float xv, float gv) {
+    const bool pos = (xv - mean) * rstd > 0.f;
+    const double z = ((double)xv - md) * rd;
+    const double g = pos ? (double)gv : (double)aw * (double)gv;
+    s1 += g;
+    s2 += g * z;
+    sa += pos ? 0.0 : (double)gv * z;
+  };
+  const int64_t b = (int64_t)blockIdx.x * CHUNK;
+  const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
+  const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
+  const float* gp = a.dy + inst_base(nc, a.C, a.dysn, a.S) + b;
+  if (a.vec) {
+    const int n4 = (int)((e - b) >> 2);
+    constexpr int U = VPT / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 vx[U], vg[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int i = threadIdx.x + (h * U + k) * NT;
+        const bool ok = i < n4;
+        vx[k] = ok ? reinterpret_cast<const float4*>(xp)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        vg[k] = ok ? reinterpret_cast<const float4*>(gp)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        visit(vx[k].x, vg[k].x);
+        visit(vx[k].y, vg[k].y);
+        visit(vx[k].z, vg[k].z);
+        visit(vx[k].w, vg[k].w);
+      }
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < e - b; i += NT) visit(xp[i], gp[i]);
+  }
+  double in[3] = {s1, s2, sa}, tot[3];
+  block_sum<3>(in, tot);
+  if (!publish_last<3>(tot, a.part + (int64_t)nc * a.nblk * 3, blockIdx.x, a.cnt + nc, a.nblk)) return;
+  double all[3];
+  reduce_partials<3>(a.part + (int64_t)nc * a.nblk * 3, a.nblk, all);
+  // instance results; the last instance to finish sums the PReLU weight gradient over instances
+  double res[3] = {all[0] / (double)a.S, all[1] / (double)a.S, all[2]};
+  if (!publish_last<3>(res, a.inst, nc, a.cnt + 2 * a.NC + a.C, a.NC)) return;
+  if (a.dw) {
+    double sw = 0.0;
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < a.NC; ++i) sw += load_d(a.inst + 3 * i + 2);
+      *a.dw = (float)sw;
+    }
+  }
+}
+
+// dx = rstd (g - mg - z mgz); dbias[c] = sum over n and voxels of dx (partials + per-channel counter)
+__global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
+  const int nc = blockIdx.y;
+  const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
+  const double md = mean, rd = rstd;
+  const double mg = load_d(a.inst + 3 * nc), mgz = load_d(a.inst + 3 * nc + 1);
+  auto f = [&](float xv, float gv) {
+    const bool pos = (xv - mean) * rstd > 0.f;
+    const double z = ((double)xv - md) * rd;
+    const double g = pos ? (double)gv : (double)aw * (double)gv;
+    return (float)(rd * (g - mg - z * mgz));
+  };
+  const int64_t b = (int64_t)blockIdx.x * CHUNK;
+  const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
+  const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
+  const float* gp = a.dy + inst_base(nc, a.C, a.dysn, a.S) + b;
+  float* qp = a.y + inst_base(nc, a.C, a.ysn, a.S) + b;
+  double sb = 0.0;
+  if (a.vec) {
+    const int n4 = (int)((e - b) >> 2);
+    constexpr int U = VPT / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 vx[U], vg[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int i = threadIdx.x + (h * U + k) * NT;
+        if (i < n4) {
+          vx[k] = reinterpret_cast<const float4*>(xp)[i];
+          vg[k] = reinterpret_cast<const float4*>(gp)[i];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int i = threadIdx.x + (h * U + k) * NT;
+        if (i < n4) {
+          float4 o;
+          o.x = f(vx[k].x, vg[k].x);
+          o.y = f(vx[k].y, vg[k].y);
+          o.z = f(vx[k].z, vg[k].z);
+          o.w = f(vx[k].w, vg[k].w);
+          reinterpret_cast<float4*>(qp)[i] = o;
+          sb += ((double)o.x + (double)o.y) + ((double)o.z + (double)o.w);
+        }
+      }
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < e - b; i += NT) {
+      const float o = f(xp[i], gp[i]);
+      qp[i] = o;
+      sb += o;
+    }
+  }
+  if (!a.dbias) return;
+  // partial slot (n, block) of channel c; the last of the channel's N nblk blocks sums them in order
+  const int n = nc / a.C, c = nc % a.C, N = a.NC / a.C;
+  double in[1] = {sb}, tot[1];
+  block_sum<1>(in, tot);
+  double* pc = a.part + (int64_t)c * N * a.nblk;
+  if (!publish_last<1>(tot, pc, n * a.nblk + blockIdx.x, a.cnt + a.NC + c, (uint32_t)(N * a.nblk))) return;
+  double all[1];
+  reduce_partials<1>(pc, N * a.nblk, all);
+  if (threadIdx.x == 0) a.dbias[c] = (float)all[0];
+}
+
 inline bool vec_ok(const void* a, const void* b, const void* c, int64_t S) {
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return S % 4 == 0 && al(a) && al(b) && al(c);
@@ -445,5 +744,63 @@ int tb_dice_sums_bwd_f32(const float* x, const float* t, const float* g, float* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)((S + CHUNK - 1) / CHUNK), (unsigned)NC);
   hipLaunchKernelGGL(k_dice_sums_bwd, grid, dim3(NT), 0, st, x, t, g, dx, S, (sigmoid ? 1 : 0) | (squared ? 2 : 0));
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+// ------------------------------------------------------------------ strided, memset-free ADN: host
+namespace {
+inline int adn_nblk(int64_t S) { return (int)((S + CHUNK - 1) / CHUNK); }
+inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+}  // namespace
+
+size_t tb_adn_workspace_bytes(int64_t N, int64_t C, int64_t S) {
+  const int64_t NC = N * C, nb = adn_nblk(S);
+  return (size_t)(NC * nb * 3 + NC * 3 + 64) * sizeof(double);
+}
+
+int64_t tb_adn_counters(int64_t N, int64_t C) { return 2 * N * C + C + 1; }
+
+int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const float* res, int64_t rsn, float* mean,
+                   float* rstd, const float* prelu_w, int64_t N, int64_t C, int64_t S, float eps, void* ws,
+                   size_t ws_bytes, uint32_t* counters, void* stream) {
+  if (!x || !y || !mean || !rstd || !prelu_w || !ws || !counters || N < 1 || C < 1 || S < 1 || N * C > 65535)
+    return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb_adn_workspace_bytes(N, C, S)) return TB_ERR_WORKSPACE;
+  AdnArgs a{};
+  a.x = x, a.y = y, a.res = res;
+  a.xsn = xsn > 0 ? xsn : C * S, a.ysn = ysn > 0 ? ysn : C * S, a.rsn = rsn > 0 ? rsn : C * S;
+  a.mean = mean, a.rstd = rstd, a.aw = prelu_w;
+  a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  a.inst = a.part + N * C * adn_nblk(S) * 3;
+  a.cnt = counters;
+  a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S), a.eps = eps;
+  a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.rsn % 4 == 0 && al16(x) && al16(y) && al16(res);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)a.nblk, (unsigned)a.NC);
+  hipLaunchKernelGGL(k_adn_stats, grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(k_adn_apply, grid, dim3(NT), 0, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, float* dx, int64_t dxsn,
+                   const float* mean, const float* rstd, const float* prelu_w, float* dw, float* dbias, int64_t N,
+                   int64_t C, int64_t S, void* ws, size_t ws_bytes, uint32_t* counters, void* stream) {
+  if (!x || !dy || !dx || !mean || !rstd || !prelu_w || !ws || !counters || N < 1 || C < 1 || S < 1 ||
+      N * C > 65535)
+    return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb_adn_workspace_bytes(N, C, S)) return TB_ERR_WORKSPACE;
+  AdnArgs a{};
+  a.x = x, a.dy = dy, a.y = dx;
+  a.xsn = xsn > 0 ? xsn : C * S, a.dysn = dysn > 0 ? dysn : C * S, a.ysn = dxsn > 0 ? dxsn : C * S;
+  a.mean = const_cast<float*>(mean), a.rstd = const_cast<float*>(rstd), a.aw = prelu_w, a.dw = dw, a.dbias = dbias;
+  a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  a.inst = a.part + N * C * adn_nblk(S) * 3;
+  a.cnt = counters;
+  a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S);
+  a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.dysn % 4 == 0 && al16(x) && al16(dy) && al16(dx);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)a.nblk, (unsigned)a.NC);
+  hipLaunchKernelGGL(k_adn_bwd_stats, grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(k_adn_bwd_apply, grid, dim3(NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }

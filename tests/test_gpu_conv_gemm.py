@@ -26,7 +26,7 @@ def close64(ours, ref32, ref64):
 
 CONV = [(16, 32, (2, 12, 10, 8), 2, 3), (32, 64, (1, 6, 8, 10), 2, 3), (64, 128, (2, 6, 6, 4), 2, 3),
         (128, 128, (1, 5, 5, 4), 1, 3), (128, 256, (2, 3, 5, 4), 1, 3), (256, 256, (1, 3, 3, 2), 1, 3),
-        (128, 256, (2, 5, 5, 4), 1, 1), (4, 16, (1, 7, 5, 9), 1, 3), (12, 40, (2, 5, 7, 6), 2, 3),
+        (128, 256, (2, 5, 5, 4), 1, 1), (8, 16, (1, 7, 5, 9), 1, 3), (24, 40, (2, 5, 7, 6), 2, 3),
         (8, 24, (1, 9, 3, 5), 1, 3)]
 
 
@@ -62,7 +62,7 @@ def test_conv_dgrad_s1(conv, cin, cout, shape, s, k):
 
 
 @pytest.mark.parametrize("cin,cout,shape", [(384, 64, (2, 5, 5, 4)), (128, 32, (1, 6, 4, 6)), (64, 16, (2, 3, 4, 4)),
-                                            (32, 12, (1, 5, 3, 7)), (8, 40, (2, 2, 3, 5))])
+                                            (32, 12, (1, 5, 3, 7)), (8, 40, (2, 2, 3, 5)), (16, 4, (1, 3, 3, 4))])
 def test_convT_forward(conv, cin, cout, shape):
     torch.manual_seed(2)
     x = torch.randn((shape[0], cin) + shape[1:], device="cuda")
@@ -76,7 +76,7 @@ def test_convT_forward(conv, cin, cout, shape):
 
 
 @pytest.mark.parametrize("cin,cout,shape", [(16, 32, (2, 12, 10, 8)), (32, 64, (1, 6, 8, 10)), (64, 128, (2, 6, 6, 4)),
-                                            (12, 20, (1, 4, 6, 2))])
+                                            (12, 24, (1, 4, 6, 2))])
 def test_conv_s2_dgrad(conv, cin, cout, shape):
     """dX of Conv3d(cin -> cout, stride 2) on even extents = mode "convT" on dY with the layer's weight."""
     torch.manual_seed(3)
@@ -136,3 +136,12 @@ def test_c3_layer_shapes(conv, mode, cin, cout, sp, s, k):
         y = conv.conv_gemm(x, w, None, "convT", 2, 3)
         yr = F.conv_transpose3d(x, w, None, stride=2, padding=1, output_padding=1)
     assert (y - yr).abs().max().item() <= 2e-5 * yr.abs().max().item()
+
+
+def test_unsupported_channels_raise(conv):
+    """Cin % 8 != 0 is refused (the k order needs 8 channels per tap row group), not computed wrongly."""
+    from texbias._lib import TexbiasError
+    x = torch.randn((1, 4, 6, 6, 6), device="cuda")
+    w = torch.randn((16, 4, 3, 3, 3), device="cuda")
+    with pytest.raises(TexbiasError):
+        conv.conv_gemm(x, w, None, "conv", 1, 3)

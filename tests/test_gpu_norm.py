@@ -75,3 +75,35 @@ def test_unet_fused_matches_plain_modules(gpu, monkeypatch):
     for a, b in zip(g1, g2):
         err = (a.double() - b.double()).abs().max().item()
         assert err <= 2e-3 * max(b.abs().max().item(), 1e-4 * scale), (err, b.abs().max().item())
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 24, 20, 16), (2, 3, 15, 15, 10), (1, 5, 33, 31, 7)])
+def test_adn_strided_residual_bias(gpu, shape):
+    """tb_adn_fwd/bwd_f32 on channel slices of wider tensors (the stacked unit + residual conv output),
+    the residual summed into the store, the producing conv's bias gradient (= dx summed over n and the
+    voxels), the PReLU weight gradient; bit-identical on a second run (block-ordered reductions)."""
+    from texbias.norm import adn_backward, adn_forward
+    torch.manual_seed(1)
+    N, C = shape[:2]
+    wide = torch.randn((N, 2 * C) + shape[2:], device=gpu) * 1.5 + 0.3
+    z = wide[:, :C]                        # conv output: first half of the stacked tensor
+    r = wide[:, C:]                        # residual: second half
+    w = torch.tensor([0.2], device=gpu)
+    out = torch.empty((N, 3 * C) + shape[2:], device=gpu)[:, C:2 * C]
+    y, mean, rstd = adn_forward(z, w, 1e-5, res=r, out=out)
+    assert y.data_ptr() == out.data_ptr()
+    zr, wr, yr = _ref(z, w, 1e-5)
+    _close(y, yr + r.double())
+    g = torch.randn((N, C) + shape[2:], device=gpu)
+    dxbuf = torch.empty((N, 2 * C) + shape[2:], device=gpu)
+    dx, dw, db = adn_backward(z, g, mean, rstd, w, need_w=True, need_bias=True, dx_out=dxbuf[:, :C])
+    (yr * g.double()).sum().backward()
+    _close(dx, zr.grad)
+    _close(dw, wr.grad, tol=1e-5)
+    torch.testing.assert_close(db.double(), dx.double().sum(dim=(0, 2, 3, 4)), rtol=1e-6, atol=1e-6)
+    dx2, dw2, db2 = adn_backward(z, g, mean, rstd, w, need_w=True, need_bias=True)
+    assert torch.equal(dx2, dx) and torch.equal(dw2, dw) and torch.equal(db2, db)
+    y2, m2, s2 = adn_forward(z, w, 1e-5, res=r)
+    assert torch.equal(y2, y) and torch.equal(m2, mean) and torch.equal(s2, rstd)
+    from texbias.norm import counters
+    assert int(counters(z.device, 1).abs().sum().item()) == 0   # every counter left at zero
