@@ -304,8 +304,8 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
  * contiguous C S), the ResidualUnit's sum fused into the forward store (y = prelu(norm(x)) + res; res
  * may be NULL), and in the backward the preceding convolution's bias gradient dbias[c] = sum over n and
  * voxels of dx (NULL: not computed) and the PReLU weight gradient dw (NULL: not computed).  No
- * accumulator memsets and no float atomics: every block publishes partial sums, the last block of an
- * instance (channel) reduces them in block order -- results are deterministic.  `counters`: DEVICE
+ * accumulator memsets and no float atomics: every block stores partial sums, a one-block-per-instance
+ * (channel) finalize kernel sums them in block order -- results are deterministic.  `counters`: DEVICE
  * uint32[tb_adn_counters(N, C)], zero before the first call, left zero by every call (one set per
  * stream); ws: tb_adn_workspace_bytes(N, C, S) bytes of device scratch.
  */

@@ -175,15 +175,16 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
         rb[sl][i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, soff + r * xsc4, 0));
     }
   };
+  const uint32_t abytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)(4 * (int64_t)a.M * Kld));
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), 0, (int)abytes, 0x00020000);
   auto aload = [&](auto SL, int k0) {
     constexpr int sl = decltype(SL)::value;
 #pragma unroll
     for (int u = 0; u < AQ; ++u) {
       const int q4 = tid + NTH * u, row = q4 % BM, kq = k0 + 4 * (q4 / BM);
       const int m = m0 + row;
-      const bool ok = m < a.M && kq < k_end;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(A + (ok ? (int64_t)m * Kld + kq : 0));
-      ra[sl][u] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int vo = (m < a.M && kq < k_end) ? 4 * (m * Kld + kq) : (int)0x80000000;
+      ra[sl][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, vo, 0, 0));
     }
   };
   auto stage_store = [&](auto SL) {  // slot sl -> LDS buffer sl (stage s uses slot and buffer s & 1)
@@ -212,24 +213,25 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
 
   const int wm = w % WGM, wn = w / WGM;
   const int kk = lane >> 5, l32 = lane & 31;
-  auto compute = [&](auto SL) {
-    constexpr int sl = decltype(SL)::value;
+  // steps h*8 .. h*8+7 of the stage in LDS buffer sl
+  auto compute_half = [&](auto SL, auto H) {
+    constexpr int sl = decltype(SL)::value, h = decltype(H)::value;
     const float* L = lds_dyn + sl * LBUF;
-    f32x4 af[TM][4], bf[TN][4];
+    f32x4 af[TM][2], bf[TN][2];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
-      const float* src = L + ((wm * TM + tm) * 32 + l32) * RS + 16 * kk;
+      const float* src = L + ((wm * TM + tm) * 32 + l32) * RS + 16 * kk + 8 * h;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) af[tm][q] = *reinterpret_cast<const f32x4*>(src + 4 * q);
+      for (int q = 0; q < 2; ++q) af[tm][q] = *reinterpret_cast<const f32x4*>(src + 4 * q);
     }
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const float* src = L + (BM + (wn * TN + tn) * 32 + l32) * RS + 16 * kk;
+      const float* src = L + (BM + (wn * TN + tn) * 32 + l32) * RS + 16 * kk + 8 * h;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bf[tn][q] = *reinterpret_cast<const f32x4*>(src + 4 * q);
+      for (int q = 0; q < 2; ++q) bf[tn][q] = *reinterpret_cast<const f32x4*>(src + 4 * q);
     }
 #pragma unroll
-    for (int st = 0; st < 16; ++st)
+    for (int st = 0; st < 8; ++st)
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -244,20 +246,19 @@ __global__ __launch_bounds__(NTH) void k_conv_gemm(const CGArgs a) {
     gather(I0{}, k_beg);
     aload(I0{}, k_beg);
     stage_store(I0{});
-  }
-  if (nst > 1) {
     gather(I1{}, k_beg + KC);
     aload(I1{}, k_beg + KC);
   }
   __syncthreads();
+  // stage s: its first 8 MFMA steps, then the loads of stage s + 2 (past the end they read zeros through
+  // the descriptors' range check: no branches), the last 8 steps, stage s + 1 to the other LDS buffer
   auto body = [&](auto SL, int s) {
     using O = std::integral_constant<int, 1 - decltype(SL)::value>;
-    if (s + 2 < nst) {
-      gather(SL, k_beg + (s + 2) * KC);
-      aload(SL, k_beg + (s + 2) * KC);
-    }
-    compute(SL);
-    if (s + 1 < nst) stage_store(O{});
+    compute_half(SL, I0{});
+    gather(SL, k_beg + (s + 2) * KC);
+    aload(SL, k_beg + (s + 2) * KC);
+    compute_half(SL, I1{});
+    stage_store(O{});
     __syncthreads();
   };
   for (int s = 0; s < nst; s += 2) {
@@ -424,21 +425,20 @@ int make_plan(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride,
   a.ptiles = (a.P + pl.BP - 1) / pl.BP;
   int Kmax = 0;
   for (int c = 0; c < a.ncls; ++c) Kmax = a.Kc[c] > Kmax ? a.Kc[c] : Kmax;
-  // split k so that the blocks fill whole rounds of the chip's block slots (LDS-bound occupancy), each
-  // slice >= 4 stages; among splits within 3 % of the best fill the smallest (less partial traffic)
+  // split k to minimise (rounds of the chip's block slots) x (stages per block + a fixed per-block cost
+  // of ~3 stages: position decode, tap masks, partial stores); ties keep the smaller split
   const int64_t base = (int64_t)a.mtiles * a.ptiles * a.ncls;
   int occ = (int)(163840 / lds_bytes(pl.BM, pl.BP));
   occ = occ > 4 ? 4 : (occ < 1 ? 1 : occ);
   const int64_t slots = (int64_t)occ * num_cu();
   const int stages = (Kmax + KC - 1) / KC;
-  double best = 0.0;
+  double best = 1e30;
   int ns = 1;
-  for (int s = 1; s <= 16; ++s) {
-    if (s > 1 && stages / s < 4) break;
+  for (int s = 1; s <= 16 && s <= stages; ++s) {
     const int64_t blocks = base * s;
     const int64_t rounds = (blocks + slots - 1) / slots;
-    const double eff = (double)blocks / (double)(rounds * slots);
-    if (eff > best * 1.03) best = eff, ns = s;
+    const double cost = (double)rounds * ((stages + s - 1) / s + 3);
+    if (cost < best * 0.97) best = cost, ns = s;
   }
   a.kper = ((Kmax + ns - 1) / ns + KC - 1) / KC * KC;
   a.nsplit = (Kmax + a.kper - 1) / a.kper;

@@ -367,10 +367,13 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_apply(const float* __restri
 // The same arithmetic as K1-K4 with (a) per-sample batch strides, so that an ADN can read a channel slice
 // of a wider tensor (the stacked unit + residual convolution of a strided ResidualUnit) and write into
 // one; (b) the residual sum fused into the forward store; (c) the preceding convolution's bias gradient
-// (dx summed over n and the voxels) out of the backward's store pass; (d) no accumulator memsets: every
-// block stores its partial sums, counts itself in on a per-instance counter, and the last block of the
-// instance reduces the partials in block order (deterministic) and resets the counter -- the counters
-// live in a caller-owned buffer that is zero before the first call and is left zero by every call.
+// (dx summed over n and the voxels) out of the backward's store pass; (d) no accumulator memsets and no
+// float atomics: every block stores its partial sums and a one-block-per-instance finalize kernel sums
+// them in block order (deterministic).  (A last-arriving-block reduction inside the sweep kernels --
+// partial store, vmcnt drain, counter atomic at the end of every block -- measured 57.6 vs 36 us per
+// backward statistics sweep: the drain serialises each block's tail.)  The PReLU weight gradient, a sum
+// over instances, is taken by the last finalize block through one counter (a caller-owned uint32, zero
+// before the first call and left zero).
 struct AdnArgs {
   const float* x;
   const float* dy;
@@ -486,7 +489,12 @@ __global__ __launch_bounds__(NT) void k_adn_stats(const AdnArgs a) {
   }
   double in[2] = {s1, s2}, tot[2];
   block_sum<2>(in, tot);
-  if (!publish_last<2>(tot, a.part + (int64_t)nc * a.nblk * 2, blockIdx.x, a.cnt + nc, a.nblk)) return;
+  if (threadIdx.x < 2) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 2 + threadIdx.x] = tot[threadIdx.x];
+}
+
+// one block per instance: the instance's block partials summed in block order -> mean, rstd
+__global__ __launch_bounds__(NT) void k_adn_fin_fwd(const AdnArgs a) {
+  const int nc = blockIdx.x;
   double all[2];
   reduce_partials<2>(a.part + (int64_t)nc * a.nblk * 2, a.nblk, all);
   if (threadIdx.x == 0) {
@@ -582,18 +590,21 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
   }
   double in[3] = {s1, s2, sa}, tot[3];
   block_sum<3>(in, tot);
-  if (!publish_last<3>(tot, a.part + (int64_t)nc * a.nblk * 3, blockIdx.x, a.cnt + nc, a.nblk)) return;
+  if (threadIdx.x < 3) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 3 + threadIdx.x] = tot[threadIdx.x];
+}
+
+// one block per instance: mg, mgz and the instance's PReLU term; the last instance block to finish sums
+// the PReLU weight gradient over the instances (in instance order)
+__global__ __launch_bounds__(NT) void k_adn_fin_bwd(const AdnArgs a) {
+  const int nc = blockIdx.x;
   double all[3];
   reduce_partials<3>(a.part + (int64_t)nc * a.nblk * 3, a.nblk, all);
-  // instance results; the last instance to finish sums the PReLU weight gradient over instances
   double res[3] = {all[0] / (double)a.S, all[1] / (double)a.S, all[2]};
-  if (!publish_last<3>(res, a.inst, nc, a.cnt + 2 * a.NC + a.C, a.NC)) return;
-  if (a.dw) {
+  if (!publish_last<3>(res, a.inst, nc, a.cnt, a.NC)) return;
+  if (a.dw && threadIdx.x == 0) {
     double sw = 0.0;
-    if (threadIdx.x == 0) {
-      for (int i = 0; i < a.NC; ++i) sw += load_d(a.inst + 3 * i + 2);
-      *a.dw = (float)sw;
-    }
+    for (int i = 0; i < a.NC; ++i) sw += load_d(a.inst + 3 * i + 2);
+    *a.dw = (float)sw;
   }
 }
 
@@ -651,14 +662,18 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
     }
   }
   if (!a.dbias) return;
-  // partial slot (n, block) of channel c; the last of the channel's N nblk blocks sums them in order
+  // partial slot (n, block) of channel c
   const int n = nc / a.C, c = nc % a.C, N = a.NC / a.C;
   double in[1] = {sb}, tot[1];
   block_sum<1>(in, tot);
-  double* pc = a.part + (int64_t)c * N * a.nblk;
-  if (!publish_last<1>(tot, pc, n * a.nblk + blockIdx.x, a.cnt + a.NC + c, (uint32_t)(N * a.nblk))) return;
+  if (threadIdx.x == 0) a.part[(int64_t)c * N * a.nblk + n * a.nblk + blockIdx.x] = tot[0];
+}
+
+// one block per channel: dbias[c] = the channel's (n, block) partials summed in order
+__global__ __launch_bounds__(NT) void k_adn_fin_bias(const AdnArgs a) {
+  const int c = blockIdx.x, N = a.NC / a.C;
   double all[1];
-  reduce_partials<1>(pc, N * a.nblk, all);
+  reduce_partials<1>(a.part + (int64_t)c * N * a.nblk, N * a.nblk, all);
   if (threadIdx.x == 0) a.dbias[c] = (float)all[0];
 }
 
@@ -758,7 +773,7 @@ size_t tb_adn_workspace_bytes(int64_t N, int64_t C, int64_t S) {
   return (size_t)(NC * nb * 3 + NC * 3 + 64) * sizeof(double);
 }
 
-int64_t tb_adn_counters(int64_t N, int64_t C) { return 2 * N * C + C + 1; }
+int64_t tb_adn_counters(int64_t N, int64_t C) { return 1 + 0 * N * C; }
 
 int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const float* res, int64_t rsn, float* mean,
                    float* rstd, const float* prelu_w, int64_t N, int64_t C, int64_t S, float eps, void* ws,
@@ -778,6 +793,7 @@ int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const flo
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)a.nblk, (unsigned)a.NC);
   hipLaunchKernelGGL(k_adn_stats, grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(k_adn_fin_fwd, dim3((unsigned)a.NC), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(k_adn_apply, grid, dim3(NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
@@ -801,6 +817,8 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)a.nblk, (unsigned)a.NC);
   hipLaunchKernelGGL(k_adn_bwd_stats, grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(k_adn_fin_bwd, dim3((unsigned)a.NC), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(k_adn_bwd_apply, grid, dim3(NT), 0, st, a);
+  if (dbias) hipLaunchKernelGGL(k_adn_fin_bias, dim3((unsigned)C), dim3(NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }

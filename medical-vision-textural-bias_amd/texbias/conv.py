@@ -117,6 +117,10 @@ def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, pa
 
 
 GEMM = os.environ.get("TEXBIAS_CONVGEMM", "1") != "0"
+# the sub-pixel (ConvTranspose3d forward / stride-2 input gradient) and 1x1x1 forms of the GEMM kernel
+# measured slower than MIOpen at the C3 shapes (scripts/diag/gemm_conv_bench.py): off unless asked for
+GEMM_T = os.environ.get("TEXBIAS_CONVGEMM_T", "0") != "0"
+GEMM_1 = os.environ.get("TEXBIAS_CONVGEMM_1X1", "0") != "0"
 
 
 def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:
@@ -132,13 +136,13 @@ def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed:
         ok = k == (3, 3, 3) and s == 2 and p == 1 and tuple(output_padding) == (1, 1, 1) and x.shape[1] == w.shape[0]
     else:
         ok = x.shape[1] == w.shape[1] and ((k == (3, 3, 3) and p == 1 and s in (1, 2)) or
-                                           (k == (1, 1, 1) and p == 0 and s == 1))
+                                           (k == (1, 1, 1) and p == 0 and s == 1 and GEMM_1))
     return ok and x.shape[1] % 8 == 0 and x.numel() // x.shape[1] * 8 * max(w.shape[0], w.shape[1], x.shape[1]) < 2 ** 31
 
 
 def gemm_applies(x, w, stride, padding, transposed: bool, output_padding=(0, 0, 0)) -> bool:
     """Forward on the implicit-GEMM kernel (csrc/conv_gemm.hip)."""
-    return _gemm_geom_ok(x, w, stride, padding, transposed, output_padding)
+    return (GEMM_T or not transposed) and _gemm_geom_ok(x, w, stride, padding, transposed, output_padding)
 
 
 def gemm_dgrad_applies(gy, x, w, stride, padding, transposed: bool, output_padding=(0, 0, 0)) -> bool:
@@ -402,6 +406,7 @@ class Route:
                     and x.shape[-1] % 8 == 0 and x.shape[-1] // 2 <= 64 and all(n % 2 == 0 for n in x.shape[2:]):
                 self.dx = "convT64"   # Conv3d(16 -> 32, s2)'s input gradient on k_convT_mfma64
             elif self.kind != "aten" and _gemm_geom_ok(x, w, st, pd, transposed, op) and w.shape[0] % 8 == 0 and \
+                    (GEMM_T or (not transposed and st[0] == 1)) and \
                     (transposed or st[0] == 1 or all(n % 2 == 0 for n in x.shape[2:])) and \
                     (w.shape[1] % 8 == 0 if transposed else w.shape[0] % 8 == 0):
                 self.dx = "gemm"

@@ -16,20 +16,104 @@ Blocks (MONAI 0.5 semantics):
   conv, 1^3 conv when only the channel count changes, else identity), summed;
 * ``SkipConnection`` = cat([x, sub(x)], dim=1).
 
-It runs on PyTorch-ROCm (MIOpen/CK forward and input-gradient convolutions); the weight
-gradient of the long-reduction 3x3x3 layers runs on the texbias split-K MFMA kernel
-(``texbias.conv``), the one U-Net op where MIOpen has no usable gfx950 path.
+On HIP float32 tensors the blocks run as fused autograd functions over the texbias kernels
+(``texbias.conv`` routes each convolution, ``texbias.norm`` the ADN):
+* ``Convolution`` with an ADN: conv -> ADN in one function whose backward gets the conv's bias gradient
+  out of the ADN backward's store pass (no channel-sum sweep);
+* a strided ``ResidualUnit`` (unit0 and the residual are both Conv3d(cin -> c, 3, stride 2)): ONE stacked
+  convolution with 2c outputs, the residual half summed into the last ADN's store, one stacked input and
+  weight gradient in the backward (no gradient-accumulation add);
+* an identity-residual ``ResidualUnit``: the residual summed into the ADN store (or after the bare conv).
+Parameters and state dicts are those of the plain modules.
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence
 
 import torch
 import torch.nn as nn
 
+from . import conv as _conv
 from .conv import Conv3d, ConvTranspose3d
 from . import norm as _norm
-from .norm import instnorm_prelu
+from .norm import adn_backward, adn_forward, instnorm_prelu
+
+FUSED = os.environ.get("TEXBIAS_FUSED_UNITS", "1") != "0"
+
+
+def _fusable(x: torch.Tensor, conv: nn.Module, adn) -> bool:
+    if not (FUSED and _norm.ENABLED and x.is_cuda and x.dtype == torch.float32 and
+            isinstance(conv, (Conv3d, ConvTranspose3d)) and conv.groups == 1 and conv.dilation == (1, 1, 1) and
+            _conv.custom_backward_applies(x, conv.weight)):
+        return False
+    if isinstance(conv, Conv3d) and conv.padding_mode != "zeros":
+        return False
+    return adn is None or adn.D.p == 0.0 or not adn.training
+
+
+class _ConvADNFn(torch.autograd.Function):
+    """y = prelu(instance_norm(conv(x))) (+ res): MONAI Convolution "NDA" (+ the ResidualUnit's sum)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, a, route, eps, res):
+        z = route.forward(x.contiguous(), w, b)
+        y, mean, rstd = adn_forward(z, a, eps, res=res)
+        ctx.save_for_backward(x, w, a, z, mean, rstd)
+        ctx.route, ctx.has_b, ctx.has_res = route, b is not None, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, a, z, mean, rstd = ctx.saved_tensors
+        n = ctx.needs_input_grad
+        g = g.contiguous()
+        dz, da, db = adn_backward(z, g, mean, rstd, a, need_w=n[3], need_bias=ctx.has_b and n[2])
+        gx = ctx.route.input_grad(dz, x, w) if n[0] else None
+        gw = ctx.route.weight_grad(dz, x, w) if n[1] else None
+        return gx, gw, db, da, None, None, (g if ctx.has_res and n[6] else None)
+
+
+class _StackedUnitFn(torch.autograd.Function):
+    """A strided ResidualUnit: [unit0 | residual] = conv(x, [W0; Wr], stride 2) as one convolution,
+    a0 = ADN0(unit0), out = ADN1(conv1(a0)) + residual."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, wr, br, a0w, w1, b1, a1w, unit, eps):
+        c = w0.shape[0]
+        w_st = torch.cat([w0, wr], 0)
+        b_st = torch.cat([b0, br], 0) if b0 is not None and br is not None else None
+        x = x.contiguous()
+        r_st = unit.stacked_route(x, w_st)
+        y2 = r_st.forward(x, w_st, b_st)                      # [N, 2c, ...]
+        z0, res = y2[:, :c], y2[:, c:]
+        a0, m0, s0 = adn_forward(z0, a0w, eps)
+        conv1 = list(unit.conv.children())[1].conv
+        r1 = _conv.route_of(conv1, a0)
+        z1 = r1.forward(a0, w1, b1)
+        out, m1, s1 = adn_forward(z1, a1w, eps, res=res)
+        ctx.save_for_backward(x, w_st, a0w, w1, a1w, y2, a0, z1, m0, s0, m1, s1)
+        ctx.cfg = (c, r_st, r1, b0 is not None, b1 is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w_st, a0w, w1, a1w, y2, a0, z1, m0, s0, m1, s1 = ctx.saved_tensors
+        c, r_st, r1, has_b0, has_b1 = ctx.cfg
+        n = ctx.needs_input_grad
+        g = g.contiguous()
+        dz1, da1, db1 = adn_backward(z1, g, m1, s1, a1w, need_w=n[8], need_bias=has_b1)
+        da0 = r1.input_grad(dz1, a0, w1)
+        gw1 = r1.weight_grad(dz1, a0, w1) if n[6] else None
+        dy2 = torch.empty_like(y2)
+        dy2[:, c:].copy_(g)                                   # the residual conv's output gradient
+        _, dw0a, db0 = adn_backward(y2[:, :c], da0, m0, s0, a0w, need_w=n[5], need_bias=has_b0,
+                                    dx_out=dy2[:, :c])
+        gx = r_st.input_grad(dy2, x, w_st) if n[0] else None
+        gw_st = r_st.weight_grad(dy2, x, w_st) if (n[1] or n[3]) else None
+        dbr = _conv.channel_sum(g) if has_b0 and n[4] else None
+        return (gx, gw_st[:c] if gw_st is not None else None, db0, gw_st[c:] if gw_st is not None else None, dbr,
+                dw0a, gw1, db1 if n[7] else None, da1, None, None)
 
 
 class ADN(nn.Sequential):
@@ -59,6 +143,18 @@ class Convolution(nn.Sequential):
         if not conv_only:
             self.add_module("adn", ADN(cout, dropout))
 
+    def fused(self, x, res=None):
+        """conv -> ADN (+ res) as one autograd function, or None when the fused path does not apply."""
+        adn = getattr(self, "adn", None)
+        if adn is None or not _fusable(x, self.conv, adn):
+            return None
+        return _ConvADNFn.apply(x, self.conv.weight, self.conv.bias, adn.A.weight, _conv.route_of(self.conv, x),
+                                adn.N.eps, res)
+
+    def forward(self, x):
+        y = self.fused(x)
+        return y if y is not None else super().forward(x)
+
 
 class ResidualUnit(nn.Module):
     def __init__(self, cin: int, cout: int, strides: int = 1, kernel_size: int = 3, subunits: int = 2,
@@ -79,8 +175,33 @@ class ResidualUnit(nn.Module):
             self.residual = nn.Identity()
 
     def forward(self, x):
+        units = list(self.conv.children())
+        if isinstance(self.residual, Conv3d) and len(units) == 2 and all(hasattr(u, "adn") for u in units):
+            u0, u1 = units
+            r = self.residual
+            if r.stride == u0.conv.stride and r.kernel_size == u0.conv.kernel_size and r.padding == u0.conv.padding \
+                    and isinstance(u0.conv, Conv3d) and _fusable(x, u0.conv, u0.adn) and _fusable(x, r, None) and \
+                    _fusable(x, u1.conv, u1.adn) and (r.bias is None) == (u0.conv.bias is None) and \
+                    u0.adn.N.eps == u1.adn.N.eps and r.padding_mode == "zeros":
+                return _StackedUnitFn.apply(x, u0.conv.weight, u0.conv.bias, r.weight, r.bias, u0.adn.A.weight,
+                                            u1.conv.weight, u1.conv.bias, u1.adn.A.weight, self, u0.adn.N.eps)
+        if isinstance(self.residual, nn.Identity) and len(units) == 1 and hasattr(units[0], "adn"):
+            y = units[0].fused(x, res=x)
+            if y is not None:
+                return y
         res = self.residual(x)
         return self.conv(x) + res
+
+    def stacked_route(self, x: torch.Tensor, w_st: torch.Tensor) -> "_conv.Route":
+        """The route of the stacked [unit0; residual] convolution for this input (cached per shape)."""
+        r = self.residual
+        key = ("stacked", tuple(x.shape), x.dtype, x.device, x.data_ptr() % 16 == 0)
+        cache = self.__dict__.setdefault("_tb_routes", {})
+        rt = cache.get(key)
+        if rt is None:
+            rt = _conv.Route(x, w_st, r.stride, r.padding, (0, 0, 0), False)
+            cache[key] = rt
+        return rt
 
 
 class SkipConnection(nn.Module):

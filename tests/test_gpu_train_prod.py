@@ -121,7 +121,7 @@ def test_small_conv_full_volume_3_3(conv):
     x = torch.randn((2, 3, 240, 240, 160), device="cuda", requires_grad=True)
     assert conv.small_conv_applies(x, m.weight, m.stride, m.padding)
     y = m(x)
-    assert "SmallConv" in type(y.grad_fn).__name__
+    assert conv.route_of(m, x).kind == "small" and "RouteFn" in type(y.grad_fn).__name__
     yr = conv_ref64(x.detach(), m.weight.detach(), m.bias.detach())
     assert relmax(y, yr) < 1e-5
     del yr
@@ -170,31 +170,24 @@ def test_dice_full_volume(gpu):
 
 def test_train_step_full_volume_finite_and_fast_paths(gpu):
     """One bench-shaped train step: every 3x3x3 layer whose gate opens takes the MFMA weight
-    gradient, and the step's loss and gradients are finite."""
-    from texbias import conv as C
+    gradient, and the step's loss and gradients are finite.  The layers' kernel choices are the routes the
+    step cached on the modules (texbias.conv.Route; the stacked strided units on their ResidualUnit)."""
     from texbias.train import TrainStep, reference_model
     torch.manual_seed(4)
     model = reference_model(4, 3)
-    fast = []
-
-    def hook(mod, inp, out):
-        x = inp[0]
-        if isinstance(mod, C.ConvTranspose3d):
-            fast.append(C.fast_wgrad_applies(x, mod.weight, None, mod.stride, mod.padding, True))
-        elif mod.weight.shape[2:] == (3, 3, 3):
-            fast.append(C.fast_wgrad_applies(x, mod.weight, list(out.shape[2:]), mod.stride, mod.padding, False)
-                        or C.small_conv_applies(x, mod.weight, mod.stride, mod.padding))
-    hs = [m.register_forward_hook(hook) for m in model.modules() if isinstance(m, (C.Conv3d, C.ConvTranspose3d))]
     step = TrainStep(model, torch.device("cuda"))
     x = torch.randn((2, 4, 240, 240, 160), device="cuda")
     lab = (torch.rand((2, 3, 240, 240, 160), device="cuda") > 0.85).float()
     loss = step(x, lab)
-    for h in hs:
-        h.remove()
     assert torch.isfinite(loss).item()
     assert all(torch.isfinite(p).all().item() for p in model.parameters())
+    routes = [r for m in model.modules() for r in m.__dict__.get("_tb_routes", {}).values()]
+    fast = [r.fast_w for r in routes if r.k == 3]
+    kinds = sorted(r.kind for r in routes)
+    print("routes:", kinds)
     # the full- and half-resolution layers (the expensive ones) are all on the texbias kernels
-    assert sum(fast) >= 10, fast
+    assert sum(fast) >= 9, (fast, kinds)
+    assert sum(k != "aten" for k in kinds) >= 12, kinds
 
 
 def test_train_step_full_volume_matches_aten(gpu, heartbeat):
