@@ -600,12 +600,11 @@ __global__ __launch_bounds__(NT) void k_adn_fin_bwd(const AdnArgs a) {
   double all[3];
   reduce_partials<3>(a.part + (int64_t)nc * a.nblk * 3, a.nblk, all);
   double res[3] = {all[0] / (double)a.S, all[1] / (double)a.S, all[2]};
-  if (!publish_last<3>(res, a.inst, nc, a.cnt, a.NC)) return;
-  if (a.dw && threadIdx.x == 0) {
-    double sw = 0.0;
-    for (int i = 0; i < a.NC; ++i) sw += load_d(a.inst + 3 * i + 2);
-    *a.dw = (float)sw;
-  }
+  if (!publish_last<3>(res, a.inst, nc, a.cnt, a.NC) || !a.dw) return;
+  double v[1] = {0.0}, sw[1];
+  for (int i = threadIdx.x; i < a.NC; i += NT) v[0] += load_d(a.inst + 3 * i + 2);
+  block_sum<1>(v, sw);
+  if (threadIdx.x == 0) *a.dw = (float)sw[0];
 }
 
 // dx = rstd (g - mg - z mgz); dbias[c] = sum over n and voxels of dx (partials + per-channel counter)

@@ -402,13 +402,16 @@ class Route:
             self.dx = self.kind
         else:
             self.dx = "aten"
-            if self.kind != "aten" and not transposed and st[0] == 2 and tuple(w.shape) == (32, 16, 3, 3, 3) and CONVT64 \
-                    and x.shape[-1] % 8 == 0 and x.shape[-1] // 2 <= 64 and all(n % 2 == 0 for n in x.shape[2:]):
-                self.dx = "convT64"   # Conv3d(16 -> 32, s2)'s input gradient on k_convT_mfma64
-            elif self.kind != "aten" and _gemm_geom_ok(x, w, st, pd, transposed, op) and w.shape[0] % 8 == 0 and \
-                    (GEMM_T or (not transposed and st[0] == 1)) and \
-                    (transposed or st[0] == 1 or all(n % 2 == 0 for n in x.shape[2:])) and \
-                    (w.shape[1] % 8 == 0 if transposed else w.shape[0] % 8 == 0):
+            if self.kind != "aten" and not transposed and st[0] == 2 and tuple(w.shape) in ((32, 16, 3, 3, 3),
+                                                                                         (64, 16, 3, 3, 3)) \
+                    and CONVT64 and x.shape[-1] % 8 == 0 and x.shape[-1] // 2 <= 64 and \
+                    all(n % 2 == 0 for n in x.shape[2:]):
+                self.dx = "convT64"   # Conv3d(16 -> 32 / 64 stacked, s2)'s input gradient on k_convT_mfma64
+            elif self.kind != "aten" and _gemm_geom_ok(x, w, st, pd, transposed, op) and \
+                    (w.shape[1] % 8 == 0 if transposed else w.shape[0] % 8 == 0) and \
+                    (transposed or st[0] == 1 or (GEMM_T and all(n % 2 == 0 for n in x.shape[2:]))):
+                # ConvTranspose3d: a stride-2 Conv3d of dY (the GEMM's conv form); stride-1 Conv3d: the
+                # flipped-weight form; stride-2 Conv3d: the sub-pixel form (GEMM_T)
                 self.dx = "gemm"
         # weight gradient: the texbias MFMA kernels where a tiling exists and the reduction is long
         if self.kind in ("fwd16", "mfma", "fewin", "small", "fewout"):
