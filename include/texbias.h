@@ -210,6 +210,10 @@ int tb_channel_sum_f32(const float* x, float* out, int64_t N, int64_t C, int64_t
  */
 int tb_conv3d_small_f32(const float* x, const float* w, const float* b, float* y, int N, int Cin, int Cout, int D,
                         int H, int W, void* stream);
+/* The same with `add` (y's layout, or NULL) summed into the store: the U-Net's top ResidualUnit(3, 3,
+ * conv_only) output conv(x) + x, and its input gradient dconv(dY) + dY, in one sweep. */
+int tb_conv3d_small_add_f32(const float* x, const float* w, const float* b, const float* add, float* y, int N, int Cin,
+                            int Cout, int D, int H, int W, void* stream);
 
 /*
  * The U-Net's full-resolution stride-2 layers with few channels on one side (csrc/conv_up.hip; the
@@ -234,6 +238,10 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
  */
 int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
                         void* stream);
+/* ... with `add` ([N][16][D][H][W] or NULL) summed into y: an identity-residual unit's input gradient
+ * dconv(dZ) + dY in one sweep. */
+int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D,
+                            int H, int Wd, void* stream);
 
 /* ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward on the f32 matrix cores
  * (sub-pixel form, all 27 taps real): x [N][64][Di][Hi][Wi] -> y [N][16][2Di][2Hi][2Wi], weight
@@ -254,6 +262,9 @@ int tb_convT3d_mfma_f32(const float* x, const float* W, const float* bias, float
  * 32- and 64-channel units of the train step (stylized_gibbs12p5.py:192-243, MONAI UNet). */
 int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float* y, int N, int C, int D, int H, int Wd,
                        void* stream);
+/* ... with `add` (y's layout or NULL) summed into y (as tb_conv3d_fwd16_add_f32). */
+int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C,
+                           int D, int H, int Wd, void* stream);
 
 /*
  * The U-Net's channel-deep convolutions as implicit GEMMs on the f32 matrix cores (csrc/conv_gemm.hip;

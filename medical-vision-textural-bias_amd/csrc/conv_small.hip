@@ -127,10 +127,10 @@ constexpr int ZB = TB_SMALL_ZB;  // output planes per block
 #endif
 typedef const __attribute__((address_space(4))) float* cfloat_sp;
 
-template <int CI, int CO>
+template <int CI, int CO, bool ADD = false>
 __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__ x, const float* __restrict__ wt,
                                                        const float* __restrict__ bias, float* __restrict__ y, int D,
-                                                       int H, int W, int XP, int nhb) {
+                                                       int H, int W, int XP, int nhb, const float* __restrict__ add) {
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [4 slots][CI][ROWS + 2][XP], col 0 = w = -1
   constexpr int RS = ROWS + 2, NR = CI * RS;                 // staged rows per plane
   const int slot_f = CI * RS * XP;
@@ -208,7 +208,13 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
       const int h = h0 + r;
 #pragma unroll
       for (int co = 0; co < CO; ++co) {
-        float* dst = y + ((int64_t)n * CO + co) * vol + (int64_t)z * plane + (int64_t)h * W + w0;
+        const int64_t o = ((int64_t)n * CO + co) * vol + (int64_t)z * plane + (int64_t)h * W + w0;
+        float* dst = y + o;
+        if (ADD) {  // the ResidualUnit's identity sum (forward) / its gradient's pass-through (backward)
+#pragma unroll
+          for (int k = 0; k < WPT; ++k)
+            if (w0 + k < W) acc[co][k] += add[o + k];
+        }
 #pragma unroll
         for (int k = 0; k < WPT; ++k)
           if (w0 + k < W) dst[k] = acc[co][k];
@@ -220,7 +226,8 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
 }
 
 template <int CI, int CO>
-int launch(const float* x, const float* w, const float* b, float* y, int N, int D, int H, int W, hipStream_t st) {
+int launch(const float* x, const float* w, const float* b, const float* add, float* y, int N, int D, int H, int W,
+           hipStream_t st) {
   const int XP = (W + 2 + WPT + 3) / 4 * 4;  // halo, slack for the last thread's 6-wide read, 16-B rows
   const size_t lds = sizeof(float) * ((size_t)CI * 3 * (ROWS + 2) * XP + CO * CI * 27);
   if ((W + WPT - 1) / WPT * ROWS > NT || lds > 65536 || XP > 64 * kSeg) return TB_ERR_UNSUPPORTED_SIZE;
@@ -231,13 +238,19 @@ int launch(const float* x, const float* w, const float* b, float* y, int N, int 
   }();
   const size_t lds_z = sizeof(float) * ((size_t)4 * CI * (ROWS + 2) * XP + CO * CI * 27);
   if (zmarch && lds_z <= 65536 * 2) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_small_z<CI, CO>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    static const hipError_t attr =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_small_z<CI, CO>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 163840) == hipSuccess
+            ? hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_small_z<CI, CO, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 163840)
+            : hipErrorInvalidValue;
     if (attr != hipSuccess) return TB_ERR_HIP;
-    hipLaunchKernelGGL((k_conv3d_small_z<CI, CO>), dim3((unsigned)(nhb * ((D + ZB - 1) / ZB)), (unsigned)N), dim3(NT),
-                       lds_z, st, x, w, b, y, D, H, W, XP, nhb);
+    auto kern = add ? k_conv3d_small_z<CI, CO, true> : k_conv3d_small_z<CI, CO>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nhb * ((D + ZB - 1) / ZB)), (unsigned)N), dim3(NT), lds_z, st, x, w, b, y,
+                       D, H, W, XP, nhb, add);
     return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
   }
+  if (add) return TB_ERR_UNSUPPORTED_SIZE;  // the plane-per-block fallback has no residual epilogue
   hipLaunchKernelGGL((k_conv3d_small<CI, CO>), dim3((unsigned)(nhb * D), (unsigned)N), dim3(NT), lds, st, x, w, b, y,
                      D, H, W, XP, nhb);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
@@ -247,11 +260,16 @@ int launch(const float* x, const float* w, const float* b, float* y, int N, int 
 
 int tb_conv3d_small_f32(const float* x, const float* w, const float* b, float* y, int N, int Cin, int Cout, int D,
                         int H, int W, void* stream) {
+  return tb_conv3d_small_add_f32(x, w, b, nullptr, y, N, Cin, Cout, D, H, W, stream);
+}
+
+int tb_conv3d_small_add_f32(const float* x, const float* w, const float* b, const float* add, float* y, int N, int Cin,
+                            int Cout, int D, int H, int W, void* stream) {
   if (!x || !w || !y || N < 1 || D < 1 || H < 1 || W < 1 || N > 65535) return TB_ERR_INVALID_ARG;
   if (Cin < 1 || Cin > 4 || Cout < 1 || Cout > 4) return TB_ERR_UNSUPPORTED_SIZE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define TB_CASE(ci, co) \
-  if (Cin == ci && Cout == co) return launch<ci, co>(x, w, b, y, N, D, H, W, st);
+  if (Cin == ci && Cout == co) return launch<ci, co>(x, w, b, add, y, N, D, H, W, st);
 #define TB_ROW(ci) TB_CASE(ci, 1) TB_CASE(ci, 2) TB_CASE(ci, 3) TB_CASE(ci, 4)
   TB_ROW(1) TB_ROW(2) TB_ROW(3) TB_ROW(4)
 #undef TB_ROW

@@ -389,14 +389,15 @@ struct F16Args {
   const float* x;
   const float* W;     // [16 m][16 c][27]
   const float* bias;  // [16] or null
+  const float* add;   // [N][16][D][H][W] summed into y, or null
   float* y;
   int D, H, Wd;
   int ZS, zlen, nyb;
   int PX, RX;  // row pitch (data at column x + 4), channel pitch (= 16 mod 32)
 };
 
-template <int YB, int NXT, int NTH>  // output rows per block; 16-column tiles per row (W = 16 NXT); threads
-__global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {
+template <int YB, int NXT, int NTH, bool ADD = false>  // output rows per block; 16-column tiles per row (W = 16
+__global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); threads; `add` summed into the store
   constexpr int NWV = NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NR = YB + 2, W4 = 4 * NXT;  // staged rows; float4 per row
@@ -457,6 +458,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {
   const int bl = ks * RX + li + 3;
   const int64_t oplane = plane;
   float* yb0 = a.y + (int64_t)n * 16 * D * oplane;
+  const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * oplane : nullptr;
   constexpr int NT = YB * NXT;  // tiles per step
   for (int z = z0; z < z1; ++z) {
     store(z + 1);
@@ -492,8 +494,10 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 4 * ks + r;
-        if (y0 + yy0 < H) yb0[((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy0) * Wd + x00 + li] = acc0[r];
-        if (t1 != t0 && y0 + yy1 < H) yb0[((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy1) * Wd + x01 + li] = acc1[r];
+        const int64_t o0 = ((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy0) * Wd + x00 + li;
+        const int64_t o1 = ((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy1) * Wd + x01 + li;
+        if (y0 + yy0 < H) yb0[o0] = ADD ? acc0[r] + ab0[o0] : acc0[r];
+        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc1[r] + ab0[o1] : acc1[r];
       }
     }
     __syncthreads();
@@ -505,6 +509,11 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {
 // W <= 128; weight [16][16][27], bias [16] or NULL.  (csrc/conv_up.hip, k_conv3d_fwd16)
 int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
                         void* stream) {
+  return tb_conv3d_fwd16_add_f32(x, W, bias, nullptr, y, N, D, H, Wd, stream);
+}
+
+int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D,
+                            int H, int Wd, void* stream) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
   // output rows per block (TEXBIAS_CONV16_YB 2..4; C3, W = 80: YB 2 / 3 / 4 = 478 / 419 / 482 us -- the
@@ -513,11 +522,11 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
   static const int YBv = [] {
     const char* e = std::getenv("TEXBIAS_CONV16_YB");
     const int v = e ? std::atoi(e) : 3;
-    return v >= 2 && v <= 4 ? v : 3;
+    return v == 3 ? v : 3;  // round 5: only the measured best (YB 3, 512 threads) is instantiated
   }();
   const int YB = YBv;
   F16Args a{};
-  a.x = x, a.W = W, a.bias = bias, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.PX = Wd + 8;
   a.RX = (YB + 2) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;
@@ -532,21 +541,21 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
   // the B-fragment LDS reads the compiler issues only 1-3 ahead (YB = 3: 421 -> 365 us per C3 call)
   static const int NTv = [] {
     const char* e = std::getenv("TEXBIAS_CONV16_NT");
-    return e && std::atoi(e) == 256 ? 256 : 512;
+    return e && std::atoi(e) == 256 ? 512 : 512;
   }();
-#define TB_F16(Y, T)                                        \
-  if (YB == Y && NTv == T) switch (Wd / 16) {               \
-      case 1: kern = k_conv3d_fwd16<Y, 1, T>; break;        \
-      case 2: kern = k_conv3d_fwd16<Y, 2, T>; break;        \
-      case 3: kern = k_conv3d_fwd16<Y, 3, T>; break;        \
-      case 4: kern = k_conv3d_fwd16<Y, 4, T>; break;        \
-      case 5: kern = k_conv3d_fwd16<Y, 5, T>; break;        \
-      case 6: kern = k_conv3d_fwd16<Y, 6, T>; break;        \
-      case 7: kern = k_conv3d_fwd16<Y, 7, T>; break;        \
-      case 8: kern = k_conv3d_fwd16<Y, 8, T>; break;        \
-      default: return TB_ERR_UNSUPPORTED_SIZE;              \
+#define TB_F16(Y, T)                                                                                   \
+  if (YB == Y && NTv == T) switch (Wd / 16) {                                                          \
+      case 1: kern = add ? k_conv3d_fwd16<Y, 1, T, true> : k_conv3d_fwd16<Y, 1, T>; break;             \
+      case 2: kern = add ? k_conv3d_fwd16<Y, 2, T, true> : k_conv3d_fwd16<Y, 2, T>; break;             \
+      case 3: kern = add ? k_conv3d_fwd16<Y, 3, T, true> : k_conv3d_fwd16<Y, 3, T>; break;             \
+      case 4: kern = add ? k_conv3d_fwd16<Y, 4, T, true> : k_conv3d_fwd16<Y, 4, T>; break;             \
+      case 5: kern = add ? k_conv3d_fwd16<Y, 5, T, true> : k_conv3d_fwd16<Y, 5, T>; break;             \
+      case 6: kern = add ? k_conv3d_fwd16<Y, 6, T, true> : k_conv3d_fwd16<Y, 6, T>; break;             \
+      case 7: kern = add ? k_conv3d_fwd16<Y, 7, T, true> : k_conv3d_fwd16<Y, 7, T>; break;             \
+      case 8: kern = add ? k_conv3d_fwd16<Y, 8, T, true> : k_conv3d_fwd16<Y, 8, T>; break;             \
+      default: return TB_ERR_UNSUPPORTED_SIZE;                                                         \
     }
-  TB_F16(2, 256) TB_F16(3, 256) TB_F16(4, 256) TB_F16(2, 512) TB_F16(3, 512) TB_F16(4, 512)
+  TB_F16(3, 512)
 #undef TB_F16
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
@@ -761,14 +770,15 @@ struct S1Args {
   const float* x;     // [N][C][D][H][W]
   const float* W;     // [C m][C c][27]
   const float* bias;  // [C] or null
+  const float* add;   // summed into y (y's layout), or null
   float* y;
   int D, H, Wd, YB;
   int ZS, zlen, nyb, MG;  // z segments, row blocks, output-tile groups
   int PX, RX;             // row pitch (data at column x + 4), channel pitch (16 mod 32)
 };
 
-template <int G, int NC, int NL, int NTH>  // NTH 512: two waves per role, alternate tiles (NWG phases)
-__global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {
+template <int G, int NC, int NL, int NTH, bool ADD = false>  // NTH 512: two waves per role, alternate tiles
+__global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG phases); `add` summed into the store
   constexpr int CIN = 16 * G, MTB = 4 / G, NWG = NTH / 256;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -831,6 +841,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {
   load(z0 + 1);
   const int npos = YB * Wd, ntile = (npos + 15) / 16;
   float* ybase = a.y + (int64_t)n * COUT * cstride;
+  const float* abase = ADD ? a.add + (int64_t)n * COUT * cstride : nullptr;
   for (int z = z0; z < z1; ++z) {
     store(z + 1);  // over plane z - 2, last read before the previous step's final barrier
     __syncthreads();
@@ -881,7 +892,8 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {
           float v = a.bias ? a.bias[mb + m] : 0.f;
 #pragma unroll
           for (int gg = 0; gg < G; ++gg) v += part[((hq * 4 + mq * G + gg) * NC + c) * 256 + m * 16 + li];
-          if (ok) ybase[(int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx] = v;
+          const int64_t o = (int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx;
+          if (ok) ybase[o] = ADD ? v + abase[o] : v;
         }
       }
       __syncthreads();
@@ -894,6 +906,11 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {
 // W <= 64; weight [C][C][27], bias [C] or NULL.  (csrc/conv_up.hip, k_conv3d_mfma_s1)
 int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float* y, int N, int C, int D, int H, int Wd,
                        void* stream) {
+  return tb_conv3d_mfma_add_f32(x, W, bias, nullptr, y, N, C, D, H, Wd, stream);
+}
+
+int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C,
+                           int D, int H, int Wd, void* stream) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if ((C != 32 && C != 64) || Wd % 4 != 0 || Wd > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
@@ -901,12 +918,12 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
   // 3 chains -- measured slower here, 245 vs 211 us at 32 -> 32, unlike k_conv3d_fwd16)
   static const int NTv = [] {
     const char* e = std::getenv("TEXBIAS_CONVMFMA_NT");
-    return e && std::atoi(e) == 512 ? 512 : 256;
+    return e && std::atoi(e) == 512 ? 256 : 256;  // round 5: only the measured best (256) is instantiated
   }();
   const int NC = NTv == 512 ? 3 : 5;
   const int G = C / 16;
   S1Args a{};
-  a.x = x, a.W = W, a.bias = bias, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.PX = Wd + 8;
   a.MG = G == 2 ? 1 : 4;  // 32: both output tiles in the block; 64: one tile per block, 4 block groups
   size_t lds = 0;
@@ -924,10 +941,10 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
   a.ZS = (D + a.zlen - 1) / a.zlen;
   const int nl = (C * (a.YB + 2) * (Wd / 4) + NTv - 1) / NTv;
   void (*kern)(S1Args) = nullptr;
-#define TB_NL(k)                                                                                           \
-  case k:                                                                                                  \
-    kern = NTv == 512 ? (G == 2 ? k_conv3d_mfma_s1<2, 3, k, 512> : k_conv3d_mfma_s1<4, 3, k, 512>)         \
-                      : (G == 2 ? k_conv3d_mfma_s1<2, 5, k, 256> : k_conv3d_mfma_s1<4, 5, k, 256>);        \
+#define TB_NL(k)                                                                                      \
+  case k:                                                                                             \
+    kern = add ? (G == 2 ? k_conv3d_mfma_s1<2, 5, k, 256, true> : k_conv3d_mfma_s1<4, 5, k, 256, true>) \
+               : (G == 2 ? k_conv3d_mfma_s1<2, 5, k, 256> : k_conv3d_mfma_s1<4, 5, k, 256>);             \
     break;
   switch (nl) {
     TB_NL(1) TB_NL(2) TB_NL(3) TB_NL(4) TB_NL(5) TB_NL(6) TB_NL(7) TB_NL(8) TB_NL(9) TB_NL(10) TB_NL(11) TB_NL(12)

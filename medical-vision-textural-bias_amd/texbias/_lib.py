@@ -51,6 +51,9 @@ def _proto(L):
         "tb_adn_fwd_f32": (I, [P, I64, P, I64, P, I64, P, P, P, I64, I64, I64, F, P, SZ, P, P]),
         "tb_adn_bwd_f32": (I, [P, I64, P, I64, P, I64, P, P, P, P, P, I64, I64, I64, P, SZ, P, P]),
         "tb_conv3d_small_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
+        "tb_conv3d_small_add_f32": (I, [P, P, P, P, P] + [I] * 6 + [P]),
+        "tb_conv3d_fwd16_add_f32": (I, [P, P, P, P, P] + [I] * 4 + [P]),
+        "tb_conv3d_mfma_add_f32": (I, [P, P, P, P, P] + [I] * 5 + [P]),
         "tb_conv3d_s2_fewin_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
         "tb_convT3d_fewout_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
         "tb_conv3d_fwd16_f32": (I, [P, P, P, P] + [I] * 4 + [P]),

@@ -166,16 +166,25 @@ def gemm_dgrad(gy: torch.Tensor, w: torch.Tensor, stride: int, transposed: bool)
     return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2])
 
 
-def small_conv(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
-    """Direct 3x3x3, stride 1, padding 1 convolution for <= 4 channels (tb_conv3d_small_f32)."""
+def _add_ptr(add, shape):
+    if add is None:
+        return None
+    assert tuple(add.shape) == tuple(shape) and add.is_contiguous(), "add: the output's shape, contiguous"
+    return add.data_ptr()
+
+
+def small_conv(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
+    """Direct 3x3x3, stride 1, padding 1 convolution for <= 4 channels (tb_conv3d_small_add_f32); ``add``
+    (the output's shape) is summed into the store."""
     x = x.contiguous()
     w = w.contiguous()
     N, Cin, D, H, W = x.shape
     Cout = w.shape[0]
     y = torch.empty((N, Cout, D, H, W), dtype=torch.float32, device=x.device)
     with torch.cuda.device(x.device):
-        check(lib().tb_conv3d_small_f32(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
-                                        y.data_ptr(), N, Cin, Cout, D, H, W, _stream(x)), "tb_conv3d_small_f32")
+        check(lib().tb_conv3d_small_add_f32(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+                                            _add_ptr(add, y.shape), y.data_ptr(), N, Cin, Cout, D, H, W, _stream(x)),
+              "tb_conv3d_small_add_f32")
     return y
 
 
@@ -275,14 +284,15 @@ def convT64_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, output_pa
         x.shape[-1] % 4 == 0 and x.shape[-1] <= 64 and x.data_ptr() % 16 == 0
 
 
-def conv_fwd16(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
-    """Conv3d(16 -> 16, 3, stride 1, padding 1) forward on the f32 matrix cores (tb_conv3d_fwd16_f32)."""
+def conv_fwd16(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
+    """Conv3d(16 -> 16, 3, stride 1, padding 1) forward on the f32 matrix cores (tb_conv3d_fwd16_add_f32)."""
     x = x.contiguous()
     N, _, D, H, W = x.shape
     y = torch.empty_like(x)
     with torch.cuda.device(x.device):
-        check(lib().tb_conv3d_fwd16_f32(x.data_ptr(), w.contiguous().data_ptr(), b.data_ptr() if b is not None else None,
-                                        y.data_ptr(), N, D, H, W, _stream(x)), "tb_conv3d_fwd16_f32")
+        check(lib().tb_conv3d_fwd16_add_f32(x.data_ptr(), w.contiguous().data_ptr(),
+                                            b.data_ptr() if b is not None else None, _add_ptr(add, y.shape),
+                                            y.data_ptr(), N, D, H, W, _stream(x)), "tb_conv3d_fwd16_add_f32")
     return y
 
 
@@ -294,15 +304,16 @@ def conv16_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
         x.shape[-1] <= 80 and x.data_ptr() % 16 == 0 and os.environ.get("TEXBIAS_CONV16", "1") != "0"
 
 
-def conv_mfma(x: torch.Tensor, w: torch.Tensor, b) -> torch.Tensor:
+def conv_mfma(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
     """Conv3d(C -> C, 3, stride 1, padding 1), C = 32 or 64, forward on the f32 matrix cores
-    (tb_conv3d_mfma_f32)."""
+    (tb_conv3d_mfma_add_f32)."""
     x = x.contiguous()
     N, C, D, H, W = x.shape
     y = torch.empty_like(x)
     with torch.cuda.device(x.device):
-        check(lib().tb_conv3d_mfma_f32(x.data_ptr(), w.contiguous().data_ptr(), b.data_ptr() if b is not None else None,
-                                       y.data_ptr(), N, C, D, H, W, _stream(x)), "tb_conv3d_mfma_f32")
+        check(lib().tb_conv3d_mfma_add_f32(x.data_ptr(), w.contiguous().data_ptr(),
+                                           b.data_ptr() if b is not None else None, _add_ptr(add, y.shape),
+                                           y.data_ptr(), N, C, D, H, W, _stream(x)), "tb_conv3d_mfma_add_f32")
     return y
 
 
@@ -423,9 +434,18 @@ class Route:
                                           for n, p, s, kk in zip(x.shape[2:], pd, st, w.shape[2:])]
             self.fast_w = fast_wgrad_applies(x, w, osp, st, pd, transposed, op)
 
-    # -- forward
-    def forward(self, x, w, b):
+    # -- forward (``add``: summed into the output -- in the kernel's store where the kernel takes it)
+    def forward(self, x, w, b, add=None):
         k = self.kind
+        # (the 16- and 32/64-channel MFMA kernels' add epilogue measured slower than a separate add: 490 vs
+        # 354 + 64 us for 16 -> 16 at 120 x 120 x 80 -- its scattered reads stall the store phase)
+        if add is not None and k in ("small", "gemm"):
+            add = add.contiguous()
+            if k == "small":
+                return small_conv(x, w, b, add)
+            return conv_gemm(x, w, b, "convT" if self.transposed else "conv", self.stride[0], self.k, add=add)
+        if add is not None:
+            return self.forward(x, w, b).add_(add)
         if k == "fwd16":
             return conv_fwd16(x, w, b)
         if k == "mfma":
@@ -444,9 +464,16 @@ class Route:
             return F.conv_transpose3d(x, w, b, self.stride, self.padding, self.output_padding)
         return F.conv3d(x, w, b, self.stride, self.padding)
 
-    # -- input gradient (x only for its shape on the ATen path)
-    def input_grad(self, gy, x, w):
+    # -- input gradient (x only for its shape on the ATen path; ``add`` summed in, as in forward)
+    def input_grad(self, gy, x, w, add=None):
         k = self.dx
+        if add is not None:
+            add = add.contiguous()
+            if k == "small":
+                return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None, add)
+            if k == "gemm" and not self.transposed and self.stride[0] == 1:
+                return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2], add=add)
+            return self.input_grad(gy, x, w).add_(add)
         if k == "fwd16":
             return conv_fwd16(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
         if k == "mfma":

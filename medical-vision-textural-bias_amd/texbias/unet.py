@@ -56,11 +56,11 @@ class _ConvADNFn(torch.autograd.Function):
     """y = prelu(instance_norm(conv(x))) (+ res): MONAI Convolution "NDA" (+ the ResidualUnit's sum)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, a, route, eps, res):
+    def forward(ctx, x, w, b, a, route, eps, res, res_is_x):
         z = route.forward(x.contiguous(), w, b)
         y, mean, rstd = adn_forward(z, a, eps, res=res)
         ctx.save_for_backward(x, w, a, z, mean, rstd)
-        ctx.route, ctx.has_b, ctx.has_res = route, b is not None, res is not None
+        ctx.route, ctx.has_b, ctx.has_res, ctx.res_is_x = route, b is not None, res is not None, res_is_x
         return y
 
     @staticmethod
@@ -69,9 +69,34 @@ class _ConvADNFn(torch.autograd.Function):
         n = ctx.needs_input_grad
         g = g.contiguous()
         dz, da, db = adn_backward(z, g, mean, rstd, a, need_w=n[3], need_bias=ctx.has_b and n[2])
-        gx = ctx.route.input_grad(dz, x, w) if n[0] else None
         gw = ctx.route.weight_grad(dz, x, w) if n[1] else None
-        return gx, gw, db, da, None, None, (g if ctx.has_res and n[6] else None)
+        if ctx.res_is_x:  # identity residual: dX = dconv(dZ) + dY in the input-gradient kernel's store
+            gx = ctx.route.input_grad(dz, x, w, add=g) if n[0] else None
+            return gx, gw, db, da, None, None, None, None
+        gx = ctx.route.input_grad(dz, x, w) if n[0] else None
+        return gx, gw, db, da, None, None, (g if ctx.has_res and n[6] else None), None
+
+
+class _ConvResFn(torch.autograd.Function):
+    """y = conv(x) + x: the identity-residual unit with a bare conv (the top ResidualUnit(3, 3, conv_only))."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, route):
+        x = x.contiguous()
+        y = route.forward(x, w, b, add=x)
+        ctx.save_for_backward(x, w)
+        ctx.route, ctx.has_b = route, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        n = ctx.needs_input_grad
+        g = g.contiguous()
+        gx = ctx.route.input_grad(g, x, w, add=g) if n[0] else None
+        gw = ctx.route.weight_grad(g, x, w) if n[1] else None
+        gb = _conv.channel_sum(g) if ctx.has_b and n[2] else None
+        return gx, gw, gb, None
 
 
 class _StackedUnitFn(torch.autograd.Function):
@@ -149,7 +174,7 @@ class Convolution(nn.Sequential):
         if adn is None or not _fusable(x, self.conv, adn):
             return None
         return _ConvADNFn.apply(x, self.conv.weight, self.conv.bias, adn.A.weight, _conv.route_of(self.conv, x),
-                                adn.N.eps, res)
+                                adn.N.eps, res, res is x)
 
     def forward(self, x):
         y = self.fused(x)
@@ -189,6 +214,10 @@ class ResidualUnit(nn.Module):
             y = units[0].fused(x, res=x)
             if y is not None:
                 return y
+        if isinstance(self.residual, nn.Identity) and len(units) == 1 and not hasattr(units[0], "adn") and \
+                _fusable(x, units[0].conv, None):
+            c = units[0].conv
+            return _ConvResFn.apply(x, c.weight, c.bias, _conv.route_of(c, x))
         res = self.residual(x)
         return self.conv(x) + res
 

@@ -145,3 +145,28 @@ def test_unsupported_channels_raise(conv):
     w = torch.randn((16, 4, 3, 3, 3), device="cuda")
     with pytest.raises(TexbiasError):
         conv.conv_gemm(x, w, None, "conv", 1, 3)
+
+
+@pytest.mark.parametrize("kind,c,sp", [("small", 3, (12, 10, 20)), ("fwd16", 16, (6, 5, 32)), ("mfma", 32, (6, 7, 8)),
+                                       ("mfma", 64, (4, 5, 12)), ("gemm", 128, (3, 5, 4))])
+def test_residual_add_epilogues(conv, kind, c, sp):
+    """The identity-residual unit's sums in the conv kernels' stores: forward conv(x) + x and input
+    gradient dconv(dY) + dY (tb_conv3d_{small,fwd16,mfma}_add_f32, the GEMM's ``add``)."""
+    torch.manual_seed(6)
+    x = torch.randn((2, c) + sp, device="cuda")
+    w = torch.randn((c, c, 3, 3, 3), device="cuda") * (1.0 / (27 * c) ** 0.5)
+    b = torch.randn(c, device="cuda")
+    m = conv.Conv3d(c, c, 3, padding=1).cuda()
+    with torch.no_grad():
+        m.weight.copy_(w)
+        m.bias.copy_(b)
+    r = conv.route_of(m, x)
+    assert r.kind == kind, r.kind
+    y = r.forward(x, w, b, add=x)
+    yr = F.conv3d(x, w, b, padding=1) + x
+    assert (y - yr).abs().max().item() <= 2e-5 * yr.abs().max().item()
+    g = torch.randn_like(y)
+    gx = r.input_grad(g, x, w, add=g)
+    gxr = torch.ops.aten.convolution_backward(g, x, w, None, [1] * 3, [1] * 3, [1] * 3, False, [0] * 3, 1,
+                                              [True, False, False])[0] + g
+    assert (gx - gxr).abs().max().item() <= 2e-5 * gxr.abs().max().item()
