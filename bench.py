@@ -84,6 +84,11 @@ def parse():
                     help="volumes per process in the CPU baseline's multi-process modes (c3: 1, c2: 8)")
     ap.add_argument("--cpu-cores", type=int, default=None, help="CPU baseline core count (default: the job's share)")
     ap.add_argument("--filter-only", action="store_true", help="diagnostic: time the filter chain alone")
+    ap.add_argument("--graph", action="store_true",
+                    help="c3, one GPU: replay the train step as a captured HIP graph (TrainStep(capturable=True)); "
+                         "unet: the filter chain still runs eagerly every step (fresh host draws) and writes the "
+                         "graph's static input; gibbs-layer: the whole step incl. Gibbs_GD is one graph (the "
+                         "layer reads its alpha from device memory)")
     a = ap.parse_args()
     c2, c5 = a.config == "c2", a.config == "c5"
     layer = a.model != "unet"
@@ -103,6 +108,9 @@ def parse():
     a.cpu_sample_vols = a.cpu_sample_vols or (8 if c2 else 1)
     if c2:
         a.filter_only = True  # config 2 is the filter kernel alone
+    if a.graph and (a.config != "c3" or a.filter_only or a.model == "spike-layer" or a.gpus != 1):
+        ap.error("--graph: c3 train step on one GPU, --model unet or gibbs-layer (spike_gd reads its slope "
+                 "on the host every step)")
     return a
 
 
@@ -242,7 +250,7 @@ def main():
         else:
             lm = SL.Spikes_UNet(11.0)
         torch.manual_seed(1000 + rank)
-        step_fn = TrainStep(lm, dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb)
+        step_fn = TrainStep(lm, dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb, capturable=args.graph)
         gd = gibbs_gd if args.model == "gibbs-layer" else spike_gd
         train_step = step_fn
 
@@ -253,7 +261,7 @@ def main():
     elif not args.filter_only:
         torch.backends.cudnn.benchmark = not args.no_cudnn_benchmark
         step_fn = TrainStep(reference_model(C, 3), dev, distributed=world > 1, bucket_cap_mb=args.bucket_mb,
-                            channels_last=args.channels_last)
+                            channels_last=args.channels_last, capturable=args.graph)
 
     def one_step(i):
         if args.random_filters:
@@ -267,12 +275,49 @@ def main():
             return step_fn(y, labels[i % 2])
         return y
 
-    for i in range(args.warmup):
-        t_w = time.perf_counter()
-        one_step(i)
+    graphs = None
+    if args.graph:
+        # static input of the U-Net step: the eager chain writes it every step (fresh draws)
+        xs = None if layer_model else torch.zeros((B, C, H, W, D + pad), device=dev)
+
+        def body(i):  # the captured part: everything but the filter chain's host draws
+            return step_fn(pool[i % 2] if layer_model else xs, labels[i % 2])
+
+        def fill(i):
+            if args.random_filters:
+                randomize_filters()
+            if not layer_model:
+                chain(pool[i % 2], pad=pad, out=xs)
+
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm up off the capture stream: plans, workspaces, solver choice, optimizer state
+            for i in range(max(args.warmup, 2)):
+                t_w = time.perf_counter()
+                fill(i)
+                body(i)
+                torch.cuda.synchronize(dev)
+                if rank == 0:
+                    print(f"[bench] warmup step {i}: {time.perf_counter() - t_w:.3f} s", file=sys.stderr, flush=True)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graphs = []
+        for k in range(2):  # one graph per resident batch; one memory pool, replayed in capture order
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=graphs[0].pool() if graphs else None):
+                body(k)
+            graphs.append(g)
         torch.cuda.synchronize(dev)
-        if rank == 0:
-            print(f"[bench] warmup step {i}: {time.perf_counter() - t_w:.3f} s", file=sys.stderr, flush=True)
+
+        def one_step(i):  # noqa: F811
+            fill(i)
+            graphs[i % 2].replay()
+    else:
+        for i in range(args.warmup):
+            t_w = time.perf_counter()
+            one_step(i)
+            torch.cuda.synchronize(dev)
+            if rank == 0:
+                print(f"[bench] warmup step {i}: {time.perf_counter() - t_w:.3f} s", file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -289,6 +334,16 @@ def main():
     elapsed = time.perf_counter() - t0
     ms, cnt, nbytes, kernels = rt.pass_stats()
     rt.set_pass_timing(False)
+    stat_steps = args.steps
+    if graphs is not None and not any(cnt[:3]):
+        # the filter launches sit inside the graph: time them on eager steps after the timed region
+        stat_steps = min(args.steps, 5)
+        rt.set_pass_timing(True)
+        for i in range(stat_steps):
+            body(i)
+        torch.cuda.synchronize(dev)
+        ms, cnt, nbytes, kernels = rt.pass_stats()
+        rt.set_pass_timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -317,13 +372,15 @@ def main():
                 "(2 no-grad forwards) per step (350_stylized_layers/gibbs0p7_layer_domain_GD.py:252-301)"
                 if args.model == "gibbs-layer" else
                 "Spikes_UNet(1->1, I=11), train step + intensity finite-difference step (2 no-grad forwards) "
-                "(350_stylized_layers/spikes11_layer_domain_GD.py:260-300)")
+                "(350_stylized_layers/spikes11_layer_domain_GD.py:260-300)") + (
+                " [whole step replayed as a HIP graph]" if args.graph else "")
         elif args.config == "c3":
             workload = ("C3 full filter chain (disk 12.5 -> plane wave (55,55,30) I=15 -> wrap 0.5 -> S&P 0.05) "
                         "+ 3D U-Net(4->3, 16..256, 2 res units) fwd/bwd/Adam(amsgrad), DiceLoss"
                         + (" [random per-batch filter params, config 4]" if args.random_filters else "")
                         + (f" [CHAIN {args.chain}: see bench.py --help]" if args.chain != "ref" else "")
-                        + (" [FILTER ONLY diagnostic]" if args.filter_only else ""))
+                        + (" [FILTER ONLY diagnostic]" if args.filter_only else "")
+                        + (" [train step replayed as a HIP graph]" if args.graph else ""))
         else:
             workload = "C2 Gibbs truncation: RandFourierDiskMaskd(r=12.5) low-pass alone, batched 4x128^3 volumes"
         traffic, traffic_file = pmc_traffic(passes[dom]["kernel"], dom_bytes,
@@ -355,7 +412,7 @@ def main():
                          "traffic_unit": f"bytes per launch (rocprofv3 PMC, {traffic_file})",
                          "algorithmic_bytes_per_launch": dom_bytes},
             "filter_passes": passes,
-            "filter_ms_per_step": round(sum(ms) / args.steps, 4),
+            "filter_ms_per_step": round(sum(ms) / stat_steps, 4),
         }
         if args.config == "c5":
             from texbias.dcgan import step_flops

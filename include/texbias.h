@@ -424,6 +424,15 @@ int tb_set_point_plans(int enable);
 int tb_set_wrap_plans(int enable);
 
 /*
+ * Full-spectrum route (Fourier.shift_fourier / inv_shift_fourier, filters_and_operators.py:594-632)
+ * on shapes with a half-unit plan (240 x 240 x 155): passes A and C run per (slab, row parity) --
+ * the W transform split at its last radix-2 step, two workgroups per CU -- and pass B finishes the
+ * W transform with the butterfly (split spectrum in the workspace).  Same results to rounding.
+ * Default on; TEXBIAS_HALF=0 in the environment or tb_set_half_units(0): whole-slab passes.
+ */
+int tb_set_half_units(int enable);
+
+/*
  * Pass C' of the band-limited plans synthesises the image on the f16 matrix cores in split
  * precision (table and V each as an f16 hi/lo pair, three products, f32 accumulation; agrees with
  * the f32 synthesis to a few 1e-7 of max |y|) whenever the launch's band columns plus all of its

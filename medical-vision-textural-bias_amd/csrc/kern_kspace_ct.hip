@@ -143,6 +143,57 @@ __global__ __launch_bounds__(NT) void k_kspace_ct2p(KspaceArgs) {
   }
 }
 
+// Persistent pass B over a split spectrum (kspace_ct.h b_mid_split): unit (bc, 16 first-half columns)
+// with their 16 partner columns W/2 spectrum rows later, one 32-column tile; the next unit's loads are
+// in flight during the middle and inverse phases (as k_kspace_ct2p).
+template <int H, int W, int D, int NT, int K>
+__global__ __launch_bounds__(NT) void k_kspace_half(KspaceArgs) {
+  using HP = ct::HalfPlan<W, D>;
+  using P = ct::TilePlan<H, 32>;
+  constexpr int TH = 16;
+  static_assert(P::N0 / 2 <= NT && (P::Q0 * TH) % NT == 0 && NT % TH == 0, "split tile items");
+  static_assert((HP::W2 * HP::Dh) % TH == 0, "whole split tiles");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const KspaceArgs& a = kargs<KspaceArgs>();
+  const int tid = (int)threadIdx.x;
+  constexpr int ncols = W * HP::Dh, nh = HP::W2 * HP::Dh, ntile = nh / TH;
+  const int units = ntile * a.nbc;
+  const bool ld = tid < P::N0 / 2;
+  for (int i = tid; i < H; i += NT) lds[P::OFF_TW + i] = ct::V(a.pl.tw[0][i].x, a.pl.tw[0][i].y);
+  auto base = [&](int u, int& bcl) {
+    bcl = u / ntile;
+    return reinterpret_cast<v2*>(a.S) + (int64_t)(a.bc0 + bcl) * H * ncols + (u - bcl * ntile) * TH;
+  };
+  ct::f4 r[P::Q0];
+  int u = (int)blockIdx.x;
+  if (u < units && ld) {
+    int bcl;
+    ct::b_load_split<P>(r, base(u, bcl), ncols, nh, tid);
+  }
+  for (; u < units; u += (int)gridDim.x) {
+    int bcl;
+    v2* Sc = base(u, bcl);
+    FreqCol f0, f1;
+    ct::tile_col_half<HP>((u - bcl * ntile) * TH + tid % TH, f0, f1);
+    __syncthreads();  // the previous unit's inverse-stage reads of the tile are done (and the twiddles are in)
+    if (ld) ct::b_s0_pair_regs<P>(lds, r, tid);
+    {
+      const int un = u + (int)gridDim.x < units ? u + (int)gridDim.x : u;
+      int bn;
+      const v2* Sn = base(un, bn);
+      if (ld) ct::b_load_split<P>(r, Sn, ncols, nh, tid);
+    }
+    __syncthreads();
+    const int sl = a.cofs + bcl;
+#pragma unroll 1
+    for (int s = 0; s < P::Q0 * TH / NT; ++s)
+      ct::b_mid_split<P, K>(lds, a.ops.s[sl / a.C], sl % a.C, f0, f1, tid + s * NT);
+    __syncthreads();
+    if (ld) ct::b_s1_split<P>(lds, Sc, ncols, nh, tid);
+  }
+}
+
 }  // namespace
 
 #ifdef TB_SLAB_PROF
@@ -268,6 +319,36 @@ hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t
     return hipGetLastError();                                                           \
   }
   TB_CT_TILE_H(TB_X)
+#undef TB_X
+  return hipErrorInvalidValue;
+}
+
+bool kspace_half_supported(int H, int W, int D) {
+  if (H != 240) return false;
+#define TB_X(w, d) if (W == w && D == d) return true;
+  TB_CT_HALF_SHAPES(TB_X)
+#undef TB_X
+  return false;
+}
+
+hipError_t launch_kspace_half(const KspaceArgs& a, int ncu, hipStream_t st) {
+  const int mk = launch_mask_kind(a);
+#define TB_X(w, d)                                                                                   \
+  if (a.pl.H == 240 && a.pl.W == w && a.pl.D == d) {                                                 \
+    constexpr size_t lds = ct::TilePlan<240, 32>::LDS_BYTES;                                         \
+    auto kern = mk == ct::MASK_GIBBS ? k_kspace_half<240, w, d, 256, ct::MASK_GIBBS>                 \
+              : mk == ct::MASK_LAYER ? k_kspace_half<240, w, d, 256, ct::MASK_LAYER>                 \
+              : mk == ct::MASK_DISK  ? k_kspace_half<240, w, d, 256, ct::MASK_DISK>                  \
+                                     : k_kspace_half<240, w, d, 256, ct::MASK_GENERIC>;              \
+    hipError_t e = allow_lds(kern, lds);                                                             \
+    if (e != hipSuccess) return e;                                                                   \
+    const int units = (w / 2) * (d / 2 + 1) / 16 * a.nbc;                                           \
+    int g = ncu * kspace_occupancy(kern, 256, lds);                                                  \
+    g = g < units ? g : units;                                                                       \
+    hipLaunchKernelGGL(kern, dim3(g), dim3(256), lds, st, a);                                        \
+    return hipGetLastError();                                                                        \
+  }
+  TB_CT_HALF_SHAPES(TB_X)
 #undef TB_X
   return hipErrorInvalidValue;
 }

@@ -283,6 +283,169 @@ __global__ __launch_bounds__(NT) void k_slab_inv_ct(SlabInvArgs) {
   }
 }
 
+// ---------------------------------------------------------------- half units (slab_ct.h HalfPlan)
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// block -> (slab, parity): blocks b and b + 8 hold the two halves of one slab -- the same XCD (blocks
+// go to the XCDs round robin) at nearly the same time, so the 128-B lines their row ends share are
+// fetched (pass A) or merged (pass C) once in that XCD's L2
+__device__ __forceinline__ void half_unit(int b, int& slab, int& e) {
+  slab = (b >> 4) * 8 + (b & 7);
+  e = (b >> 3) & 1;
+}
+static int half_grid(int units) { return 16 * ((units + 7) / 8); }
+
+// Pass A of one half unit: rows 2 w'' + e staged raw[w''][d] by 4-B global->LDS DMA (no registers:
+// the other workgroup on the CU computes while these land), then F0 / D1+U (or fused DU) / W0 / W1
+// with the SlabPlan<W/2, D> items, W1 storing the unit's split rows (e = 1 scaled by w^k'').
+template <int W, int D, int NT, bool FUSE>
+__global__ __launch_bounds__(NT) void k_slab_fwd_half(SlabFwdArgs) {
+  using HP = ct::HalfPlan<W, D>;
+  using P = typename HP::P;
+  constexpr int SF = ct::Slots<P::N_F0, NT>::value;
+  constexpr int SU = ct::Slots<P::N_U, NT>::value;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  float* raw = reinterpret_cast<float*>(smem);
+  const SlabFwdArgs& a = kargs<SlabFwdArgs>();
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.pl.H, units = H * a.nbc;
+  int slab, e;
+  half_unit((int)blockIdx.x, slab, e);
+  if (slab >= units) return;
+  const int bcl = slab / H, h = slab - bcl * H;
+  const float* xb = a.x + (int64_t)(a.bc0 + bcl) * a.sbc + (int64_t)h * a.sh + (int64_t)e * a.sw;
+  const int64_t sw2 = 2 * a.sw;
+  {
+    constexpr int NCH = (HP::NRAW + 63) / 64;
+    for (int c = wave; c < NCH; c += NT / 64) {
+      const int L = c * 64 + lane;
+      if (L < HP::NRAW) {
+        const int w2 = L / D, d = L - w2 * D;
+        __builtin_amdgcn_global_load_lds((gptr_t)(xb + w2 * sw2 + d), (lptr_t)(raw + c * 64), 4, 0, 0);
+      }
+    }
+  }
+  DevCtx ctx{tid, NT};
+  ct::load_tw_half<HP>(ctx, lds, a.pl);
+  __syncthreads();  // vmcnt(0): the staged rows have landed
+  {
+    v2 rf[SF][P::R0];
+#pragma unroll
+    for (int s = 0; s < SF; ++s)
+      if (tid + s * NT < P::N_F0) ct::a_load_raw<P>(raw, rf[s], tid + s * NT);
+    __syncthreads();  // raw is the bytes of Z
+#pragma unroll
+    for (int s = 0; s < SF; ++s)
+      if (tid + s * NT < P::N_F0) ct::a_f0<P>(lds, rf[s], tid + s * NT);
+  }
+  __syncthreads();
+  if constexpr (FUSE && P::FUSED_DU) {
+    constexpr int SD = ct::Slots<P::N_DU, NT>::value;
+    v2 rd[SD][2 * P::R1];
+#pragma unroll
+    for (int s = 0; s < SD; ++s)
+      if (tid + s * NT < P::N_DU) ct::a_du_load<P>(lds, rd[s], tid + s * NT);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SD; ++s)
+      if (tid + s * NT < P::N_DU) ct::a_du_compute<P>(lds, rd[s], tid + s * NT);
+  } else {
+    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::a_d1<P>(lds, it);
+    __syncthreads();
+    v2 ru[SU][2];
+#pragma unroll
+    for (int s = 0; s < SU; ++s)
+      if (tid + s * NT < P::N_U) ct::a_u_read<P>(lds, ru[s], tid + s * NT);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SU; ++s)
+      if (tid + s * NT < P::N_U) ct::a_u_write<P>(lds, ru[s], tid + s * NT);
+  }
+  __syncthreads();
+  _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::a_w0<P>(lds, it);
+  __syncthreads();
+  v2* Sb = reinterpret_cast<v2*>(a.S) + ((int64_t)(a.bc0 + bcl) * H + h) * (int64_t)(W * P::Dh) +
+           (int64_t)e * HP::W2 * P::Dh;
+  _Pragma("unroll 1") for (int it = tid; it < P::N_W1; it += NT) ct::a_w1_half<HP>(lds, Sb, e, it);
+}
+
+// Pass C of one half unit: the unit's split rows (e = 1 scaled by w^-k'') -> inverse W/2-point DFT ->
+// C2R along D -> rows 2 w'' + e of the image, zero padding, min/max
+template <int W, int D, int NT, bool FUSE>
+__global__ __launch_bounds__(NT) void k_slab_inv_half(SlabInvArgs) {
+  using HP = ct::HalfPlan<W, D>;
+  using P = typename HP::P;
+  constexpr int SG = ct::Slots<P::N_W1, NT>::value;
+  constexpr int SU = ct::Slots<P::N_U, NT>::value;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[2 * NT / 64];
+  v2* lds = reinterpret_cast<v2*>(smem);
+  const SlabInvArgs& a = kargs<SlabInvArgs>();
+  const int tid = (int)threadIdx.x;
+  const int H = a.pl.H, units = H * a.nbc;
+  int slab, e;
+  half_unit((int)blockIdx.x, slab, e);
+  if (slab >= units) return;
+  const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
+  const v2* Sb = reinterpret_cast<const v2*>(a.S) + ((int64_t)bc * H + h) * (int64_t)(W * P::Dh) +
+                 (int64_t)e * HP::W2 * P::Dh;
+  {
+    v2 rg[SG][P::Q1];
+#pragma unroll
+    for (int s = 0; s < SG; ++s)
+      if (tid + s * NT < P::N_W1) ct::c_load_half<HP>(rg[s], Sb, tid + s * NT);
+    DevCtx ctx{tid, NT};
+    ct::load_tw_half<HP>(ctx, lds, a.pl);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SG; ++s)
+      if (tid + s * NT < P::N_W1) {
+        ct::c_twiddle_half<HP>(lds, rg[s], e, tid + s * NT);
+        ct::c_g0<P>(lds, rg[s], tid + s * NT);
+      }
+  }
+  __syncthreads();
+  _Pragma("unroll 1") for (int it = tid; it < P::N_W0; it += NT) ct::c_g1<P>(lds, it);
+  __syncthreads();
+  if constexpr (FUSE && P::FUSED_DU) {
+    constexpr int SD = ct::Slots<P::N_DU, NT>::value;
+    v2 rd[SD][2 * P::R1];
+#pragma unroll
+    for (int s = 0; s < SD; ++s)
+      if (tid + s * NT < P::N_DU) ct::c_re_load<P>(lds, rd[s], tid + s * NT);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SD; ++s)
+      if (tid + s * NT < P::N_DU) ct::c_re_compute<P>(lds, rd[s], tid + s * NT);
+  } else {
+    v2 ru[SU][2];
+#pragma unroll
+    for (int s = 0; s < SU; ++s)
+      if (tid + s * NT < P::N_U) ct::c_r_read<P>(lds, ru[s], tid + s * NT);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SU; ++s)
+      if (tid + s * NT < P::N_U) ct::c_r_write<P>(lds, ru[s], tid + s * NT);
+    __syncthreads();
+    _Pragma("unroll 1") for (int it = tid; it < P::N_D1; it += NT) ct::c_e1<P>(lds, it);
+  }
+  __syncthreads();
+  float lo = 3.402823466e38f, hi = -3.402823466e38f;
+  float* yb = a.y + (int64_t)bc * a.sbc + (int64_t)h * a.sh + (int64_t)e * a.sw;
+  const int64_t sw2 = 2 * a.sw;
+  _Pragma("unroll 1") for (int it = tid; it < P::N_F0; it += NT) ct::c_e0<P>(lds, yb, sw2, a.scale, it, lo, hi);
+  if (a.ypad > 0) {
+    const FastDiv fp = FastDiv::make(a.ypad);
+    for (int t = tid; t < HP::W2 * a.ypad; t += NT) {
+      const int w = fp.div(t);
+      yb[(int64_t)w * sw2 + D + (t - w * a.ypad)] = 0.f;
+    }
+  }
+  if (a.mm) block_minmax_atomic<NT>(lo, hi, red, a.mm + 2 * (bc / a.C));
+}
+
 int slab_grid(int units, size_t lds, int ncu) {
   int per_cu = (int)(163840 / (lds ? lds : 1));
   per_cu = per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu);
@@ -384,6 +547,60 @@ hipError_t launch_slab_inv_ct(const SlabInvArgs& a, int ncu, hipStream_t st) {
     return launch_ct(k_slab_inv_ct<w, d, 768, false>, 768, lds, units, ncu, a, st);                 \
   }
   TB_CT_SLAB_SHAPES(TB_X)
+#undef TB_X
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------- half units
+bool slab_half_supported(int W, int D) {
+#define TB_X(w, d) if (W == w && D == d) return true;
+  TB_CT_HALF_SHAPES(TB_X)
+#undef TB_X
+  return false;
+}
+
+// TEXBIAS_HALF_CFG (tuning): 0 = 256 threads with the fused DU / RE phase (default), 1 = 256 threads
+// unfused, 2 = 512 threads unfused
+static int half_cfg() {
+  static const int c = [] {
+    const char* e = std::getenv("TEXBIAS_HALF_CFG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return c;
+}
+
+template <class K, class A>
+static hipError_t launch_half(K kern, int nt, size_t lds, int units, const A& a, hipStream_t st) {
+  hipError_t e = allow_lds(kern, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(half_grid(units)), dim3(nt), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_slab_fwd_half(const SlabFwdArgs& a, hipStream_t st) {
+  const int units = a.pl.H * a.nbc;
+#define TB_X(w, d)                                                                                   \
+  if (a.pl.W == w && a.pl.D == d) {                                                                  \
+    constexpr size_t lds = ct::HalfPlan<w, d>::LDS_BYTES;                                            \
+    if (half_cfg() == 2) return launch_half(k_slab_fwd_half<w, d, 512, false>, 512, lds, units, a, st); \
+    if (half_cfg() == 1) return launch_half(k_slab_fwd_half<w, d, 256, false>, 256, lds, units, a, st); \
+    return launch_half(k_slab_fwd_half<w, d, 256, true>, 256, lds, units, a, st);                    \
+  }
+  TB_CT_HALF_SHAPES(TB_X)
+#undef TB_X
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_slab_inv_half(const SlabInvArgs& a, hipStream_t st) {
+  const int units = a.pl.H * a.nbc;
+#define TB_X(w, d)                                                                                   \
+  if (a.pl.W == w && a.pl.D == d) {                                                                  \
+    constexpr size_t lds = ct::HalfPlan<w, d>::LDS_BYTES;                                            \
+    if (half_cfg() == 2) return launch_half(k_slab_inv_half<w, d, 512, false>, 512, lds, units, a, st); \
+    if (half_cfg() == 1) return launch_half(k_slab_inv_half<w, d, 256, false>, 256, lds, units, a, st); \
+    return launch_half(k_slab_inv_half<w, d, 256, true>, 256, lds, units, a, st);                    \
+  }
+  TB_CT_HALF_SHAPES(TB_X)
 #undef TB_X
   return hipErrorInvalidValue;
 }

@@ -77,6 +77,13 @@ bool kspace_ct_supported(int H);
 int kspace_ct_tile(int ncols);
 hipError_t launch_kspace_ct(const KspaceArgs& a, dim3 grid, int ncu, hipStream_t st);
 bool kspace_ct_persistent(int ncols);  // launch_kspace_ct runs the persistent k_kspace_ct2p
+// Half units and split spectra (slab_ct.h HalfPlan): passes A / C per (slab, row parity), two
+// workgroups per CU; pass B finishes the W transform (kspace_ct.h b_mid_split).
+bool slab_half_supported(int W, int D);
+hipError_t launch_slab_fwd_half(const SlabFwdArgs& a, hipStream_t st);
+hipError_t launch_slab_inv_half(const SlabInvArgs& a, hipStream_t st);
+bool kspace_half_supported(int H, int W, int D);
+hipError_t launch_kspace_half(const KspaceArgs& a, int ncu, hipStream_t st);
 
 // Direct-DFT fallback (kern_generic.hip) for sizes the mixed-radix passes do not take: full complex
 // spectrum in two ping-pong buffers S[2][nbc][H][W][D] (gen_workspace_bytes).

@@ -352,6 +352,149 @@ TB_HD FreqCol tile_col(const tb_plan_dev& pl, int col) {
   return freq_col(pl.irev_w[wp], col - wp * Dh, pl.W, pl.D);
 }
 
+// ------------------------------------------------------------------ split spectra (slab_ct.h HalfPlan)
+// Pass B over a split spectrum: a unit is TH = T/2 first-half columns (rows w' < W/2 of the slab's
+// half spectrum: E0(k'')) and their partners W/2 rows later (T1(k'')), tile columns c and c + TH.
+// The middle item (blk, c < TH) forms X(k'') = E0 + T1 and X(k'' + W/2) = E0 - T1 (the last W
+// butterfly, which commutes with the H stages), runs both through the last H stage, the op program
+// and the first inverse H stage, and stores X'(k'') + X'(k'' + W/2), X'(k'') - X'(k'' + W/2): the
+// inputs of pass C's two half units (no 1/2 -- their W/2-point inverses complete the W-point one).
+template <class HP>
+TB_HD void tile_col_half(int col, FreqCol& f0, FreqCol& f1) {
+  const int wp = col / HP::Dh, kd = col - wp * HP::Dh;
+  const int k = HP::freq(wp);
+  f0 = freq_col(k, kd, HP::W, HP::D);
+  f1 = freq_col(k + HP::W2, kd, HP::W, HP::D);
+}
+
+// mask-only programs (kind K) on the Q1 coefficients of butterfly blk, in registers (b_mid_mask)
+template <class P, int K, class SO>
+TB_HD void mask_bfly(const SO& so, int chan, const FreqCol& fc, int blk, v2* a) {
+  int g0[P::Q1], g1[P::Q1];
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) {  // slot blk*L + q holds kh = blk + Q0*q
+    const AxisGeo h = axis_geo(blk + P::Q0 * q, P::H);
+    g0[q] = K == MASK_DISK ? h.dsq + fc.dsq : h.ef + fc.ef;
+    g1[q] = h.en + fc.en;
+  }
+  for (int o = 0; o < so.n; ++o) {
+    const tb_op& op = so.op[o];
+    if (op.chan >= 0 && op.chan != chan) continue;
+    if constexpr (K == MASK_GIBBS) {
+      TB_UNROLL
+      for (int q = 0; q < P::Q1; ++q) {
+        const float m = 0.5f * (((int64_t)g0[q] <= op.l ? 1.f : 0.f) + ((int64_t)g1[q] <= op.l ? 1.f : 0.f));
+        a[q] = m * a[q];
+      }
+    } else if constexpr (K == MASK_LAYER) {
+      TB_UNROLL
+      for (int q = 0; q < P::Q1; ++q) {
+        const float m = 0.5f * ((layer_in(op, g0[q]) ? 1.f : 0.f) + (layer_in(op, g1[q]) ? 1.f : 0.f));
+        a[q] = m * a[q];
+      }
+    } else {
+      const bool ir = op.i[0] != 0, off = op.i[1] != 0;
+      TB_UNROLL
+      for (int q = 0; q < P::Q1; ++q) {
+        bool in = ir ? ((int64_t)g0[q] < op.l) : ((float)g0[q] < op.f[0]);
+        if (off) in = !in;
+        a[q] = in ? a[q] : V(0.f, 0.f);
+      }
+    }
+  }
+}
+
+// middle item of a split tile; K = MASK_GENERIC applies the op program per coefficient from LDS
+template <class P, int K, class SO>
+TB_HD void b_mid_split(v2* lds, const SO& so, int chan, const FreqCol& f0, const FreqCol& f1, int it) {
+  constexpr int TH = P::T / 2;
+  const int blk = it / TH, c = it - blk * TH;
+  v2* t0 = lds + (blk * P::L) * P::T + c;
+  v2* t1 = t0 + TH;
+  v2 a[P::Q1], b[P::Q1];
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) {
+    const v2 u = t0[q * P::T], v = t1[q * P::T];
+    a[q] = u + v;
+    b[q] = u - v;
+  }
+  Dv<P::Q1, true>::run(a);
+  Dv<P::Q1, true>::run(b);
+  if constexpr (K != MASK_GENERIC) {
+    mask_bfly<P, K>(so, chan, f0, blk, a);
+    mask_bfly<P, K>(so, chan, f1, blk, b);
+  } else {
+    TB_UNROLL
+    for (int q = 0; q < P::Q1; ++q) {
+      t0[q * P::T] = a[q];
+      t1[q * P::T] = b[q];
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+    for (int q = 0; q < P::Q1; ++q) {
+      const int kh = blk + P::Q0 * q;
+      const v2 u = t0[q * P::T], v = t1[q * P::T];
+      const cf ou = apply_ops(so, chan, mk(u.x, u.y), f0, kh, P::H);
+      const cf ov = apply_ops(so, chan, mk(v.x, v.y), f1, kh, P::H);
+      t0[q * P::T] = V(ou.x, ou.y);
+      t1[q * P::T] = V(ov.x, ov.y);
+    }
+    TB_UNROLL
+    for (int q = 0; q < P::Q1; ++q) {
+      a[q] = t0[q * P::T];
+      b[q] = t1[q * P::T];
+    }
+  }
+  Dv<P::Q1, false>::run(a);
+  Dv<P::Q1, false>::run(b);
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) {
+    t0[q * P::T] = a[q] + b[q];
+    t1[q * P::T] = a[q] - b[q];
+  }
+}
+
+// stage-0 loads / stores of a split tile: column pair c of row j; columns c < TH from the first
+// half (Sc + c), the others from the partner columns (Sc + nh + c - TH)
+template <class P>
+TB_HD int64_t split_col(int64_t nh, int c) {
+  constexpr int TH = P::T / 2;
+  return c < TH ? (int64_t)c : nh + (c - TH);
+}
+template <class P>
+TB_HD void b_load_split(f4* r, const v2* __restrict__ Sc, int64_t ncols, int64_t nh, int it) {
+  const int j = it / (P::T / 2), c = 2 * (it - j * (P::T / 2));
+  const f4* s = reinterpret_cast<const f4*>(Sc + (int64_t)j * ncols + split_col<P>(nh, c));
+  const int64_t st = (int64_t)P::L * (ncols / 2);
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) r[q] = ld_stream<TB_NT_SPEC>(s + q * st);
+}
+template <class P>
+TB_HD void b_s1_split(const v2* lds, v2* __restrict__ Sc, int64_t ncols, int64_t nh, int it) {
+  const int j = it / (P::T / 2), c = 2 * (it - j * (P::T / 2));
+  const v2* tw = lds + P::OFF_TW;
+  const f4* t = reinterpret_cast<const f4*>(lds + j * P::T + c);
+  v2 a[P::Q0], b[P::Q0];
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) {
+    const f4 u = t[q * P::L * P::T / 2];
+    a[q] = V(u.x, u.y);
+    b[q] = V(u.z, u.w);
+    if (q && j) {
+      const v2 w = tw[j * q];
+      a[q] = cmulc(a[q], w);
+      b[q] = cmulc(b[q], w);
+    }
+  }
+  Dv<P::Q0, false>::run(a);
+  Dv<P::Q0, false>::run(b);
+  f4* s = reinterpret_cast<f4*>(Sc + (int64_t)j * ncols + split_col<P>(nh, c));
+  const int64_t st = (int64_t)P::L * (ncols / 2);
+  TB_UNROLL
+  for (int q = 0; q < P::Q0; ++q) s[q * st] = f4{a[q].x, a[q].y, b[q].x, b[q].y};
+}
+
 // H extents with a compile-time pass-B plan in the device library (tile width T = 16 columns)
 #define TB_CT_TILE_H(X) X(240) X(128)
 constexpr int kCtTileT = 16;

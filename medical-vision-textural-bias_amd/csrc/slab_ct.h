@@ -513,8 +513,80 @@ TB_HD void load_tw(Ctx& ctx, v2* lds, const tb_plan_dev& pl) {
   for (int i = ctx.tid; i < P::D; i += ctx.nthreads) lds[P::OFF_TWD + i] = V(pl.tw[2][i].x, pl.tw[2][i].y);
 }
 
+// ------------------------------------------------------------------ half slabs (W split by parity)
+// A (bc, h) slab's W transform split at its last radix-2 step (decimation in time): unit (slab, e)
+// transforms rows w = 2 w'' + e (w'' < W/2) with the SlabPlan<W/2, D> item functions -- R2C along D,
+// the W/2-point DFT along w'' -- and for e = 1 scales the result by w^k'' (w = e^{-2 pi i / W}).  The
+// half spectrum is then stored "split": row w' = e W/2 + slot(k'') of the slab holds E0(k'') (e = 0)
+// or w^k'' E1(k'') (e = 1), and pass B finishes the W transform with the butterfly
+// X(k'') = E0 + T1, X(k'' + W/2) = E0 - T1 (and stores X' (k'') +- X' (k'' + W/2) back).  Pass C
+// inverts: unit (slab, e) reads its rows, scales e = 1 by w^-k'', runs the inverse W/2-point DFT and
+// the C2R D transform, and writes rows 2 w'' + e.  Each unit needs half the LDS of a slab, so two
+// workgroups share a CU and one's HBM traffic overlaps the other's butterflies (a whole slab fills a
+// CU's LDS: its loads and stores stall the CU's only workgroup).
+template <int W_, int D_> struct HalfPlan {
+  using P = SlabPlan<W_ / 2, D_>;
+  static constexpr int W = W_, W2 = W_ / 2, D = D_, Dh = P::Dh;
+  static_assert(W_ % 2 == 0, "even W");
+  static constexpr int OFF_TWE = P::TOTAL;  // w^k, k < W/2 (the W-point table)
+  static constexpr int TOTAL = OFF_TWE + W2;
+  static constexpr size_t LDS_BYTES = (size_t)TOTAL * 8;
+  static constexpr int NRAW = W2 * D;  // raw floats of a unit (pass A staging, the bytes of Z)
+  TB_HD static int freq(int slot) { return (slot / P::LW) + P::Q0 * (slot % P::LW); }  // slot -> k''
+};
+
+// twiddles of a half unit: the W/2-point table (even entries of the W-point one), D, and w^k
+template <class HP, class Ctx>
+TB_HD void load_tw_half(Ctx& ctx, v2* lds, const tb_plan_dev& pl) {
+  using P = typename HP::P;
+  for (int i = ctx.tid; i < HP::W2; i += ctx.nthreads) {
+    lds[P::OFF_TWW + i] = V(pl.tw[1][2 * i].x, pl.tw[1][2 * i].y);
+    lds[HP::OFF_TWE + i] = V(pl.tw[1][i].x, pl.tw[1][i].y);
+  }
+  for (int i = ctx.tid; i < P::D; i += ctx.nthreads) lds[P::OFF_TWD + i] = V(pl.tw[2][i].x, pl.tw[2][i].y);
+}
+
+// W1 of a half unit: slot blk*LW + q holds k'' = blk + Q0 q; e = 1 scales by w^k''
+template <class HP>
+TB_HD void a_w1_half(const v2* lds, v2* __restrict__ Sb, int e, int it) {
+  using P = typename HP::P;
+  const int blk = it / P::Dh, k = it - blk * P::Dh;
+  const v2* x = lds + k * P::PX + blk * P::LW;
+  const v2* te = lds + HP::OFF_TWE;
+  v2 a[P::Q1];
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) a[q] = x[q];
+  v2* s = Sb + (blk * P::LW) * P::Dh + k;
+  dft_store<P::Q1, true>(a, [&](int q, v2 v) { s[q * P::Dh] = e ? cmul(v, te[blk + P::Q0 * q]) : v; });
+}
+
+// G0 inputs of a half unit (pass C): slot blk*LW + q of the unit's rows, e = 1 scaled by w^-k''
+template <class HP>
+TB_HD void c_load_half(v2* r, const v2* __restrict__ Sb, int it) {
+  using P = typename HP::P;
+  const int blk = it / P::Dh, k = it - blk * P::Dh;
+  const v2* s = Sb + (blk * P::LW) * P::Dh + k;
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) {
+    const f2v t = ld_stream<TB_NT_SPEC>(reinterpret_cast<const f2v*>(s + q * P::Dh));
+    r[q] = V(t.x, t.y);
+  }
+}
+template <class HP>
+TB_HD void c_twiddle_half(const v2* lds, v2* r, int e, int it) {
+  using P = typename HP::P;
+  if (!e) return;
+  const int blk = it / P::Dh;
+  const v2* te = lds + HP::OFF_TWE;
+  TB_UNROLL
+  for (int q = 0; q < P::Q1; ++q) r[q] = cmulc(r[q], te[blk + P::Q0 * q]);
+}
+
 // Slab shapes (W, D) with a compile-time plan in the device library
 #define TB_CT_SLAB_SHAPES(X) X(240, 155) X(128, 128)
+// ... of which these run as half units (split spectrum; W/2 two-stage, half slab <= 80 KB of LDS)
+#define TB_CT_HALF_SHAPES(X) X(240, 155)
 
 }  // namespace ct
 }  // namespace tb

@@ -260,6 +260,7 @@ struct tb_plan {
   int ncu = 256;         // compute units (grid of the persistent compiled-plan slab kernels)
   bool ct_slab = false;  // (W, D) has a compile-time slab plan (slab_ct.h)
   bool ct_tile = false;  // H has a compile-time pass-B plan (kspace_ct.h)
+  bool ct_half = false;  // (H, W, D) has half-unit passes A / C and the split pass B (slab_ct.h HalfPlan)
   float* tds = nullptr;  // band pass C': [D/2 + 1][2][NCOLS] cos / sin(2 pi kd d / D), d < D/2 + 1, else 0
   float* tbt = nullptr;  // band pass A': [2][KSd][2][64] B fragments of the folded D product
   bool generic = false;  // full-spectrum route on the direct-DFT fallback (kern_generic.hip)
@@ -349,6 +350,7 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   // compile-time slab plan: same shape and therefore the same radix order as the runtime plan
   p->ct_slab = !p->generic && tb::slab_ct_supported(W, D);
   p->ct_tile = !p->generic && tb::kspace_ct_supported(H);
+  p->ct_half = p->ct_slab && tb::slab_half_supported(W, D) && tb::kspace_half_supported(H, W, D);
   const SlabGeo sg = slab_geo(W, D);
   if ((size_t)sg.total_cf * 8 > (size_t)p->lds_max) p->generic = true;  // slab above the LDS: fallback too
   // device tables: tw[H], tw[W], tw[D] (cf) + rev_d[D], irev_h[H], irev_w[W] (int)
@@ -465,6 +467,14 @@ int tb_plan_radices(const tb_plan* plan, int axis, int* radices) {
 }
 
 static bool use_ct_slab(const tb_plan* p) { return g_compiled_plans && p->ct_slab; }
+
+// Half units + split spectrum for the full route's passes (slab_ct.h HalfPlan) where the plan has
+// them; TEXBIAS_HALF=0 or tb_set_half_units(0): the whole-slab compiled passes.
+static bool g_half = [] {
+  const char* e = std::getenv("TEXBIAS_HALF");
+  return !(e && e[0] == '0');
+}();
+static bool use_half(const tb_plan* p) { return g_half && use_ct_slab(p) && p->ct_half; }
 
 // channel-volumes per A -> B -> C chain (TEXBIAS_CHUNK_BC; 0 = all, the default).  Chunks of
 // 2..4 channel-volumes keep the spectrum within the Infinity Cache between passes, but measured
@@ -707,17 +717,27 @@ static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* 
     const int ng = (nbc - c0) < g ? (nbc - c0) : g;
     const int bc0 = b0 * C + c0;
     const double vox = (double)ng * H * W * D, spec = (double)ng * H * W * Dh * 8.0;
+    const bool half = use_half(p);
     {
-      Timer t(0, st, vox * 4.0 + spec, use_ct_slab(p) ? "k_slab_fwd_ct16" : "k_slab_fwd");
-      const int rc = launch_slab_fwd<RA>(p, x, xs, S, bc0, ng, st);
-      if (rc) return rc;
+      Timer t(0, st, vox * 4.0 + spec, half ? "k_slab_fwd_half" : use_ct_slab(p) ? "k_slab_fwd_ct16" : "k_slab_fwd");
+      if (half) {
+        SlabFwdArgs a{p->dev, x, xs[0], xs[1], xs[2], S, bc0, ng};
+        TB_HIP(tb::launch_slab_fwd_half(a, st));
+      } else {
+        const int rc = launch_slab_fwd<RA>(p, x, xs, S, bc0, ng, st);
+        if (rc) return rc;
+      }
     }
     {
       Timer t(1, st, 2.0 * spec,
-              (g_compiled_plans && p->ct_tile)
+              half ? "k_kspace_half"
+              : (g_compiled_plans && p->ct_tile)
                   ? (tb::kspace_ct_persistent(W * Dh) ? "k_kspace_ct2p" : "k_kspace_ct2")
                   : "k_kspace");
-      if (g_compiled_plans && p->ct_tile) {
+      if (half) {
+        KspaceArgs ka{p->dev, S, bc0, C, 32, c0, bo, ng};
+        TB_HIP(tb::launch_kspace_half(ka, p->ncu, st));
+      } else if (g_compiled_plans && p->ct_tile) {
         const int Tc = tb::kspace_ct_tile(W * Dh);
         KspaceArgs ka{p->dev, S, bc0, C, Tc, c0, bo, ng};
         TB_HIP(tb::launch_kspace_ct(ka, dim3((W * Dh + Tc - 1) / Tc, ng), p->ncu, st));
@@ -727,9 +747,12 @@ static int run_full(const tb_plan* p, const float* x, const int64_t* xs, float* 
       }
     }
     {
-      Timer t(2, st, spec + (double)ng * H * W * (D + y_pad) * 4.0, use_ct_slab(p) ? "k_slab_inv_ct" : "k_slab_inv");
+      Timer t(2, st, spec + (double)ng * H * W * (D + y_pad) * 4.0,
+              half ? "k_slab_inv_half" : use_ct_slab(p) ? "k_slab_inv_ct" : "k_slab_inv");
       SlabInvArgs ia{p->dev, S, y, ys[0], ys[1], ys[2], y_pad, bc0, C, scale, minmax, ng};
-      if (use_ct_slab(p))
+      if (half)
+        TB_HIP(tb::launch_slab_inv_half(ia, st));
+      else if (use_ct_slab(p))
         TB_HIP(tb::launch_slab_inv_ct(ia, p->ncu, st));
       else
         TB_HIP(launch_slab_inv<RA>(ia, dim3(H, ng), lds_s, st));
@@ -1159,6 +1182,11 @@ int tb_set_band_plans(int enable) {
 
 int tb_set_wrap_plans(int enable) {
   g_wrap = enable != 0;
+  return TB_OK;
+}
+
+int tb_set_half_units(int enable) {
+  g_half = enable != 0;
   return TB_OK;
 }
 

@@ -76,6 +76,7 @@ def _proto(L):
         "tb_set_band_inv16": (I, [I]),
         "tb_set_point_plans": (I, [I]),
         "tb_set_wrap_plans": (I, [I]),
+        "tb_set_half_units": (I, [I]),
         "tb_brats_prep_workspace_bytes": (SZ, [I, I]),
         "tb_brats_prep_f32": (I, [P, P, I, I, I, I, I, P, I, I, I, P, P, P, SZ, P]),
     }

@@ -197,16 +197,18 @@ class FusedChain:
     # --- device side --------------------------------------------------------------------
     def __call__(self, x: torch.Tensor, pad: int = 0, plans: Optional[List[List]] = None,
                  phases: Optional[Sequence[Sequence[float]]] = None, u: Optional[torch.Tensor] = None,
-                 cls: Optional[torch.Tensor] = None, seed: Optional[int] = None) -> torch.Tensor:
+                 cls: Optional[torch.Tensor] = None, seed: Optional[int] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``seed``: Philox key of the salt-and-pepper field (default: drawn from torch's global
         generator, which synchronises with the host; pass it explicitly to capture the chain in a
-        HIP graph)."""
+        HIP graph).  ``out``: optional [B, C, *spatial[:-1], D + pad] float32 buffer receiving the
+        result (the first k-space pass writes it directly, e.g. a captured train step's static input)."""
         rt.require_hip(x, "FusedChain")
         if x.dim() != 5:
             raise ValueError("FusedChain expects [B, C, H, W, D]")
         B, C = x.shape[:2]
         plans = plans if plans is not None else self.plan(B, tuple(x.shape[2:]), phases, C)
-        return self.execute(x, plans, pad=pad, u=u, cls=cls, seed=seed)
+        return self.execute(x, plans, pad=pad, u=u, cls=cls, seed=seed, out=out)
 
     def apply(self, data: dict, pad: int = 0, **kw) -> dict:
         """Dictionary form: ``data[self.key]`` through the chain; a "label" entry gets the channel
@@ -223,8 +225,10 @@ class FusedChain:
         return d
 
     def execute(self, x: torch.Tensor, plans: List[List], pad: int = 0, u: Optional[torch.Tensor] = None,
-                cls: Optional[torch.Tensor] = None, seed: Optional[int] = None) -> torch.Tensor:
-        """Run per-sample stage lists (``plan`` or deferred plans) over the batch x [B, C, *spatial]."""
+                cls: Optional[torch.Tensor] = None, seed: Optional[int] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Run per-sample stage lists (``plan`` or deferred plans) over the batch x [B, C, *spatial]
+        (``out``: see ``__call__``)."""
         rt.require_hip(x, "FusedChain")
         if x.dim() != 5:
             raise ValueError("FusedChain expects [B, C, H, W, D]")
@@ -235,6 +239,10 @@ class FusedChain:
                 raise ValueError(f"{nm} must have the input's shape {tuple(x.shape)}")
         if len(plans) != B:
             raise ValueError(f"{len(plans)} plans for a batch of {B}")
+        if out is not None:
+            want = tuple(x.shape[:-1]) + (x.shape[-1] + pad,)
+            if tuple(out.shape) != want or out.dtype != torch.float32 or out.device != x.device:
+                raise ValueError(f"out must be a float32 {want} tensor on the input's device")
         nst = len(plans[0])
         if any(len(p) != nst or [s[0] for s in p] != [s[0] for s in plans[0]] for p in plans):
             raise ValueError("all samples of a batch must share the stage structure")
@@ -254,7 +262,11 @@ class FusedChain:
                 if not any(progs):
                     continue   # every sample drew "no transform": identity
                 out_pad = pad if not padded else 0
-                if padded:   # filter the padded buffer in place (pass A reads all before C writes)
+                if out is not None and cur is x and C == x.shape[1]:   # first pass: straight into the caller's buffer
+                    rt.kspace_filter(cur, 3, progs, C, out=out, pad=out_pad, minmax=mm)
+                    cur = out
+                    padded = out_pad > 0
+                elif padded:   # filter the padded buffer in place (pass A reads all before C writes)
                     view = cur[..., : spatial[-1]]
                     rt.kspace_filter(view, 3, progs, C, out=view, minmax=mm)
                 else:   # the functional custom op (torch.compile / graph-capture friendly)
@@ -316,6 +328,9 @@ class FusedChain:
             cur = x.clone() if not pad else torch.nn.functional.pad(x, (0, pad))
         elif pad and not padded:
             cur = torch.nn.functional.pad(cur, (0, pad))
+        if out is not None and cur is not out:
+            out.copy_(cur)
+            cur = out
         return cur
 
 

@@ -388,6 +388,12 @@ def set_wrap_plans(enable: bool) -> None:
     check(lib().tb_set_wrap_plans(1 if enable else 0))
 
 
+def set_half_units(enable: bool) -> None:
+    """Full-spectrum passes A / C as half units (row parity) over a split spectrum where the plan
+    has them (240 x 240 x 155) when True (default), else whole slabs (tb_set_half_units)."""
+    check(lib().tb_set_half_units(1 if enable else 0))
+
+
 def set_band_inv16(enable: bool) -> None:
     """Pass C' synthesis in split f16 on the matrix cores when True (default, where the launch's
     V rows fit), else the f32 MFMA synthesis (tb_set_band_inv16)."""

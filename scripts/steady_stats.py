@@ -15,11 +15,12 @@ ap.add_argument("trace")
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--marker", default="k_slab_fwd")
 ap.add_argument("--top", type=int, default=40)
+ap.add_argument("--per-step", type=int, default=1, help="marker launches per step")
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [int(r["Start_Timestamp"]) for r in rows if a.marker in r["Kernel_Name"]]
-t0 = starts[-a.steps]
+t0 = starts[-a.steps * a.per_step]
 agg = collections.defaultdict(lambda: [0, 0])
 t_end = 0
 for r in rows:

@@ -66,7 +66,7 @@ def kspace_filter(x: np.ndarray, n_dims: int, programs, pad: int = 0, T: int = 0
     mm = np.zeros((B, 2), np.float32)
     progs = programs_array(programs)
     rc = lib().tbemu_kspace_filter_f32(H, W, D, x.ctypes.data, xs.ctypes.data, y.ctypes.data, ys.ctypes.data, pad,
-                                       B, Cc, C.addressof(progs), mm.ctypes.data, T, 1 if ct else 0)
+                                       B, Cc, C.addressof(progs), mm.ctypes.data, T, int(ct))
     if rc:
         raise RuntimeError(f"emulator error {rc}")
     if pad:

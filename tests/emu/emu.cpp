@@ -157,6 +157,116 @@ void ct_inv(int W, int D, const tb_plan_dev& pl, v2* lds, const v2* Sb, float* y
   TB_EMU_CT_SHAPES(TB_X)
 #undef TB_X
 }
+// ---- half units + split spectrum (slab_ct.h HalfPlan, kspace_ct.h b_mid_split), device phase order
+template <int W, int D>
+void half_fwd(const tb_plan_dev& pl, v2* lds, const float* xb, int64_t sw, v2* Sslab, int e) {
+  using HP = ct::HalfPlan<W, D>;
+  using P = typename HP::P;
+  HostCtx ctx;
+  ct::load_tw_half<HP>(ctx, lds, pl);
+  float* raw = reinterpret_cast<float*>(lds);
+  for (int L = 0; L < HP::NRAW; ++L) raw[L] = xb[(2 * (L / D) + e) * sw + L % D];
+  std::vector<v2> rf((size_t)P::N_F0 * P::R0);
+  for (int it = 0; it < P::N_F0; ++it) ct::a_load_raw<P>(raw, &rf[(size_t)P::R0 * it], it);
+  for (int it = 0; it < P::N_F0; ++it) ct::a_f0<P>(lds, &rf[(size_t)P::R0 * it], it);
+  if constexpr (P::FUSED_DU) {
+    std::vector<v2> rd(2 * (size_t)P::R1 * P::N_DU);
+    for (int it = 0; it < P::N_DU; ++it) ct::a_du_load<P>(lds, &rd[2 * P::R1 * it], it);
+    for (int it = 0; it < P::N_DU; ++it) ct::a_du_compute<P>(lds, &rd[2 * P::R1 * it], it);
+  } else {
+    for (int it = 0; it < P::N_D1; ++it) ct::a_d1<P>(lds, it);
+    std::vector<v2> ru(2 * (size_t)P::N_U);
+    for (int it = 0; it < P::N_U; ++it) ct::a_u_read<P>(lds, &ru[2 * it], it);
+    for (int it = 0; it < P::N_U; ++it) ct::a_u_write<P>(lds, &ru[2 * it], it);
+  }
+  for (int it = 0; it < P::N_W0; ++it) ct::a_w0<P>(lds, it);
+  for (int it = 0; it < P::N_W1; ++it) ct::a_w1_half<HP>(lds, Sslab + (int64_t)e * HP::W2 * P::Dh, e, it);
+}
+
+template <int W, int D>
+void half_inv(const tb_plan_dev& pl, v2* lds, const v2* Sslab, float* yb, int64_t sw, int ypad, float scale, int e,
+              float& lo, float& hi) {
+  using HP = ct::HalfPlan<W, D>;
+  using P = typename HP::P;
+  HostCtx ctx;
+  ct::load_tw_half<HP>(ctx, lds, pl);
+  v2 r[P::Q1];
+  const v2* Sb = Sslab + (int64_t)e * HP::W2 * P::Dh;
+  for (int it = 0; it < P::N_W1; ++it) {
+    ct::c_load_half<HP>(r, Sb, it);
+    ct::c_twiddle_half<HP>(lds, r, e, it);
+    ct::c_g0<P>(lds, r, it);
+  }
+  for (int it = 0; it < P::N_W0; ++it) ct::c_g1<P>(lds, it);
+  if constexpr (P::FUSED_DU) {
+    std::vector<v2> rd(2 * (size_t)P::R1 * P::N_DU);
+    for (int it = 0; it < P::N_DU; ++it) ct::c_re_load<P>(lds, &rd[2 * P::R1 * it], it);
+    for (int it = 0; it < P::N_DU; ++it) ct::c_re_compute<P>(lds, &rd[2 * P::R1 * it], it);
+  } else {
+    std::vector<v2> ru(2 * (size_t)P::N_U);
+    for (int it = 0; it < P::N_U; ++it) ct::c_r_read<P>(lds, &ru[2 * it], it);
+    for (int it = 0; it < P::N_U; ++it) ct::c_r_write<P>(lds, &ru[2 * it], it);
+    for (int it = 0; it < P::N_D1; ++it) ct::c_e1<P>(lds, it);
+  }
+  float* y0 = yb + (int64_t)e * sw;
+  for (int it = 0; it < P::N_F0; ++it) ct::c_e0<P>(lds, y0, 2 * sw, scale, it, lo, hi);
+  for (int w = 0; w < HP::W2; ++w)
+    for (int d = D; d < D + ypad; ++d) y0[2 * w * sw + d] = 0.f;
+}
+
+template <int H, int W, int D>
+void half_tile(const tb_plan_dev& pl, v2* lds, v2* S, int bc, int tile, const tb_sample_ops& so, int chan) {
+  using HP = ct::HalfPlan<W, D>;
+  using P = ct::TilePlan<H, 32>;
+  constexpr int TH = 16, ncols = W * HP::Dh, nh = HP::W2 * HP::Dh;
+  v2* Sc = S + (int64_t)bc * H * ncols + tile * TH;
+  for (int i = 0; i < H; ++i) lds[P::OFF_TW + i] = ct::V(pl.tw[0][i].x, pl.tw[0][i].y);
+  std::vector<ct::f4> r((size_t)(P::N0 / 2) * P::Q0);
+  for (int it = 0; it < P::N0 / 2; ++it) ct::b_load_split<P>(&r[(size_t)P::Q0 * it], Sc, ncols, nh, it);
+  for (int it = 0; it < P::N0 / 2; ++it) ct::b_s0_pair_regs<P>(lds, &r[(size_t)P::Q0 * it], it);
+  const int mk = ct::mask_kind(&so, 1);
+  for (int it = 0; it < P::Q0 * TH; ++it) {
+    FreqCol f0, f1;
+    ct::tile_col_half<HP>(tile * TH + it % TH, f0, f1);
+    if (mk == ct::MASK_GIBBS) ct::b_mid_split<P, ct::MASK_GIBBS>(lds, so, chan, f0, f1, it);
+    else if (mk == ct::MASK_LAYER) ct::b_mid_split<P, ct::MASK_LAYER>(lds, so, chan, f0, f1, it);
+    else if (mk == ct::MASK_DISK) ct::b_mid_split<P, ct::MASK_DISK>(lds, so, chan, f0, f1, it);
+    else ct::b_mid_split<P, ct::MASK_GENERIC>(lds, so, chan, f0, f1, it);
+  }
+  for (int it = 0; it < P::N0 / 2; ++it) ct::b_s1_split<P>(lds, Sc, ncols, nh, it);
+}
+
+// the device's half shapes (H = 240) plus a small one
+#define TB_EMU_HALF_SHAPES(X) X(240, 240, 155) X(20, 48, 35)
+bool half_has(int H, int W, int D) {
+#define TB_X(h, w, d) if (H == h && W == w && D == d) return true;
+  TB_EMU_HALF_SHAPES(TB_X)
+#undef TB_X
+  return false;
+}
+size_t half_lds_cf(int H, int W, int D) {
+#define TB_X(h, w, d) if (H == h && W == w && D == d) return std::max((size_t)ct::HalfPlan<w, d>::TOTAL, (size_t)ct::TilePlan<h, 32>::TOTAL);
+  TB_EMU_HALF_SHAPES(TB_X)
+#undef TB_X
+  return 0;
+}
+void half_run_fwd(int H, int W, int D, const tb_plan_dev& pl, v2* lds, const float* xb, int64_t sw, v2* Ss, int e) {
+#define TB_X(h, w, d) if (H == h && W == w && D == d) return half_fwd<w, d>(pl, lds, xb, sw, Ss, e);
+  TB_EMU_HALF_SHAPES(TB_X)
+#undef TB_X
+}
+void half_run_inv(int H, int W, int D, const tb_plan_dev& pl, v2* lds, const v2* Ss, float* yb, int64_t sw, int ypad,
+                  float scale, int e, float& lo, float& hi) {
+#define TB_X(h, w, d) if (H == h && W == w && D == d) return half_inv<w, d>(pl, lds, Ss, yb, sw, ypad, scale, e, lo, hi);
+  TB_EMU_HALF_SHAPES(TB_X)
+#undef TB_X
+}
+void half_run_tile(int H, int W, int D, const tb_plan_dev& pl, v2* lds, v2* S, int bc, int tile, const tb_sample_ops& so,
+                   int chan) {
+#define TB_X(h, w, d) if (H == h && W == w && D == d) return half_tile<h, w, d>(pl, lds, S, bc, tile, so, chan);
+  TB_EMU_HALF_SHAPES(TB_X)
+#undef TB_X
+}
 }  // namespace
 
 extern "C" {
@@ -181,9 +291,11 @@ int tbemu_kspace_filter_f32(int H, int W, int D, const float* x, const int64_t* 
   const SlabGeo sg = slab_geo(W, D);
   if (T <= 0) T = 64;
   const TileGeo tg = tile_geo(H, T);
+  const bool half = use_ct == 2 && half_has(H, W, D);
   const bool ct_on = use_ct && ct_has(W, D);
   const bool ct_b = use_ct && ct_tile_has(H);
-  std::vector<cf> lds((size_t)std::max({(size_t)sg.total_cf, (size_t)tg.total_cf, ct_lds_cf(W, D), ct_tile_lds_cf(H)}) +
+  std::vector<cf> lds((size_t)std::max({(size_t)sg.total_cf, (size_t)tg.total_cf, ct_lds_cf(W, D), ct_tile_lds_cf(H),
+                                        half_lds_cf(H, W, D)}) +
                       16);
   v2* ldsv = reinterpret_cast<v2*>(lds.data());
   std::vector<cf> S((size_t)B * C * H * W * Dh);
@@ -194,6 +306,23 @@ int tbemu_kspace_filter_f32(int H, int W, int D, const float* x, const int64_t* 
     float lo = 3.402823466e38f, hi = -3.402823466e38f;
     for (int c = 0; c < C; ++c) {
       const int bc = b * C + c;
+      for (int h = 0; h < H && half; ++h)
+        for (int e = 0; e < 2; ++e)
+          half_run_fwd(H, W, D, pl, ldsv, x + bc * xs[0] + h * xs[1], xs[2],
+                       reinterpret_cast<v2*>(S.data()) + ((int64_t)bc * H + h) * W * Dh, e);
+      if (half) {
+        for (int t = 0; t < (W / 2) * Dh / 16; ++t)
+          half_run_tile(H, W, D, pl, ldsv, reinterpret_cast<v2*>(S.data()), bc, t, ops[b], c);
+        for (int h = 0; h < H; ++h)
+          for (int e = 0; e < 2; ++e) {
+            float l = 3.402823466e38f, u = -3.402823466e38f;
+            half_run_inv(H, W, D, pl, ldsv, reinterpret_cast<const v2*>(S.data()) + ((int64_t)bc * H + h) * W * Dh,
+                         y + bc * ys[0] + h * ys[1], ys[2], y_pad, scale, e, l, u);
+            lo = l < lo ? l : lo;
+            hi = u > hi ? u : hi;
+          }
+        continue;
+      }
       for (int h = 0; h < H; ++h) {
         if (ct_on)
           ct_fwd(W, D, pl, ldsv, x + bc * xs[0] + h * xs[1], xs[2],

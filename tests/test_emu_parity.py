@@ -219,3 +219,34 @@ def test_compiled_tile_plan(shape):
     y2c, _ = _emu.kspace_filter(x[None], 3, [prog2], ct=True)
     y2g, _ = _emu.kspace_filter(x[None], 3, [prog2], ct=False)
     assert relerr(y2c, y2g) < 2e-6
+
+
+@pytest.mark.parametrize("shape", [(2, 20, 48, 35), (1, 240, 240, 155)])
+def test_half_units_split_spectrum(shape):
+    """Passes A / C as half units (row parity) over the split spectrum, pass B finishing the W
+    transform (slab_ct.h HalfPlan, kspace_ct.h b_mid_split): == oracle for the generic program path
+    (disk, spike, wrap; a grouped spike pair) and each mask-only middle phase (Gibbs, disk), == the
+    whole-slab compiled passes to rounding; pads zeroed, min/max epilogue exact."""
+    rng = np.random.default_rng(sum(shape) + 5)
+    x = rng.standard_normal(shape).astype(np.float32)
+    sp = x.shape[1:]
+    geo = K.geometry(sp)
+    idx = (min(5, sp[0] - 1), min(3, sp[1] - 1), min(7, sp[2] // 2))
+    prog = [K.disk_op(0.3 * min(sp), False), K.spike_op(idx, geo, 6.0, phase=0.7), K.wrap_op(0.5)]
+    yh, mmh = _emu.kspace_filter(x[None], 3, [prog], pad=3, ct=2)
+    ref = O.wrap_artifact(O.plane_waves(O.fourier_disk(x, 0.3 * min(sp)), idx, 6.0, phase=[0.7] * shape[0]), 0.5)
+    assert relerr(yh[0, ..., :sp[-1]], ref) < TOL
+    assert np.all(yh[0, ..., sp[-1]:] == 0)
+    y0 = yh[0, ..., :sp[-1]]
+    np.testing.assert_array_equal(mmh[0], [y0.min(), y0.max()])
+    yw, _ = _emu.kspace_filter(x[None], 3, [prog], pad=3, ct=True)
+    assert relerr(yh, yw) < 2e-6
+    yg, _ = _emu.kspace_filter(x[None], 3, [[K.gibbs_op(0.4, sp)]], ct=2)
+    assert relerr(yg[0], O.gibbs_noise(x, 0.4)) < TOL
+    yd, _ = _emu.kspace_filter(x[None], 3, [[K.disk_op(0.25 * min(sp), True)]], ct=2)
+    assert relerr(yd[0], O.fourier_disk(x, 0.25 * min(sp), inside_off=True)) < TOL
+    prog2 = [K.spike_op(idx, geo, 5.0, phase=0.1, chan=0), K.spike_op((1, 1, 1), geo, 7.0, phase=-0.3, chan=0)]
+    prog2[1].reserved = 1
+    y2h, _ = _emu.kspace_filter(x[None], 3, [prog2], ct=2)
+    y2g, _ = _emu.kspace_filter(x[None], 3, [prog2], ct=False)
+    assert relerr(y2h, y2g) < 2e-6
