@@ -505,8 +505,207 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
 }
 }  // namespace
 
+// ------------------------------------------------- the same layer in split precision on the bf16 matrix cores
+// f32 operands as three bf16 parts, x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1):
+// 24 significant bits, exact), and the six products whose magnitude reaches 2^-24 of the leading one,
+// a0 b0 + a0 b1 + a1 b0 + a0 b2 + a2 b0 + a1 b1, accumulated in f32 on mfma_f32_16x16x32_bf16 (8192
+// MACs per 16 cycles against 1024 per 32 for the f32 MFMA: 6 products cost 96 cycles where the f32 form
+// takes 256).  The three dropped terms are below 2^-24 of the leading product, so a dot product's error
+// is that of an f32 FMA chain (the f32 fixtures of tests/test_gpu_conv_up.py hold it to 4x ATen's own).
+// k = (tap, channel): a 32-k MFMA step is two taps x 16 channels; lane group g = lane >> 4 holds tap
+// 2 q + (g >> 1), channels 8 (g & 1) .. + 7, so its B operand is 8 channels of ONE input position: the
+// staged planes are channel-innermost bf16 [split][row][column][16], one 16-B read per split (lanes of a
+// ds_read_b128 group hit distinct banks at the 32-B position pitch).  The block's A operand (14 steps x 3
+// parts) lives in registers for the kernel's life.  Staging: a task (row, column, channel half) loads 8
+// channels (each a coalesced row of the NCDHW plane), splits them and writes 3 x 16 B.
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4b __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(const float* v, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)v[j];
+    const float r1 = v[j] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    p0[j] = h;
+    p1[j] = m;
+    p2[j] = (__bf16)r2;
+  }
+}
+
+struct X3Args {
+  const float* x;
+  const float* W;     // [16 m][16 c][27]
+  const float* bias;  // [16] or null
+  const float* add;   // [N][16][D][H][W] summed into y, or null
+  float* y;
+  int D, H, Wd;
+  int ZS, zlen, nyb;
+};
+
+template <int NXT, int NTH, bool ADD>
+__global__ __launch_bounds__(NTH) void k_conv16_x3(X3Args a) {
+  constexpr int YB = 3, NR = YB + 2, W = 16 * NXT, PXP = W + 2, NWV = NTH / 64;
+  constexpr int SPL = NR * PXP * 16;      // bf16 per split of one plane
+  constexpr int SLOT = 3 * SPL;           // bf16 per plane (3 splits)
+  constexpr int NTASK = NR * W * 2;       // (row, column, channel half)
+  constexpr int NL = (NTASK + NTH - 1) / NTH;
+  extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // [3 slots][3 splits][NR][PXP][16]
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int D = a.D, H = a.H;
+  for (int i = tid; i < 3 * SLOT / 8; i += NTH) reinterpret_cast<bf16x8*>(ring)[i] = bf16x8{};
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
+  // A: lane (m = l & 15, g = l >> 4), step q: tap 2 q + (g >> 1), channels 8 (g & 1) + j
+  const int li = lane & 15, g = lane >> 4;
+  bf16x8 af[14][3];
+#pragma unroll
+  for (int q = 0; q < 14; ++q) {
+    const int t = 2 * q + (g >> 1);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t < 27 ? a.W[(li * 16 + 8 * (g & 1) + j) * 27 + (t < 27 ? t : 0)] : 0.f;
+    split3(v, af[q][0], af[q][1], af[q][2]);
+  }
+  const int64_t plane = (int64_t)H * W;
+  const float* xb = a.x + (int64_t)n * 16 * D * plane;
+  // staging tasks of this thread: (row r, column x, channel half hh); goff = -1 for rows outside the image
+  int goff[NL], loff[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + NTH * j;
+    const int x = i % W, t = i / W, r = t % NR, hh = t / NR;
+    const int yi = y0 - 1 + r;
+    const bool ok = i < NTASK && yi >= 0 && yi < H;
+    goff[j] = ok ? (int)((int64_t)8 * hh * D * plane + (int64_t)yi * W + x) : -1;
+    loff[j] = (r * PXP + x + 1) * 16 + 8 * hh;
+  }
+  float rg[NL][8];
+  auto load = [&](int zi) {
+    const bool in = zi >= 0 && zi < D;
+    const float* src = xb + (int64_t)(in ? zi : 0) * plane;
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float v = src[(goff[j] < 0 ? 0 : goff[j]) + (int64_t)c * D * plane];
+        rg[j][c] = (in && goff[j] >= 0) ? v : 0.f;
+      }
+  };
+  auto store = [&](int zi) {
+    __bf16* d = ring + ((zi + 3) % 3) * SLOT;
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+      if (goff[j] >= 0) {
+        bf16x8 p0, p1, p2;
+        split3(rg[j], p0, p1, p2);
+        *reinterpret_cast<bf16x8*>(d + loff[j]) = p0;
+        *reinterpret_cast<bf16x8*>(d + SPL + loff[j]) = p1;
+        *reinterpret_cast<bf16x8*>(d + 2 * SPL + loff[j]) = p2;
+      }
+  };
+  __syncthreads();
+  load(z0 - 1);
+  store(z0 - 1);
+  load(z0);
+  store(z0);
+  load(z0 + 1);
+  const float bm[4] = {a.bias ? a.bias[4 * g] : 0.f, a.bias ? a.bias[4 * g + 1] : 0.f,
+                       a.bias ? a.bias[4 * g + 2] : 0.f, a.bias ? a.bias[4 * g + 3] : 0.f};
+  float* yb0 = a.y + (int64_t)n * 16 * D * plane;
+  const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * plane : nullptr;
+  constexpr int NT = YB * NXT;
+  for (int z = z0; z < z1; ++z) {
+    store(z + 1);
+    __syncthreads();
+    if (z + 1 < z1) load(z + 2);
+    for (int t0 = wave; t0 < NT; t0 += 2 * NWV) {
+      const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
+      const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
+      const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
+      f32x4b acc0 = {bm[0], bm[1], bm[2], bm[3]}, acc1 = acc0;
+#pragma unroll
+      for (int q = 0; q < 14; ++q) {
+        const int t = 2 * q + (g >> 1) < 27 ? 2 * q + (g >> 1) : 26;
+        const int tz = t / 9, ty = (t / 3) % 3, tx = t % 3;
+        const __bf16* sl = ring + ((z + tz + 2) % 3) * SLOT + 8 * (g & 1);
+        const int o0 = ((yy0 + ty) * PXP + x00 + li + tx) * 16, o1 = ((yy1 + ty) * PXP + x01 + li + tx) * 16;
+        bf16x8 b0[3], b1[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          b0[s] = *reinterpret_cast<const bf16x8*>(sl + s * SPL + o0);
+          b1[s] = *reinterpret_cast<const bf16x8*>(sl + s * SPL + o1);
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b0[1], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b1[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b0[2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b1[2], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][2], b0[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][2], b1[0], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b0[1], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b1[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b0[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b1[0], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b0[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b1[0], acc1, 0, 0, 0);
+      }
+      // C: column x = li, rows m = 4 g + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * g + r;
+        const int64_t o0 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy0) * W + x00 + li;
+        const int64_t o1 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy1) * W + x01 + li;
+        if (y0 + yy0 < H) yb0[o0] = ADD ? acc0[r] + ab0[o0] : acc0[r];
+        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc1[r] + ab0[o1] : acc1[r];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// TEXBIAS_CONV_X3=0: the f32-MFMA k_conv3d_fwd16 instead of the split-precision kernel
+bool conv_x3_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_CONV_X3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int launch_conv16_x3(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
+                     int Wd, hipStream_t st) {
+  X3Args a{};
+  a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.nyb = (H + 2) / 3;
+  const size_t lds = (size_t)3 * 3 * 5 * (Wd + 2) * 16 * 2;
+  if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
+  a.zlen = zseg(D, N * a.nyb, 1, 2);
+  a.ZS = (D + a.zlen - 1) / a.zlen;
+  void (*kern)(X3Args) = nullptr;
+#define TB_X3(NX)                                                                      \
+  case NX: kern = add ? k_conv16_x3<NX, 512, true> : k_conv16_x3<NX, 512, false>; break;
+  switch (Wd / 16) {
+    TB_X3(1) TB_X3(2) TB_X3(3) TB_X3(4) TB_X3(5) TB_X3(6) TB_X3(7)
+    default: return TB_ERR_UNSUPPORTED_SIZE;
+  }
+#undef TB_X3
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
+      hipSuccess)
+    return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(512), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+}  // namespace
+
 // Conv3d(16 -> 16, 3, stride 1, padding 1) forward: x [N][16][D][H][W] -> y [N][16][D][H][W], W % 16 == 0,
-// W <= 128; weight [16][16][27], bias [16] or NULL.  (csrc/conv_up.hip, k_conv3d_fwd16)
+// W <= 128; weight [16][16][27], bias [16] or NULL.  (csrc/conv_up.hip, k_conv16_x3 / k_conv3d_fwd16)
 int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
                         void* stream) {
   return tb_conv3d_fwd16_add_f32(x, W, bias, nullptr, y, N, D, H, Wd, stream);
@@ -516,6 +715,8 @@ int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, c
                             int H, int Wd, void* stream) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
+  if (conv_x3_on() && Wd <= 112)
+    return launch_conv16_x3(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
   // output rows per block (TEXBIAS_CONV16_YB 2..4; C3, W = 80: YB 2 / 3 / 4 = 478 / 419 / 482 us -- the
   // YB x 5 tiles of a step over 4 waves x 2 chains: 10 of 16, 15 of 16, 20 of 24 slots used; YB = 2's
   // second block per CU did not make up for it)

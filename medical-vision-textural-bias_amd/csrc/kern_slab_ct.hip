@@ -559,12 +559,12 @@ bool slab_half_supported(int W, int D) {
   return false;
 }
 
-// TEXBIAS_HALF_CFG (tuning): 0 = 256 threads with the fused DU / RE phase (default), 1 = 256 threads
-// unfused, 2 = 512 threads unfused
+// TEXBIAS_HALF_CFG (tuning): 2 = 512 threads unfused (default; gibbs-aug C3 chain 0.471 ms), 0 = 256
+// threads with the fused DU / RE phase (0.542), 1 = 256 threads unfused (0.551), 3 = 768 threads unfused
 static int half_cfg() {
   static const int c = [] {
     const char* e = std::getenv("TEXBIAS_HALF_CFG");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 2;
   }();
   return c;
 }
@@ -582,6 +582,7 @@ hipError_t launch_slab_fwd_half(const SlabFwdArgs& a, hipStream_t st) {
 #define TB_X(w, d)                                                                                   \
   if (a.pl.W == w && a.pl.D == d) {                                                                  \
     constexpr size_t lds = ct::HalfPlan<w, d>::LDS_BYTES;                                            \
+    if (half_cfg() == 3) return launch_half(k_slab_fwd_half<w, d, 768, false>, 768, lds, units, a, st); \
     if (half_cfg() == 2) return launch_half(k_slab_fwd_half<w, d, 512, false>, 512, lds, units, a, st); \
     if (half_cfg() == 1) return launch_half(k_slab_fwd_half<w, d, 256, false>, 256, lds, units, a, st); \
     return launch_half(k_slab_fwd_half<w, d, 256, true>, 256, lds, units, a, st);                    \
@@ -596,6 +597,7 @@ hipError_t launch_slab_inv_half(const SlabInvArgs& a, hipStream_t st) {
 #define TB_X(w, d)                                                                                   \
   if (a.pl.W == w && a.pl.D == d) {                                                                  \
     constexpr size_t lds = ct::HalfPlan<w, d>::LDS_BYTES;                                            \
+    if (half_cfg() == 3) return launch_half(k_slab_inv_half<w, d, 768, false>, 768, lds, units, a, st); \
     if (half_cfg() == 2) return launch_half(k_slab_inv_half<w, d, 512, false>, 512, lds, units, a, st); \
     if (half_cfg() == 1) return launch_half(k_slab_inv_half<w, d, 256, false>, 256, lds, units, a, st); \
     return launch_half(k_slab_inv_half<w, d, 256, true>, 256, lds, units, a, st);                    \
