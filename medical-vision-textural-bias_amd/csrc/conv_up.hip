@@ -45,15 +45,21 @@ struct S2Args {
   int PX, RR;  // LDS row pitch; rows per channel slab (2 TY + 1)
 };
 
-template <int CIN, int MOUT, int TY, int WV>  // WV: most float4 per input row (Wi <= 4 WV)
-__global__ __launch_bounds__(256) void k_conv_s2_fewin(S2Args a) {
+// NTH = 512: the two halves of the block share the positions and split the output pairs (registers of
+// the 27 CIN inputs + half the accumulators: two waves per SIMD instead of one for CIN = 4, MOUT = 32)
+template <int CIN, int MOUT, int TY, int WV, int NTH = 256>  // WV: most float4 per input row (Wi <= 4 WV)
+__global__ __launch_bounds__(NTH) void k_conv_s2_fewin(S2Args a) {
   static_assert(MOUT % 2 == 0, "packed output pairs");
+  constexpr int NHALF = NTH / 256, MP = MOUT / 2 / NHALF;  // output pairs per half
   constexpr int NR = 2 * TY + 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x;
   constexpr int PX = 4 * WV + 12, SS = CIN * NR * PX;  // row pitch (odd multiple of 4), slot stride
-  float* ring = smem;                        // [5][CIN][NR][PX], input column xi at xi + 4
-  for (int i = tid; i < 5 * SS; i += 256) ring[i] = 0.f;  // halos, padding rows stay 0
+  // [3][CIN][NR][PX], input column xi at xi + 4: step z reads planes 2z - 1 .. 2z + 1; its first stores
+  // put planes 2z, 2z + 1 over the slots of 2z - 3, 2z - 2 (three slots instead of five: 58 KB at the
+  // C3 shapes, two blocks per CU)
+  float* ring = smem;
+  for (int i = tid; i < 3 * SS; i += NTH) ring[i] = 0.f;  // halos, padding rows stay 0
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -65,11 +71,11 @@ __global__ __launch_bounds__(256) void k_conv_s2_fewin(S2Args a) {
   const float4* inb = reinterpret_cast<const float4*>(a.in + (int64_t)n * CIN * Di * iplane);
   // staging items of one plane: (c, r, q) -> input row 2 y0 - 1 + r, float4 q
   const int W4 = Wi >> 2;
-  constexpr int NL = (CIN * NR * WV + 255) / 256;
+  constexpr int NL = (CIN * NR * WV + NTH - 1) / NTH;
   int gof[NL], lof[NL];
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NTH * j;
     const int q = i % W4, t = i / W4, r = t % NR, c = t / NR;
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < CIN && yi >= 0 && yi < Hi;
@@ -82,29 +88,32 @@ __global__ __launch_bounds__(256) void k_conv_s2_fewin(S2Args a) {
     const float4* src = inb + (int64_t)(in ? zi : 0) * iplane4;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const float4 v = src[gof[j] < 0 ? 0 : gof[j]];
-      r[j] = (in && gof[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      r[j] = src[gof[j] < 0 ? 0 : gof[j]];  // zeroed at the store (a select here waits for the load)
     }
   };
   auto store = [&](int zi, const float4 (&r)[NL]) {
-    float* d = ring + ((zi + 5) % 5) * SS;
+    float* d = ring + ((zi + 3) % 3) * SS;
+    const bool in = zi >= 0 && zi < Di;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = r[j];
+      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = in ? r[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   __syncthreads();  // zero fill before any slab store
   load(2 * z0 - 1, ra);
   store(2 * z0 - 1, ra);
   load(2 * z0, ra);
   load(2 * z0 + 1, rb);
-  // this thread's output position: row y0 + oy, column ox
-  const int Wo = a.Wo, oy = tid / Wo, ox = tid - oy * Wo;
+  // this thread's output position: row y0 + oy, column ox; output pairs mh * MP .. + MP - 1
+  const int pt = tid & 255, mh = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int Wo = a.Wo, oy = pt / Wo, ox = pt - oy * Wo;
   const bool act = oy < TY && y0 + oy < a.Ho;
   const int roff = (2 * oy) * PX + 2 * ox + 3;  // + (ty PX + tx): input row 2 oy + ty, column 2 ox + tx - 1
-  f2v bias2[MOUT / 2];
+  f2v bias2[MP];
 #pragma unroll
-  for (int m = 0; m < MOUT / 2; ++m)
-    bias2[m] = a.bias ? f2v{a.bias[2 * m], a.bias[2 * m + 1]} : f2v{0.f, 0.f};
+  for (int mm = 0; mm < MP; ++mm) {
+    const int m = mh * MP + mm;
+    bias2[mm] = a.bias ? f2v{a.bias[2 * m], a.bias[2 * m + 1]} : f2v{0.f, 0.f};
+  }
   const int64_t oplane = (int64_t)a.Ho * Wo;
   float* outb = a.out + (int64_t)n * MOUT * a.Do * oplane + (int64_t)(y0 + oy) * Wo + ox;
   for (int z = z0; z < z1; ++z) {
@@ -120,7 +129,7 @@ __global__ __launch_bounds__(256) void k_conv_s2_fewin(S2Args a) {
       float v[CIN * 27];
 #pragma unroll
       for (int tz = 0; tz < 3; ++tz) {
-        const float* sl = ring + ((2 * z - 1 + tz + 5) % 5) * SS + roff;
+        const float* sl = ring + ((2 * z - 1 + tz + 3) % 3) * SS + roff;
 #pragma unroll
         for (int c = 0; c < CIN; ++c)
 #pragma unroll
@@ -131,8 +140,9 @@ __global__ __launch_bounds__(256) void k_conv_s2_fewin(S2Args a) {
       const cf2v_p kp = (cf2v_p)(cfloat_p)a.K;
       float* o = outb + (int64_t)z * oplane;
 #pragma unroll
-      for (int m = 0; m < MOUT / 2; ++m) {
-        f2v acc = bias2[m];
+      for (int mm = 0; mm < MP; ++mm) {
+        const int m = mh * MP + mm;
+        f2v acc = bias2[mm];
 #pragma unroll
         for (int k = 0; k < CIN * 27; ++k) acc = __builtin_elementwise_fma(f2v{v[k], v[k]}, kp[m * CIN * 27 + k], acc);
         o[(int64_t)(2 * m) * a.Do * oplane] = acc.x;
@@ -154,14 +164,16 @@ struct TArgs {
   int PX, CS;  // LDS row pitch, channel slab stride (TY + 1 rows)
 };
 
-template <int MO, int TY, int WV>
-__global__ __launch_bounds__(256) void k_convT_fewout(TArgs a) {
+template <int MO, int TY, int WV, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_convT_fewout(TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x;
   constexpr int PX = 4 * WV + 8, CS = (TY + 1) * PX;
   const int Cin = a.Cin, SS = Cin * CS;
-  float* ring = smem;            // [3][Cin][TY + 1][PX], column xi at xi + 4 (xi = Wi: zero)
-  for (int i = tid; i < 3 * SS; i += 256) ring[i] = 0.f;
+  // [2][Cin][TY + 1][PX], column xi at xi + 4 (xi = Wi: zero): step z reads planes z, z + 1; its first
+  // store puts plane z + 1 over the slot of z - 1
+  float* ring = smem;
+  for (int i = tid; i < 2 * SS; i += NTH) ring[i] = 0.f;
   const cfloat_p wg = (cfloat_p)a.W;  // [Cin][MO][27], scalar loads
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
@@ -174,12 +186,12 @@ __global__ __launch_bounds__(256) void k_convT_fewout(TArgs a) {
   const float4* xb = reinterpret_cast<const float4*>(a.x + (int64_t)n * Cin * Di * iplane);
   const int W4 = Wi >> 2;
   // staging items of one plane: (c, r, q) -> input row y0 + r (r <= TY), float4 q; at most 32 channels
-  constexpr int NL = (32 * (TY + 1) * WV + 255) / 256;
+  constexpr int NL = (32 * (TY + 1) * WV + NTH - 1) / NTH;
   const int nitem = Cin * (TY + 1) * W4;
   int gof[NL], lof[NL];
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NTH * j;
     const int q = i % W4, t = i / W4, r = t % (TY + 1), c = t / (TY + 1);
     const int yi = y0 + r;
     const bool ok = i < nitem && yi < Hi;
@@ -192,15 +204,15 @@ __global__ __launch_bounds__(256) void k_convT_fewout(TArgs a) {
     const float4* src = xb + (int64_t)(in ? zi : 0) * iplane4;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const float4 v = src[gof[j] < 0 ? 0 : gof[j]];
-      rg[j] = (in && gof[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      rg[j] = src[gof[j] < 0 ? 0 : gof[j]];  // zeroed at the store (a select here waits for the load)
     }
   };
   auto store = [&](int zi) {
-    float* d = ring + (zi % 3) * SS;
+    float* d = ring + (zi & 1) * SS;
+    const bool in = zi < Di;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = in ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   __syncthreads();
   load(z0);
@@ -226,8 +238,8 @@ __global__ __launch_bounds__(256) void k_convT_fewout(TArgs a) {
 #pragma unroll
       for (int p = 0; p < 8; ++p) acc[m][p >> 2][(p >> 1) & 1][p & 1] = bia[m];
     if (act) {
-      const float* s0 = ring + (z % 3) * SS + roff;
-      const float* s1 = ring + ((z + 1) % 3) * SS + roff;
+      const float* s0 = ring + (z & 1) * SS + roff;
+      const float* s1 = ring + ((z + 1) & 1) * SS + roff;
 #pragma unroll 1
       for (int c = 0; c < Cin; ++c) {
         float v[2][2][2];  // [dz][dy][dx]
@@ -301,14 +313,16 @@ int zseg(int D, int base, int per_cu, int fill) {
 template <int CIN, int MOUT, int WV>
 int launch_s2(S2Args& a, size_t lds, int N, hipStream_t st) {
   constexpr int TY = 3;
-  auto kern = k_conv_s2_fewin<CIN, MOUT, TY, WV>;
+  // CIN = 4, MOUT = 32 (the stacked entry unit + residual): 512 threads splitting the output pairs
+  constexpr int NT = (CIN == 4 && MOUT == 32) ? 512 : 256;
+  auto kern = k_conv_s2_fewin<CIN, MOUT, TY, WV, NT>;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;
   const int per_cu = lds <= 81920 ? 2 : 1;
   a.zlen = zseg(a.Do, N * a.nyb, per_cu, 1);
   a.ZS = (a.Do + a.zlen - 1) / a.zlen;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(NT), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
@@ -330,7 +344,7 @@ int tb_conv3d_s2_fewin_f32(const float* in, const float* K, const float* bias, f
   a.PX = 4 * (wide ? 64 : 40) + 12;  // = the kernel's compile-time pitch: data at column 4 .. Wi + 3
   a.RR = 2 * TY + 1;
   a.nyb = (Ho + TY - 1) / TY;
-  const size_t lds = (size_t)4 * 5 * Cin * a.RR * a.PX;
+  const size_t lds = (size_t)4 * 3 * Cin * a.RR * a.PX;
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define TB_S2(CI, MO)                                                                                  \
@@ -347,14 +361,18 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
   if (!x || !W || !y || N < 1 || Di < 1 || Hi < 1 || Wi < 1) return TB_ERR_INVALID_ARG;
   if (Cin < 1 || Cin > 32 || Mout < 1 || Mout > 4 || Wi % 4 != 0 || Wi > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
-  const int TY = 256 / Wi >= 3 ? 3 : 256 / Wi >= 2 ? 2 : 1;
+  // 512 threads over 6 input rows where the two-slot ring of 7 rows fits (one block of 8 waves per CU,
+  // two per SIMD, so the scalar weight loads of one wave hide under the other's FMAs); else 256 threads
+  const bool big = Wi <= 80 && (size_t)4 * 2 * Cin * 7 * (4 * 20 + 8) <= 163840;
+  const int TY = big ? 6 : 256 / Wi >= 3 ? 3 : 256 / Wi >= 2 ? 2 : 1;
+  const int nth = big ? 512 : 256;
   TArgs a{};
   a.x = x, a.W = W, a.bias = bias, a.y = y;
   a.Cin = Cin, a.Di = Di, a.Hi = Hi, a.Wi = Wi;
   a.PX = 4 * (Wi <= 80 ? 20 : 32) + 8;  // = the kernel's compile-time pitch
   a.CS = (TY + 1) * a.PX;
   a.nyb = (Hi + TY - 1) / TY;
-  const size_t lds = (size_t)4 * 3 * Cin * a.CS;
+  const size_t lds = (size_t)4 * 2 * Cin * a.CS;
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
   const int per_cu = lds <= 81920 ? 2 : 1;
   a.zlen = zseg(Di, N * a.nyb, per_cu, 1);
@@ -367,11 +385,13 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
   TB_T(1, 1) TB_T(1, 2) TB_T(1, 3) TB_T(2, 1) TB_T(2, 2) TB_T(2, 3) TB_T(3, 1) TB_T(3, 2) TB_T(3, 3) TB_T(4, 1)
   TB_T(4, 2) TB_T(4, 3)
 #undef TB_T
+  if (big) kern = Mout == 1 ? k_convT_fewout<1, 6, 20, 512> : Mout == 2 ? k_convT_fewout<2, 6, 20, 512>
+                : Mout == 3 ? k_convT_fewout<3, 6, 20, 512> : k_convT_fewout<4, 6, 20, 512>;
   if (!kern) return TB_ERR_UNSUPPORTED_SIZE;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(nth), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
@@ -436,15 +456,15 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
     const float4* src = xb + (int64_t)(in ? zi : 0) * plane4;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const float4 v = src[gof[j] < 0 ? 0 : gof[j]];
-      rg[j] = (in && gof[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      rg[j] = src[gof[j] < 0 ? 0 : gof[j]];  // zeroed at the store (a select here waits for the load)
     }
   };
   auto store = [&](int zi) {
     float* d = ring + ((zi + 3) % 3) * SS;
+    const bool in = zi >= 0 && zi < D;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = in ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   __syncthreads();
   load(z0 - 1);
@@ -505,6 +525,157 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
 }
 }  // namespace
 
+// ------------------------------------------------- the same kernel with DMA-staged planes
+// k_conv3d_fwd16 stages the next plane through registers, and hipcc puts `s_waitcnt vmcnt(0)` before the
+// first MFMA of every step (it cannot tell the A fragments' start-up loads from the plane loads), so the
+// fetch of plane z + 2 never overlaps step z's MFMAs.  Here the planes arrive by global -> LDS DMA (no
+// registers) into a 4-slot ring -- plane z + 2 in flight during step z, drained by the step's closing
+// barrier -- and the weights and bias come through LDS, so no ordinary global load is outstanding in
+// the loop.  Same arithmetic and accumulation order as k_conv3d_fwd16 (bitwise the same results).
+namespace {
+typedef __attribute__((address_space(1))) const void* gptr_tc;
+typedef __attribute__((address_space(3))) void* lptr_tc;
+
+template <int NXT, bool ADD>
+__global__ __launch_bounds__(512) void k_conv3d_fwd16_dma(F16Args a) {
+  constexpr int YB = 3, NTH = 512, NWV = 8, NR = YB + 2, W = 16 * NXT, NSEG = (W + 63) / 64;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int D = a.D, H = a.H, PX = a.PX, RX = a.RX, SS = 16 * RX;
+  float* ring = smem;            // [4][16 c][NR][PX], column x at x + 4
+  float* wl = smem + 4 * SS;     // W [16][16][27], then bias [16]
+  for (int i = tid; i < 4 * SS; i += NTH) ring[i] = 0.f;
+  for (int i = tid; i < 16 * 16 * 27; i += NTH) wl[i] = a.W[i];
+  if (tid < 16) wl[16 * 16 * 27 + tid] = a.bias ? a.bias[tid] : 0.f;
+  int b = (int)blockIdx.x;
+  const int zs = b % a.ZS;
+  b /= a.ZS;
+  const int yb = b % a.nyb, n = b / a.nyb;
+  const int y0 = yb * YB;
+  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
+  const int64_t plane = (int64_t)H * W;
+  const float* xb = a.x + (int64_t)n * 16 * D * plane;
+  __syncthreads();
+  const int li = lane & 15, ks = lane >> 4;
+  float af[108];
+#pragma unroll
+  for (int kk = 0; kk < 108; ++kk) af[kk] = wl[(li * 16 + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
+  float bm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bm[r] = wl[16 * 16 * 27 + 4 * ks + r];
+  // plane zi into slot zi & 3: each in-image row by 4-B DMA pieces (one row per wave instruction group);
+  // a plane outside [0, D) zeroes the slot's in-image rows (rows outside the image stay zero)
+  auto stage = [&](int zi) {
+    float* sl = ring + (zi & 3) * SS;
+    const bool in = zi >= 0 && zi < D;
+    for (int row = wave; row < 16 * NR; row += NWV) {
+      const int c = row / NR, r = row - c * NR, yi = y0 - 1 + r;
+      if (yi < 0 || yi >= H) continue;
+      float* dst = sl + c * RX + r * PX + 4;
+      if (in) {
+        const float* src = xb + ((int64_t)c * D + zi) * plane + (int64_t)yi * W;
+#pragma unroll
+        for (int sg = 0; sg < NSEG; ++sg) {
+          const int xx = lane + 64 * sg;
+          if (xx < W) __builtin_amdgcn_global_load_lds((gptr_tc)(src + xx), (lptr_tc)(dst + 64 * sg), 4, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int sg = 0; sg < NSEG; ++sg) {
+          const int xx = lane + 64 * sg;
+          if (xx < W) dst[xx] = 0.f;
+        }
+      }
+    }
+  };
+  stage(z0 - 1);
+  stage(z0);
+  stage(z0 + 1);
+  __syncthreads();  // (drains the DMA)
+  const int bl = ks * RX + li + 3;
+  float* yb0 = a.y + (int64_t)n * 16 * D * plane;
+  const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * plane : nullptr;
+  constexpr int NT = YB * NXT;
+  for (int z = z0; z < z1; ++z) {
+    if (z + 1 < z1) stage(z + 2);  // over plane z - 2 (last read in step z - 1)
+    const float* s0 = ring + ((z + 3) & 3) * SS + bl;  // tz = 0: plane z - 1
+    const float* s1 = ring + (z & 3) * SS + bl;
+    const float* s2 = ring + ((z + 1) & 3) * SS + bl;
+    for (int t0 = wave; t0 < NT; t0 += 2 * NWV) {
+      const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
+      const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
+      const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
+      const int o0 = yy0 * PX + x00, o1 = yy1 * PX + x01;
+      f32x4 acc0 = {bm[0], bm[1], bm[2], bm[3]}, acc1 = acc0;
+#pragma unroll
+      for (int tz = 0; tz < 3; ++tz) {
+        const float* sl = tz == 0 ? s0 : tz == 1 ? s1 : s2;
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const int t = tz * 9 + ty * 3 + tx;
+#pragma unroll
+            for (int cq = 0; cq < 4; ++cq) {
+              const int off = 4 * cq * RX + ty * PX + tx;
+              const float b0 = sl[o0 + off], b1 = sl[o1 + off];
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], b0, acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], b1, acc1, 0, 0, 0);
+            }
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * ks + r;
+        const int64_t o0 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy0) * W + x00 + li;
+        const int64_t o1 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy1) * W + x01 + li;
+        if (y0 + yy0 < H) yb0[o0] = ADD ? acc0[r] + ab0[o0] : acc0[r];
+        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc1[r] + ab0[o1] : acc1[r];
+      }
+    }
+    __syncthreads();  // plane z + 2 landed (vmcnt(0)); every wave is done with plane z - 1's slot
+  }
+}
+
+// TEXBIAS_CONV16_DMA=1: this variant instead of the register-staged k_conv3d_fwd16 (off: 439 vs 382 us
+// at 2 x 16 x 120 x 120 x 80 -- 4-B DMA pieces, 4x the memory instructions of the float4 loads)
+bool conv16_dma_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_CONV16_DMA");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+int launch_fwd16_dma(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
+                     int Wd, hipStream_t st) {
+  F16Args a{};
+  a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.PX = Wd + 8;
+  a.RX = 5 * a.PX;
+  while ((a.RX & 31) != 16) ++a.RX;
+  a.nyb = (H + 2) / 3;
+  const size_t lds = (size_t)4 * (4 * 16 * a.RX + 16 * 16 * 27 + 16);
+  if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
+  a.zlen = zseg(D, N * a.nyb, 1, 2);
+  a.ZS = (D + a.zlen - 1) / a.zlen;
+  void (*kern)(F16Args) = nullptr;
+#define TB_FD(NX) \
+  case NX: kern = add ? k_conv3d_fwd16_dma<NX, true> : k_conv3d_fwd16_dma<NX, false>; break;
+  switch (Wd / 16) {
+    TB_FD(1) TB_FD(2) TB_FD(3) TB_FD(4) TB_FD(5) TB_FD(6) TB_FD(7) TB_FD(8)
+    default: return TB_ERR_UNSUPPORTED_SIZE;
+  }
+#undef TB_FD
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
+      hipSuccess)
+    return TB_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(512), lds, st, a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+}  // namespace
+
 // ------------------------------------------------- the same layer in split precision on the bf16 matrix cores
 // f32 operands as three bf16 parts, x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1):
 // 24 significant bits, exact), and the six products whose magnitude reaches 2^-24 of the leading one,
@@ -543,6 +714,7 @@ struct X3Args {
   float* y;
   int D, H, Wd;
   int ZS, zlen, nyb;
+  int diag;  // measurement only (TEXBIAS_X3_DIAG): 1 skips the plane loads, 2 the MFMA phase; results invalid
 };
 
 template <int NXT, int NTH, bool ADD>
@@ -587,24 +759,26 @@ __global__ __launch_bounds__(NTH) void k_conv16_x3(X3Args a) {
     goff[j] = ok ? (int)((int64_t)8 * hh * D * plane + (int64_t)yi * W + x) : -1;
     loff[j] = (r * PXP + x + 1) * 16 + 8 * hh;
   }
+  // loads unconditional (clamped to valid addresses), validity applied when the plane is stored: a
+  // select right after a load made the compiler branch on the plane test and wait for every load
   float rg[NL][8];
   auto load = [&](int zi) {
-    const bool in = zi >= 0 && zi < D;
-    const float* src = xb + (int64_t)(in ? zi : 0) * plane;
+    const float* src = xb + (int64_t)(zi >= 0 && zi < D ? zi : 0) * plane;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const float v = src[(goff[j] < 0 ? 0 : goff[j]) + (int64_t)c * D * plane];
-        rg[j][c] = (in && goff[j] >= 0) ? v : 0.f;
-      }
+      for (int c = 0; c < 8; ++c) rg[j][c] = src[(goff[j] < 0 ? 0 : goff[j]) + (int64_t)c * D * plane];
   };
   auto store = [&](int zi) {
     __bf16* d = ring + ((zi + 3) % 3) * SLOT;
+    const bool in = zi >= 0 && zi < D;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
       if (goff[j] >= 0) {
         bf16x8 p0, p1, p2;
+        if (!in)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) rg[j][c] = 0.f;
         split3(rg[j], p0, p1, p2);
         *reinterpret_cast<bf16x8*>(d + loff[j]) = p0;
         *reinterpret_cast<bf16x8*>(d + SPL + loff[j]) = p1;
@@ -625,8 +799,8 @@ __global__ __launch_bounds__(NTH) void k_conv16_x3(X3Args a) {
   for (int z = z0; z < z1; ++z) {
     store(z + 1);
     __syncthreads();
-    if (z + 1 < z1) load(z + 2);
-    for (int t0 = wave; t0 < NT; t0 += 2 * NWV) {
+    if (z + 1 < z1 && !(a.diag & 1)) load(z + 2);
+    for (int t0 = wave; t0 < NT && !(a.diag & 2); t0 += 2 * NWV) {
       const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
       const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
       const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
@@ -670,11 +844,12 @@ __global__ __launch_bounds__(NTH) void k_conv16_x3(X3Args a) {
   }
 }
 
-// TEXBIAS_CONV_X3=0: the f32-MFMA k_conv3d_fwd16 instead of the split-precision kernel
+// TEXBIAS_CONV_X3=1: the split-precision kernel instead of the f32-MFMA k_conv3d_fwd16 (off: in the C3
+// step it measured no faster, 350-365 vs 352 us -- the layer is not bound by the matrix cores, see DESIGN)
 bool conv_x3_on() {
   static const bool on = [] {
     const char* e = std::getenv("TEXBIAS_CONV_X3");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -683,6 +858,11 @@ int launch_conv16_x3(const float* x, const float* W, const float* bias, const fl
                      int Wd, hipStream_t st) {
   X3Args a{};
   a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  static const int diag = [] {
+    const char* e = std::getenv("TEXBIAS_X3_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.diag = diag;
   a.nyb = (H + 2) / 3;
   const size_t lds = (size_t)3 * 3 * 5 * (Wd + 2) * 16 * 2;
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
@@ -717,6 +897,10 @@ int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, c
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
   if (conv_x3_on() && Wd <= 112)
     return launch_conv16_x3(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
+  if (conv16_dma_on()) {
+    const int rc = launch_fwd16_dma(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
+    if (rc != TB_ERR_UNSUPPORTED_SIZE) return rc;
+  }
   // output rows per block (TEXBIAS_CONV16_YB 2..4; C3, W = 80: YB 2 / 3 / 4 = 478 / 419 / 482 us -- the
   // YB x 5 tiles of a step over 4 waves x 2 chains: 10 of 16, 15 of 16, 20 of 24 slots used; YB = 2's
   // second block per CU did not make up for it)
@@ -833,16 +1017,17 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
     const float* src = xb + (int64_t)(in ? zi : 0) * plane;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const bool ok = in && gof[j] >= 0;
-      const float4 v = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
-      rg[j] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool ok = in && gof[j] >= 0;  // zeroed at the store (a select here waits for the load)
+      rg[j] = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
     }
   };
   auto store = [&](int zi) {
     float* d = ring + (zi & 1) * SS;
+    const bool in = zi < Di;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (lof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+      if (lof[j] >= 0)
+        *reinterpret_cast<float4*>(d + lof[j]) = (in && gof[j] >= 0) ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   __syncthreads();
   load(z0);
@@ -1023,16 +1208,17 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
     const float* src = xb + (int64_t)(in ? zi : 0) * plane;
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const bool ok = in && gof[j] >= 0;
-      const float4 v = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
-      rg[j] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool ok = in && gof[j] >= 0;  // zeroed at the store (a select here waits for the load)
+      rg[j] = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
     }
   };
   auto store = [&](int zi) {
     float* d = ring + ((zi + 3) % 3) * SS;
+    const bool in = zi >= 0 && zi < D;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (lof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = rg[j];
+      if (lof[j] >= 0)
+        *reinterpret_cast<float4*>(d + lof[j]) = (in && gof[j] >= 0) ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   __syncthreads();
   load(z0 - 1);
