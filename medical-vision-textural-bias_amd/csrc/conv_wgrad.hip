@@ -335,50 +335,76 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
   const int64_t plane = (int64_t)H * W;
   const float* Gb = a.G + ((int64_t)n * a.M + m0) * D * plane;
   const float* Xb = a.X + ((int64_t)n * a.Cc + c0) * D * plane;
-  // slabs arrive by global -> LDS DMA, one row per wave-instruction group (4-B pieces, no registers):
-  // register staging left hipcc waiting for the next plane's loads right after issuing them (it ran out
-  // of registers for the staging and the addresses), so no slab was ever in flight across a step.  X
-  // rows: channel c < cv, image row y0 - 1 + r; G rows: m < mv, row y0 + yy (absent rows stay zero).
-  constexpr int NSEG = WV * 4 / 64 + 1;
-  auto dma_row = [&](const float* src, float* dst) {
+  // staging items, fixed per thread for the whole march: global offset within a plane (-1: none)
+  // and LDS offset within a slab -- X (c, r, q) with row y0 - 1 + r in range, G (m, yy, q)
+  const int W4v = W >> 2;
+  constexpr int NXL = (16 * NXR * WV + 255) / 256, NGL = (16 * YB * WV + 255) / 256;
+  int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
 #pragma unroll
-    for (int sg = 0; sg < NSEG; ++sg) {
-      const int xx = lane + 64 * sg;
-      if (xx < W) __builtin_amdgcn_global_load_lds((gptr_t)(src + xx), (lptr_t)(dst + 64 * sg), 4, 0, 0);
+  for (int j = 0; j < NXL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4v, t = i / W4v, r = t % NXR, c = t / NXR;
+    const int y = y0 - 1 + r;
+    const bool ok = c < cv && y >= 0 && y < H;
+    xg[j] = ok ? (int)(((int64_t)c * D) * plane / 4 + (y * W + 4 * q) / 4) : -1;  // in float4 of the plane-0 base
+    xl[j] = c * a.RX + r * a.PX + 2 + 4 * q;
+  }
+#pragma unroll
+  for (int j = 0; j < NGL; ++j) {
+    const int i = tid + 256 * j;
+    const int q = i % W4v, t = i / W4v, yy = t % YB, m = t / YB;
+    const int y = y0 + yy;
+    const bool ok = m < mv && y < H;
+    gg[j] = ok ? (int)(((int64_t)m * D) * plane / 4 + (y * W + 4 * q) / 4) : -1;
+    gl[j] = m * a.MS + yy * W4 + 4 * q;
+  }
+  float4 rx[NXL], rg[NGL];
+  const int64_t plane4 = plane / 4;
+  auto load_x = [&](int zi) {
+    const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)zi * plane4;
+#pragma unroll
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      rx[j] = xg[j] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
     }
   };
-  auto stage_x = [&](int zi, int slot) {  // zi in [0, D)
+  auto store_x = [&](int slot) {
     float* d = xsl + slot * XS;
-    for (int row = wave; row < 16 * NXR; row += 4) {
-      const int c = row / NXR, r = row - c * NXR, y = y0 - 1 + r;
-      if (c < cv && y >= 0 && y < H) dma_row(Xb + ((int64_t)c * D + zi) * plane + (int64_t)y * W, d + c * a.RX + r * a.PX + 2);
-    }
-  };
-  auto stage_g = [&](int pz, int slot) {  // G plane pz; zero outside [0, D)
-    float* d = gsl + slot * GS;
-    const bool in = pz >= 0 && pz < D;
-    for (int row = wave; row < 16 * YB; row += 4) {
-      const int m = row / YB, yy = row - m * YB, y = y0 + yy;
-      if (m >= mv || y >= H) continue;
-      float* dr = d + m * a.MS + yy * W4;
-      if (in) {
-        dma_row(Gb + ((int64_t)m * D + pz) * plane + (int64_t)y * W, dr);
-      } else {
 #pragma unroll
-        for (int sg = 0; sg < NSEG; ++sg) {
-          const int xx = lane + 64 * sg;
-          if (xx < W) dr[xx] = 0.f;
-        }
+    for (int j = 0; j < NXL; ++j)
+      if (xg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + xl[j]);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
       }
+  };
+  auto load_g = [&](int pz) {  // G plane pz (zero outside [0, D))
+    const bool in = pz >= 0 && pz < D;
+    const float4* src = reinterpret_cast<const float4*>(Gb) + (int64_t)(in ? pz : 0) * plane4;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = src[gg[j] < 0 ? 0 : gg[j]];
+      rg[j] = (in && gg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  __syncthreads();  // the zero fill is done before any slab lands
-  // prologue: G planes z0 - 1, z0, z0 + 1 and X[z0]
-  stage_g(z0 - 1, (z0 + 3) & 3);
-  stage_g(z0, z0 & 3);
-  stage_g(z0 + 1, (z0 + 1) & 3);
-  stage_x(z0, z0 & 1);
-  __syncthreads();  // (drains the DMA)
+  auto store_g = [&](int slot) {
+    float* d = gsl + slot * GS;
+#pragma unroll
+    for (int j = 0; j < NGL; ++j)
+      if (gg[j] >= 0) {
+        float2* p = reinterpret_cast<float2*>(d + gl[j]);
+        p[0] = make_float2(rg[j].x, rg[j].y);
+        p[1] = make_float2(rg[j].z, rg[j].w);
+      }
+  };
+  __syncthreads();  // the zero fill is done before any slab store
+  // prologue: G planes z0 - 1 and z0 into their ring slots, then X[z0] and G[z0 + 1] in registers
+  load_g(z0 - 1);
+  store_g((z0 + 3) & 3);
+  load_g(z0);
+  store_g(z0 & 3);
+  load_x(z0);
+  load_g(z0 + 1);
 
   const int li = lane & 15, lk = lane >> 4;
   const int aoff = li * a.MS + lk;                 // A: G[m = li][yy][x0 + lk]
@@ -388,9 +414,12 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
 #pragma unroll
   for (int j = 0; j < 27; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int zi = z0; zi < z1; ++zi) {
-    if (zi + 1 < z1) {  // next step's slabs fly during this step's MFMAs (over X[zi - 1], G[zi - 2])
-      stage_x(zi + 1, (zi + 1) & 1);
-      stage_g(zi + 2, (zi + 2) & 3);
+    store_x(zi & 1);
+    store_g((zi + 1) & 3);
+    __syncthreads();  // slabs of this step visible; every wave is past the step that last read these slots
+    if (zi + 1 < z1) {  // next step's slabs fly during this step's MFMAs
+      load_x(zi + 1);
+      load_g(zi + 2);
     }
     const float* g0 = gsl + ((zi + 1) & 3) * GS + aoff;  // tz = 0: plane zi + 1
     const float* g1 = gsl + (zi & 3) * GS + aoff;        // tz = 1: plane zi
@@ -429,9 +458,9 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
       }
       if (k < ke) mm(a0, b0);
     }
-    __syncthreads();  // next step's slabs landed (vmcnt(0)); every wave is done with this step's slots
   }
-  // the waves' sums meet in LDS (the ring is free after the last barrier), one atomic per entry
+  // the waves' sums meet in LDS (the ring is free after this barrier), one atomic per entry
+  __syncthreads();
   float* red = smem;  // [27][4 waves][4 rr][64 lanes]
 #pragma unroll
   for (int j = 0; j < 27; ++j)
@@ -511,27 +540,30 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   const int64_t iplane4 = iplane / 4, oplane4 = oplane / 4;
   float4 rx0[NXL], rx1[NXL], rg[NGL];
   auto load_x = [&](int zi, float4 (&rx)[NXL]) {  // input plane zi (zero outside [0, Di))
-    const bool in = zi >= 0 && zi < Di;  // (zeroed at the store: a select here waits for the load)
+    const bool in = zi >= 0 && zi < Di;
     const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(in ? zi : 0) * iplane4;
 #pragma unroll
-    for (int j = 0; j < NXL; ++j) rx[j] = src[xg[j] < 0 ? 0 : xg[j]];
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      rx[j] = (in && xg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   auto store_x = [&](int zi, const float4 (&rx)[NXL]) {
     float* d = xsl + ((zi + 5) % 5) * XS;
-    const bool in = zi >= 0 && zi < Di;
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
-        const float4 v = in ? rx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         float2* p = reinterpret_cast<float2*>(d + xl[j]);
-        p[0] = make_float2(v.x, v.y);
-        p[1] = make_float2(v.z, v.w);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
       }
   };
-  auto load_g = [&](int z) {  // rows outside are never stored
+  auto load_g = [&](int z) {
 #pragma unroll
-    for (int j = 0; j < NGL; ++j)
-      rg[j] = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
+      rg[j] = gg[j] >= 0 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   auto store_g = [&](int z) {
     float* d = gsl + (z & 1) * GS;
@@ -688,27 +720,30 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
   const int64_t iplane4 = iplane / 4, oplane4 = oplane / 4;
   float4 rx0[NXL], rx1[NXL], rg[NGL];
   auto load_x = [&](int zi, float4 (&rx)[NXL]) {
-    const bool in = zi >= 0 && zi < Di;  // (zeroed at the store: a select here waits for the load)
+    const bool in = zi >= 0 && zi < Di;
     const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(in ? zi : 0) * iplane4;
 #pragma unroll
-    for (int j = 0; j < NXL; ++j) rx[j] = src[xg[j] < 0 ? 0 : xg[j]];
+    for (int j = 0; j < NXL; ++j) {
+      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
+      rx[j] = (in && xg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   auto store_x = [&](int zi, const float4 (&rx)[NXL]) {
     float* d = xsl + ((zi + 5) % 5) * XS;
-    const bool in = zi >= 0 && zi < Di;
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
-        const float4 v = in ? rx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         float2* p = reinterpret_cast<float2*>(d + xl[j]);
-        p[0] = make_float2(v.x, v.y);
-        p[1] = make_float2(v.z, v.w);
+        p[0] = make_float2(rx[j].x, rx[j].y);
+        p[1] = make_float2(rx[j].z, rx[j].w);
       }
   };
-  auto load_g = [&](int z) {  // rows outside are never stored
+  auto load_g = [&](int z) {
 #pragma unroll
-    for (int j = 0; j < NGL; ++j)
-      rg[j] = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
+    for (int j = 0; j < NGL; ++j) {
+      const float4 v = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
+      rg[j] = gg[j] >= 0 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   auto store_g = [&](int z) {
     float* d = gsl + (z & 1) * GS;
