@@ -242,6 +242,10 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
  * dconv(dZ) + dY in one sweep. */
 int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D,
                             int H, int Wd, void* stream);
+/* The layer's input gradient dX = conv(dY, W') (+ add) with W' = W[c][m][26 - t] read in the kernel from the
+ * layer's own weight W [16][16][3][3][3] (no flipped copy); gy, add, dx [N][16][D][H][W]. */
+int tb_conv3d_fwd16_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int D, int H, int Wd,
+                              void* stream);
 
 /* ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward on the f32 matrix cores
  * (sub-pixel form, all 27 taps real): x [N][64][Di][Hi][Wi] -> y [N][16][2Di][2Hi][2Wi], weight
@@ -265,6 +269,10 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
 /* ... with `add` (y's layout or NULL) summed into y (as tb_conv3d_fwd16_add_f32). */
 int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C,
                            int D, int H, int Wd, void* stream);
+/* The layer's input gradient with the flipped, transposed weight read in the kernel from W [C][C][3][3][3]
+ * (as tb_conv3d_fwd16_dgrad_f32). */
+int tb_conv3d_mfma_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int C, int D, int H,
+                             int Wd, void* stream);
 
 /*
  * The U-Net's channel-deep convolutions as implicit GEMMs on the f32 matrix cores (csrc/conv_gemm.hip;

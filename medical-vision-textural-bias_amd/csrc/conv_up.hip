@@ -414,6 +414,7 @@ struct F16Args {
   int D, H, Wd;
   int ZS, zlen, nyb;
   int PX, RX;  // row pitch (data at column x + 4), channel pitch (= 16 mod 32)
+  int flip;    // 1: W is the layer's weight and the call its input gradient: A = W[c][m][26 - t]
 };
 
 template <int YB, int NXT, int NTH, bool ADD = false>  // output rows per block; 16-column tiles per row (W = 16
@@ -436,7 +437,10 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
   const int li = lane & 15, ks = lane >> 4;
   float af[108];
 #pragma unroll
-  for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[(li * 16 + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
+  for (int kk = 0; kk < 108; ++kk) {
+    const int c = 4 * (kk & 3) + ks, t = kk >> 2;
+    af[kk] = a.flip ? a.W[(c * 16 + li) * 27 + 26 - t] : a.W[(li * 16 + c) * 27 + t];
+  }
   const int64_t plane = (int64_t)H * Wd, plane4 = plane / 4;
   const float4* xb = reinterpret_cast<const float4*>(a.x + (int64_t)n * 16 * D * plane);
   constexpr int NL = (16 * NR * W4 + NTH - 1) / NTH;
@@ -891,13 +895,26 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
   return tb_conv3d_fwd16_add_f32(x, W, bias, nullptr, y, N, D, H, Wd, stream);
 }
 
+static int fwd16_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
+                      int Wd, int flip, void* stream);
+
 int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D,
                             int H, int Wd, void* stream) {
+  return fwd16_call(x, W, bias, add, y, N, D, H, Wd, 0, stream);
+}
+
+int tb_conv3d_fwd16_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int D, int H, int Wd,
+                              void* stream) {
+  return fwd16_call(gy, W, nullptr, add, dx, N, D, H, Wd, 1, stream);
+}
+
+static int fwd16_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
+                      int Wd, int flip, void* stream) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
-  if (conv_x3_on() && Wd <= 112)
+  if (conv_x3_on() && Wd <= 112 && !flip)
     return launch_conv16_x3(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
-  if (conv16_dma_on()) {
+  if (conv16_dma_on() && !flip) {
     const int rc = launch_fwd16_dma(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
     if (rc != TB_ERR_UNSUPPORTED_SIZE) return rc;
   }
@@ -912,6 +929,7 @@ int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, c
   const int YB = YBv;
   F16Args a{};
   a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.flip = flip;
   a.PX = Wd + 8;
   a.RX = (YB + 2) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;
@@ -1161,6 +1179,7 @@ struct S1Args {
   int D, H, Wd, YB;
   int ZS, zlen, nyb, MG;  // z segments, row blocks, output-tile groups
   int PX, RX;             // row pitch (data at column x + 4), channel pitch (16 mod 32)
+  int flip;               // 1: W is the layer's weight and the call its input gradient (W[c][m][26 - t])
 };
 
 template <int G, int NC, int NL, int NTH, bool ADD = false>  // NTH 512: two waves per role, alternate tiles
@@ -1188,7 +1207,10 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
   const int m0 = (mg * MTB + mt) * 16;
   float af[108];
 #pragma unroll
-  for (int kk = 0; kk < 108; ++kk) af[kk] = a.W[((m0 + li) * CIN + 16 * g + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
+  for (int kk = 0; kk < 108; ++kk) {
+    const int c = 16 * g + 4 * (kk & 3) + ks, t = kk >> 2;
+    af[kk] = a.flip ? a.W[(c * CIN + m0 + li) * 27 + 26 - t] : a.W[((m0 + li) * CIN + c) * 27 + t];
+  }
   const int64_t plane = (int64_t)H * Wd, cstride = (int64_t)D * plane;
   const float* xb = a.x + (int64_t)n * CIN * cstride;
   const int W4 = Wd >> 2, per_c = NR * W4, total = CIN * per_c;
@@ -1296,8 +1318,21 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
   return tb_conv3d_mfma_add_f32(x, W, bias, nullptr, y, N, C, D, H, Wd, stream);
 }
 
+static int mfma_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C, int D,
+                     int H, int Wd, int flip, void* stream);
+
 int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C,
                            int D, int H, int Wd, void* stream) {
+  return mfma_call(x, W, bias, add, y, N, C, D, H, Wd, 0, stream);
+}
+
+int tb_conv3d_mfma_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int C, int D, int H,
+                             int Wd, void* stream) {
+  return mfma_call(gy, W, nullptr, add, dx, N, C, D, H, Wd, 1, stream);
+}
+
+static int mfma_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C, int D,
+                     int H, int Wd, int flip, void* stream) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if ((C != 32 && C != 64) || Wd % 4 != 0 || Wd > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
@@ -1311,6 +1346,7 @@ int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, co
   const int G = C / 16;
   S1Args a{};
   a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
+  a.flip = flip;
   a.PX = Wd + 8;
   a.MG = G == 2 ? 1 : 4;  // 32: both output tiles in the block; 64: one tile per block, 4 block groups
   size_t lds = 0;

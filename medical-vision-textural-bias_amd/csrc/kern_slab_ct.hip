@@ -559,13 +559,19 @@ bool slab_half_supported(int W, int D) {
   return false;
 }
 
-// TEXBIAS_HALF_CFG (tuning): 2 = 512 threads unfused (default; gibbs-aug C3 chain 0.471 ms), 0 = 256
-// threads with the fused DU / RE phase (0.542), 1 = 256 threads unfused (0.551), 3 = 768 threads unfused
+// TEXBIAS_HALF_CFG / TEXBIAS_HALF_CFG_INV (tuning, passes A / C): 0 = 256 threads with the fused DU / RE
+// phase, 1 = 256 threads unfused, 2 = 512 threads unfused, 3 = 768 threads unfused.  Measured on the
+// gibbs-aug C3 chain (A / C us): 0: 220 / 207, 1: 224 / 211, 2: 184 / 167, 3: 224 / 151 -> A 2, C 3.
+static int half_cfg_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
 static int half_cfg() {
-  static const int c = [] {
-    const char* e = std::getenv("TEXBIAS_HALF_CFG");
-    return e ? std::atoi(e) : 2;
-  }();
+  static const int c = half_cfg_env("TEXBIAS_HALF_CFG", 2);
+  return c;
+}
+static int half_cfg_inv() {
+  static const int c = half_cfg_env("TEXBIAS_HALF_CFG_INV", std::getenv("TEXBIAS_HALF_CFG") ? half_cfg() : 3);
   return c;
 }
 
@@ -597,9 +603,9 @@ hipError_t launch_slab_inv_half(const SlabInvArgs& a, hipStream_t st) {
 #define TB_X(w, d)                                                                                   \
   if (a.pl.W == w && a.pl.D == d) {                                                                  \
     constexpr size_t lds = ct::HalfPlan<w, d>::LDS_BYTES;                                            \
-    if (half_cfg() == 3) return launch_half(k_slab_inv_half<w, d, 768, false>, 768, lds, units, a, st); \
-    if (half_cfg() == 2) return launch_half(k_slab_inv_half<w, d, 512, false>, 512, lds, units, a, st); \
-    if (half_cfg() == 1) return launch_half(k_slab_inv_half<w, d, 256, false>, 256, lds, units, a, st); \
+    if (half_cfg_inv() == 3) return launch_half(k_slab_inv_half<w, d, 768, false>, 768, lds, units, a, st); \
+    if (half_cfg_inv() == 2) return launch_half(k_slab_inv_half<w, d, 512, false>, 512, lds, units, a, st); \
+    if (half_cfg_inv() == 1) return launch_half(k_slab_inv_half<w, d, 256, false>, 256, lds, units, a, st); \
     return launch_half(k_slab_inv_half<w, d, 256, true>, 256, lds, units, a, st);                    \
   }
   TB_CT_HALF_SHAPES(TB_X)

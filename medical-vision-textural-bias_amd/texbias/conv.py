@@ -121,6 +121,8 @@ GEMM = os.environ.get("TEXBIAS_CONVGEMM", "1") != "0"
 # measured slower than MIOpen at the C3 shapes (scripts/diag/gemm_conv_bench.py): off unless asked for
 GEMM_T = os.environ.get("TEXBIAS_CONVGEMM_T", "0") != "0"
 GEMM_1 = os.environ.get("TEXBIAS_CONVGEMM_1X1", "0") != "0"
+# ConvTranspose3d input gradient (a stride-2 Conv3d of dY) on the GEMM kernel while its forward stays on MIOpen
+GEMM_TDX = os.environ.get("TEXBIAS_CONVGEMM_TDX", "1") != "0"
 
 
 def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:
@@ -296,6 +298,18 @@ def conv_fwd16(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
     return y
 
 
+def conv_fwd16_dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """The input gradient of Conv3d(16 -> 16, 3, 1, 1) with weight ``w``: the forward kernel reading
+    W[c][m][26 - t] in place of a flipped, transposed copy (tb_conv3d_fwd16_dgrad_f32)."""
+    gy = gy.contiguous()
+    N, _, D, H, W = gy.shape
+    dx = torch.empty_like(gy)
+    with torch.cuda.device(gy.device):
+        check(lib().tb_conv3d_fwd16_dgrad_f32(gy.data_ptr(), w.contiguous().data_ptr(), None, dx.data_ptr(),
+                                              N, D, H, W, _stream(gy)), "tb_conv3d_fwd16_dgrad_f32")
+    return dx
+
+
 def conv16_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     """Conv3d(16 -> 16, 3, stride 1, padding 1), rows of 16k <= 128 floats: k_conv3d_fwd16 (forward and
     input gradient) + the z-marching weight gradient."""
@@ -315,6 +329,18 @@ def conv_mfma(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
                                            b.data_ptr() if b is not None else None, _add_ptr(add, y.shape),
                                            y.data_ptr(), N, C, D, H, W, _stream(x)), "tb_conv3d_mfma_add_f32")
     return y
+
+
+def conv_mfma_dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """The input gradient of Conv3d(C -> C, 3, 1, 1), C = 32 / 64, reading the flipped weight in the
+    kernel (tb_conv3d_mfma_dgrad_f32)."""
+    gy = gy.contiguous()
+    N, C, D, H, W = gy.shape
+    dx = torch.empty_like(gy)
+    with torch.cuda.device(gy.device):
+        check(lib().tb_conv3d_mfma_dgrad_f32(gy.data_ptr(), w.contiguous().data_ptr(), None, dx.data_ptr(),
+                                             N, C, D, H, W, _stream(gy)), "tb_conv3d_mfma_dgrad_f32")
+    return dx
 
 
 def conv_mfma_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
@@ -418,7 +444,7 @@ class Route:
                     and CONVT64 and x.shape[-1] % 8 == 0 and x.shape[-1] // 2 <= 64 and \
                     all(n % 2 == 0 for n in x.shape[2:]):
                 self.dx = "convT64"   # Conv3d(16 -> 32 / 64 stacked, s2)'s input gradient on k_convT_mfma64
-            elif self.kind != "aten" and _gemm_geom_ok(x, w, st, pd, transposed, op) and \
+            elif (self.kind != "aten" or (transposed and GEMM_TDX)) and _gemm_geom_ok(x, w, st, pd, transposed, op) and \
                     (w.shape[1] % 8 == 0 if transposed else w.shape[0] % 8 == 0) and \
                     (transposed or st[0] == 1 or (GEMM_T and all(n % 2 == 0 for n in x.shape[2:]))):
                 # ConvTranspose3d: a stride-2 Conv3d of dY (the GEMM's conv form); stride-1 Conv3d: the
@@ -475,9 +501,9 @@ class Route:
                 return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2], add=add)
             return self.input_grad(gy, x, w).add_(add)
         if k == "fwd16":
-            return conv_fwd16(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+            return conv_fwd16_dgrad(gy, w)
         if k == "mfma":
-            return conv_mfma(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
+            return conv_mfma_dgrad(gy, w)
         if k == "small":
             return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None)
         if k == "fewout":   # dX[m][i] = sum_{c, t} W[m][c][t] dY[c][2 i + t - 1]

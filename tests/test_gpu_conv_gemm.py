@@ -170,3 +170,25 @@ def test_residual_add_epilogues(conv, kind, c, sp):
     gxr = torch.ops.aten.convolution_backward(g, x, w, None, [1] * 3, [1] * 3, [1] * 3, False, [0] * 3, 1,
                                               [True, False, False])[0] + g
     assert (gx - gxr).abs().max().item() <= 2e-5 * gxr.abs().max().item()
+
+
+@pytest.mark.parametrize("cin,cout,shape", [(128, 32, (1, 6, 4, 6)), (128, 32, (2, 30, 30, 20)), (64, 16, (2, 3, 5, 4))])
+def test_convT_input_grad_route(conv, cin, cout, shape):
+    """ConvTranspose3d whose forward stays on MIOpen (the sub-pixel GEMM form is off by default): its input
+    gradient still runs on the GEMM kernel as a stride-2 Conv3d of dY (Route.dx "gemm"), vs ATen and float64;
+    the C3 up2 shape (128 -> 32 at 30 x 30 x 20) included."""
+    torch.manual_seed(7)
+    x = torch.randn((shape[0], cin) + shape[1:], device="cuda", requires_grad=True)
+    m = conv.ConvTranspose3d(cin, cout, 3, stride=2, padding=1, output_padding=1).cuda()
+    r = conv.Route(x, m.weight, m.stride, m.padding, m.output_padding, True)
+    assert r.dx == "gemm"
+    y = m(x)
+    g = torch.randn_like(y)
+    gx, = torch.autograd.grad(y, (x,), g)
+    x64 = x.detach().double().requires_grad_(True)
+    y64 = F.conv_transpose3d(x64, m.weight.detach().double(), m.bias.detach().double(), stride=2, padding=1,
+                             output_padding=1)
+    gx64, = torch.autograd.grad(y64, (x64,), g.double())
+    gxr = torch.ops.aten.convolution_backward(g, x.detach(), m.weight.detach(), None, [2] * 3, [1] * 3, [1] * 3, True,
+                                              [1] * 3, 1, [True, False, False])[0]
+    close64(gx, gxr, gx64)
