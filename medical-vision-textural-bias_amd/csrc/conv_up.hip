@@ -452,7 +452,11 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
     const int yi = y0 - 1 + r;
     const bool ok = i < 16 * NR * W4 && yi >= 0 && yi < H;
     gof[j] = ok ? (int)((int64_t)c * D * plane4 + ((int64_t)yi * Wd + 4 * q) / 4) : -1;
-    lof[j] = c * RX + r * PX + 4 + 4 * q;
+    // rows outside the volume store zeros over their (zero) staging rows; slots past the staged block
+    // store zeros over the first four pad columns -- every lane stores, so that no path skips the wait for
+    // the plane loads (a skippable wait makes the compiler wait again, for the output stores too, before
+    // the next plane's loads reuse the registers)
+    lof[j] = i < 16 * NR * W4 ? c * RX + r * PX + 4 + 4 * q : 0;
   }
   float4 rg[NL];
   auto load = [&](int zi) {
@@ -468,30 +472,42 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
     const bool in = zi >= 0 && zi < D;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (gof[j] >= 0) *reinterpret_cast<float4*>(d + lof[j]) = in ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(d + lof[j]) = in && gof[j] >= 0 ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
+  const float bm[4] = {a.bias ? a.bias[4 * ks] : 0.f, a.bias ? a.bias[4 * ks + 1] : 0.f,
+                       a.bias ? a.bias[4 * ks + 2] : 0.f, a.bias ? a.bias[4 * ks + 3] : 0.f};
   __syncthreads();
   load(z0 - 1);
   store(z0 - 1);
   load(z0);
   store(z0);
   load(z0 + 1);
-  const float bm[4] = {a.bias ? a.bias[4 * ks] : 0.f, a.bias ? a.bias[4 * ks + 1] : 0.f,
-                       a.bias ? a.bias[4 * ks + 2] : 0.f, a.bias ? a.bias[4 * ks + 3] : 0.f};
+  store(z0 + 1);
+  // every start-up load (A fragments, bias, the first planes) retired here, so that the compiler does not
+  // wait for the loop's plane loads (vmcnt(0)) before a step's first MFMA
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
   // B lane base: channel 4 cq + ks (cq added per k-step), column x = li of the tile (+ tx - 1 at + 4)
   const int bl = ks * RX + li + 3;
   const int64_t oplane = plane;
   float* yb0 = a.y + (int64_t)n * 16 * D * oplane;
   const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * oplane : nullptr;
-  constexpr int NT = YB * NXT;  // tiles per step
+  constexpr int NT = YB * NXT;                        // tiles per step
+  constexpr int NIT = (NT + 2 * NWV - 1) / (2 * NWV);  // tile pairs per wave
+  // step z: fetch plane z + 2 (registers) | MFMAs over planes z - 1 .. z + 1 | barrier | plane z + 2 into
+  // the slot plane z - 1 held | the step's output stores | barrier.  The output stores come after the
+  // plane's LDS store, so the wait for the plane loads never includes an output store's write-back.
   for (int z = z0; z < z1; ++z) {
-    store(z + 1);
-    __syncthreads();
-    if (z + 1 < z1) load(z + 2);
+    const bool more = z + 1 < z1;
+    if (more) load(z + 2);
     const float* s0 = ring + ((z + 2) % 3) * SS + bl;  // tz = 0: plane z - 1
     const float* s1 = ring + (z % 3) * SS + bl;
     const float* s2 = ring + ((z + 1) % 3) * SS + bl;
-    for (int t0 = wave; t0 < NT; t0 += 2 * NWV) {  // tiles t0 and t0 + NWV of this wave
+    f32x4 acc[NIT][2];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {  // tiles t0 and t0 + NWV of this wave
+      const int t0 = wave + 2 * NWV * it;
+      if (t0 >= NT) break;
       const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
       const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
       const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
@@ -514,14 +530,24 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
             }
           }
       }
-      // C: column x = li, rows m = 4 ks + r
+      acc[it][0] = acc0, acc[it][1] = acc1;
+    }
+    __syncthreads();
+    store(z + 2);  // unconditionally (after the last step a dead slot): no path skips the loads' wait
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {  // C: column x = li, rows m = 4 ks + r
+      const int t0 = wave + 2 * NWV * it;
+      if (t0 >= NT) break;
+      const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
+      const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
+      const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 4 * ks + r;
         const int64_t o0 = ((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy0) * Wd + x00 + li;
         const int64_t o1 = ((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy1) * Wd + x01 + li;
-        if (y0 + yy0 < H) yb0[o0] = ADD ? acc0[r] + ab0[o0] : acc0[r];
-        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc1[r] + ab0[o1] : acc1[r];
+        if (y0 + yy0 < H) yb0[o0] = ADD ? acc[it][0][r] + ab0[o0] : acc[it][0][r];
+        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc[it][1][r] + ab0[o1] : acc[it][1][r];
       }
     }
     __syncthreads();
@@ -1016,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
   const int64_t plane = (int64_t)Hi * Wi;
   const float* xb = a.x + (int64_t)n * CIN * Di * plane;
   // staging: float4 pieces of (channel, row, column quad); Wi % 4 == 0.  gof: offset in the
-  // channel-plane's floats (-1: a row past Hi, staged as zeros), lof: LDS offset (-1: no piece)
+  // channel-plane's floats (-1: a row past Hi, staged as zeros), lof: LDS offset
   const int W4 = Wi >> 2, per_c = NR * W4, total = CIN * per_c;
   const int64_t cstride = (int64_t)Di * plane;
   int gof[NL], lof[NL], gch[NL];
@@ -1025,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
     const int i = tid + 256 * j;
     const int c = i / per_c, r2 = i - c * per_c, r = r2 / W4, q = r2 - r * W4;
     const int yi = y0 + r;
-    lof[j] = i < total ? c * RX + r * PX + 4 * q : -1;
+    lof[j] = i < total ? c * RX + r * PX + 4 * q : Wi;  // past the block: zeros over row 0's pad columns
     gof[j] = (i < total && yi < Hi) ? yi * Wi + 4 * q : -1;
     gch[j] = i < total ? c : 0;
   }
@@ -1039,28 +1065,54 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
       rg[j] = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
     }
   };
-  auto store = [&](int zi) {
+  auto store = [&](int zi) {  // every lane stores (see k_conv3d_fwd16: no path skips the loads' wait)
     float* d = ring + (zi & 1) * SS;
     const bool in = zi < Di;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (lof[j] >= 0)
-        *reinterpret_cast<float4*>(d + lof[j]) = (in && gof[j] >= 0) ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(d + lof[j]) = (in && gof[j] >= 0) ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
+  float bm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bm[r] = a.bias ? a.bias[4 * ks + r] : 0.f;
   __syncthreads();
   load(z0);
   store(z0);
   load(z0 + 1);
+  store(z0 + 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // start-up loads retired (as in k_conv3d_fwd16)
+  __syncthreads();
   const int npos = YB * Wi, ntile = (npos + 15) / 16;
-  float bm[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bm[r] = a.bias ? a.bias[4 * ks + r] : 0.f;
   const int64_t oplane = 4 * plane, orow = 2 * Wi;
   float* yb0 = a.y + (int64_t)n * 16 * (2 * Di) * oplane;
+  // (tile phase h', parity pair (pz, py, 0 / 1)) combos over the waves: the G groups' partials summed
+  auto sums = [&](int z, int t0, int pb) {
+    const float* pr = part + pb * 4 * 8 * 256;
+    for (int k = w; k < 4 * HT; k += 4) {
+      const int hq = k >> 2, pz = (k >> 1) & 1, py = k & 1, q0 = pz * 4 + py * 2;
+      const int pq = 16 * (t0 + hq) + li, yq = pq / Wi, xq = pq - yq * Wi;
+      const bool okp = t0 + hq < ntile && pq < npos && y0 + yq < Hi;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * ks + r, e = m * 16 + li;
+        float v0 = bm[r], v1 = bm[r];
+#pragma unroll
+        for (int v = 0; v < G; ++v) {
+          v0 += pr[((hq * G + v) * 8 + q0) * 256 + e];
+          v1 += pr[((hq * G + v) * 8 + q0 + 1) * 256 + e];
+        }
+        if (okp)
+          *reinterpret_cast<float2*>(yb0 + ((int64_t)m * (2 * Di) + 2 * z + pz) * oplane +
+                                     (int64_t)(2 * (y0 + yq) + py) * orow + 2 * xq) = make_float2(v0, v1);
+      }
+    }
+  };
   int buf = 0;
+  // step z: fetch plane z + 2 | per tile: MFMAs, partials, barrier, the previous tile's sums and stores |
+  // plane z + 2 over plane z's slot | the last tile's sums and stores | barrier.  The plane's LDS store
+  // waits for its loads and the stores of all but the last tile (issued a tile earlier), never for the
+  // stores just issued.
   for (int z = z0; z < z1; ++z) {
-    store(z + 1);  // slot (z + 1) & 1 last held plane z - 1, read before the previous step's last barrier
-    __syncthreads();
     if (z + 1 < z1) load(z + 2);
     const float* sz[2] = {ring + (z & 1) * SS, ring + ((z + 1) & 1) * SS};
     for (int t0 = 0; t0 < ntile; t0 += HT) {
@@ -1091,28 +1143,11 @@ __global__ __launch_bounds__(256) void k_convT_mfma64(T64Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) pw[q * 256 + (4 * ks + r) * 16 + li] = acc[q][r];
       __syncthreads();
-      // (tile phase h', parity pair (pz, py, 0 / 1)) combos over the waves: the G groups' partials summed
-      const float* pr = part + buf * 4 * 8 * 256;
-      for (int k = w; k < 4 * HT; k += 4) {
-        const int hq = k >> 2, pz = (k >> 1) & 1, py = k & 1, q0 = pz * 4 + py * 2;
-        const int pq = 16 * (t0 + hq) + li, yq = pq / Wi, xq = pq - yq * Wi;
-        const bool okp = t0 + hq < ntile && pq < npos && y0 + yq < Hi;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 4 * ks + r, e = m * 16 + li;
-          float v0 = bm[r], v1 = bm[r];
-#pragma unroll
-          for (int v = 0; v < G; ++v) {
-            v0 += pr[((hq * G + v) * 8 + q0) * 256 + e];
-            v1 += pr[((hq * G + v) * 8 + q0 + 1) * 256 + e];
-          }
-          if (okp)
-            *reinterpret_cast<float2*>(yb0 + ((int64_t)m * (2 * Di) + 2 * z + pz) * oplane +
-                                       (int64_t)(2 * (y0 + yq) + py) * orow + 2 * xq) = make_float2(v0, v1);
-        }
-      }
+      if (t0 > 0) sums(z, t0 - HT, buf ^ 1);
       buf ^= 1;
     }
+    store(z + 2);  // slot (z + 2) & 1 = plane z's, read by no wave after the last tile's barrier; unconditional
+    sums(z, ((ntile - 1) / HT) * HT, buf ^ 1);
     __syncthreads();
   }
 }
@@ -1193,6 +1228,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
   const int NR = YB + 2;
   float* ring = smem;            // [3][CIN][NR rows][PX]
   float* part = smem + 3 * SS;   // [NTH / 64 waves][NC][16 m][16 pos]
+  float* bsm = part + (NTH / 64) * NC * 256;  // the block's bias values [MTB * 16] (no global load in the loop)
   for (int i = tid; i < 3 * SS; i += NTH) ring[i] = 0.f;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
@@ -1205,6 +1241,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
   const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
   const int li = lane & 15, ks = lane >> 4;
   const int m0 = (mg * MTB + mt) * 16;
+  if (tid < MTB * 16) bsm[tid] = a.bias ? a.bias[mg * MTB * 16 + tid] : 0.f;
   float af[108];
 #pragma unroll
   for (int kk = 0; kk < 108; ++kk) {
@@ -1220,7 +1257,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
     const int i = tid + NTH * j;
     const int c = i / per_c, r2 = i - c * per_c, r = r2 / W4, q = r2 - r * W4;
     const int yi = y0 - 1 + r;
-    lof[j] = i < total ? c * RX + r * PX + 4 + 4 * q : -1;
+    lof[j] = i < total ? c * RX + r * PX + 4 + 4 * q : 0;  // past the block: zeros over pad columns 0..3
     gof[j] = (i < total && yi >= 0 && yi < H) ? yi * Wd + 4 * q : -1;
     gch[j] = i < total ? c : 0;
   }
@@ -1234,13 +1271,12 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
       rg[j] = *reinterpret_cast<const float4*>(src + gch[j] * cstride + (ok ? gof[j] : 0));
     }
   };
-  auto store = [&](int zi) {
+  auto store = [&](int zi) {  // every lane stores (see k_conv3d_fwd16: no path skips the loads' wait)
     float* d = ring + ((zi + 3) % 3) * SS;
     const bool in = zi >= 0 && zi < D;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
-      if (lof[j] >= 0)
-        *reinterpret_cast<float4*>(d + lof[j]) = (in && gof[j] >= 0) ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(d + lof[j]) = (in && gof[j] >= 0) ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   __syncthreads();
   load(z0 - 1);
@@ -1248,65 +1284,67 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
   load(z0);
   store(z0);
   load(z0 + 1);
-  const int npos = YB * Wd, ntile = (npos + 15) / 16;
+  store(z0 + 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // start-up loads retired (as in k_conv3d_fwd16)
+  __syncthreads();
+  // the host sizes YB so that a step's positions fit the block's NWG x NC chains: one tile round per step
+  const int npos = YB * Wd;
   float* ybase = a.y + (int64_t)n * COUT * cstride;
   const float* abase = ADD ? a.add + (int64_t)n * COUT * cstride : nullptr;
+  int bl[NC];  // chain c of this wave: position tile NWG c + h
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int p = 16 * (NWG * c + h) + li, pc = p < npos ? p : npos - 1;
+    const int yy = pc / Wd, xx = pc - yy * Wd;
+    bl[c] = (16 * g + ks) * RX + yy * PX + xx + 3;
+  }
+  // step z: fetch plane z + 2 | MFMAs over planes z - 1 .. z + 1 into the group partials | barrier | plane
+  // z + 2 over plane z - 1's slot, the partials summed and stored | barrier
   for (int z = z0; z < z1; ++z) {
-    store(z + 1);  // over plane z - 2, last read before the previous step's final barrier
-    __syncthreads();
     if (z + 1 < z1) load(z + 2);
     const float* sp[3] = {ring + ((z + 2) % 3) * SS, ring + (z % 3) * SS, ring + ((z + 1) % 3) * SS};
-    for (int t0 = 0; t0 < ntile; t0 += NWG * NC) {  // chain c of this wave: tile t0 + NWG c + h
-      int bl[NC];
+    f32x4 acc[NC];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int p = 16 * (t0 + NWG * c + h) + li, pc = p < npos ? p : npos - 1;
-        const int yy = pc / Wd, xx = pc - yy * Wd;
-        bl[c] = (16 * g + ks) * RX + yy * PX + xx + 3;
-      }
-      f32x4 acc[NC];
+    for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int tz = 0; tz < 3; ++tz)
 #pragma unroll
-      for (int tz = 0; tz < 3; ++tz)
+      for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-        for (int ty = 0; ty < 3; ++ty)
+        for (int tx = 0; tx < 3; ++tx) {
+          const int t = tz * 9 + ty * 3 + tx;
+          const float* s = sp[tz] + ty * PX + tx;
 #pragma unroll
-          for (int tx = 0; tx < 3; ++tx) {
-            const int t = tz * 9 + ty * 3 + tx;
-            const float* s = sp[tz] + ty * PX + tx;
+          for (int cq = 0; cq < 4; ++cq)
 #pragma unroll
-            for (int cq = 0; cq < 4; ++cq)
-#pragma unroll
-              for (int c = 0; c < NC; ++c)
-                acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], s[bl[c] + 4 * cq * RX], acc[c], 0, 0, 0);
-          }
-      float* pw = part + w * NC * 256;
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pw[c * 256 + (4 * ks + r) * 16 + li] = acc[c][r];
-      __syncthreads();
-      // (output tile mt', phase h', chain c) combos over the waves: the G groups' partials summed + bias
-      for (int k = w; k < MTB * NWG * NC; k += NTH / 64) {
-        const int mq = k / (NWG * NC), r2 = k - mq * (NWG * NC), hq = r2 / NC, c = r2 - hq * NC;
-        const int tq = t0 + NWG * c + hq;
-        const int p = 16 * tq + li;
-        const int yy = p / Wd, xx = p - yy * Wd;
-        const bool ok = tq < ntile && p < npos && y0 + yy < H;
-        const int mb = (mg * MTB + mq) * 16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 4 * ks + r;
-          float v = a.bias ? a.bias[mb + m] : 0.f;
-#pragma unroll
-          for (int gg = 0; gg < G; ++gg) v += part[((hq * 4 + mq * G + gg) * NC + c) * 256 + m * 16 + li];
-          const int64_t o = (int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx;
-          if (ok) ybase[o] = ADD ? v + abase[o] : v;
+            for (int c = 0; c < NC; ++c)
+              acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], s[bl[c] + 4 * cq * RX], acc[c], 0, 0, 0);
         }
+    float* pw = part + w * NC * 256;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pw[c * 256 + (4 * ks + r) * 16 + li] = acc[c][r];
+    __syncthreads();
+    store(z + 2);  // unconditionally (after the last step a dead slot)
+    // (output tile mt', phase h', chain c) combos over the waves: the G groups' partials summed + bias
+    for (int k = w; k < MTB * NWG * NC; k += NTH / 64) {
+      const int mq = k / (NWG * NC), r2 = k - mq * (NWG * NC), hq = r2 / NC, c = r2 - hq * NC;
+      const int p = 16 * (NWG * c + hq) + li;
+      const int yy = p / Wd, xx = p - yy * Wd;
+      const bool ok = p < npos && y0 + yy < H;
+      const int mb = (mg * MTB + mq) * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * ks + r;
+        float v = bsm[mq * 16 + m];
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg) v += part[((hq * 4 + mq * G + gg) * NC + c) * 256 + m * 16 + li];
+        const int64_t o = (int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx;
+        if (ok) ybase[o] = ADD ? v + abase[o] : v;
       }
-      __syncthreads();
     }
+    __syncthreads();
   }
 }
 }  // namespace
@@ -1350,11 +1388,12 @@ static int mfma_call(const float* x, const float* W, const float* bias, const fl
   a.PX = Wd + 8;
   a.MG = G == 2 ? 1 : 4;  // 32: both output tiles in the block; 64: one tile per block, 4 block groups
   size_t lds = 0;
-  int YB = (16 * 5 + Wd - 1) / Wd;  // about 5 tiles of positions per step
+  // rows per step: the most whose positions fit one round of the block's NWG x NC position tiles
+  int YB = std::max(1, 16 * NC * (NTv / 256) / Wd);
   for (; YB >= 1; --YB) {
     a.RX = (YB + 2) * a.PX;
     while ((a.RX & 31) != 16) ++a.RX;
-    lds = (size_t)4 * (3 * C * a.RX + (NTv / 64) * NC * 256);
+    lds = (size_t)4 * (3 * C * a.RX + (NTv / 64) * NC * 256 + 64);
     if (lds <= 163840) break;
   }
   if (YB < 1) return TB_ERR_UNSUPPORTED_SIZE;

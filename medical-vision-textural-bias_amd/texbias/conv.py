@@ -122,7 +122,8 @@ GEMM = os.environ.get("TEXBIAS_CONVGEMM", "1") != "0"
 GEMM_T = os.environ.get("TEXBIAS_CONVGEMM_T", "0") != "0"
 GEMM_1 = os.environ.get("TEXBIAS_CONVGEMM_1X1", "0") != "0"
 # ConvTranspose3d input gradient (a stride-2 Conv3d of dY) on the GEMM kernel while its forward stays on MIOpen
-GEMM_TDX = os.environ.get("TEXBIAS_CONVGEMM_TDX", "1") != "0"
+# (off: up2 128 -> 32 at C3 measured 2 x 100 us + reduce in the step vs MIOpen/CK's 152 us)
+GEMM_TDX = os.environ.get("TEXBIAS_CONVGEMM_TDX", "0") != "0"
 
 
 def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:

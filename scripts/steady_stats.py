@@ -16,6 +16,7 @@ ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--marker", default="k_slab_fwd")
 ap.add_argument("--top", type=int, default=40)
 ap.add_argument("--per-step", type=int, default=1, help="marker launches per step")
+ap.add_argument("--calls", default=None, help="also list the last step's launches whose name matches this regex")
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -37,3 +38,16 @@ print(f"window {(t_end - t0) / 1e6:.2f} ms over {a.steps} steps; kernel busy {to
 print(f"{'ms/step':>9} {'%':>6} {'calls/step':>10} {'avg_us':>9}  kernel")
 for nm, (n, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
     print(f"{d / a.steps / 1e6:9.3f} {100 * d / tot:6.1f} {n / a.steps:10.1f} {d / n / 1e3:9.1f}  {nm}")
+
+if a.calls:
+    last = starts[-a.per_step]
+    print(f"\nlast step's launches matching {a.calls!r} (start offset us, duration us, grid, workgroup):")
+    for r in rows:
+        s = int(r["Start_Timestamp"])
+        if s < last or not re.search(a.calls, r["Kernel_Name"]):
+            continue
+        g = r.get("Grid_Size") or "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+        wg = r.get("Workgroup_Size") or "x".join(r.get(k, "?") for k in ("Workgroup_Size_X", "Workgroup_Size_Y",
+                                                                          "Workgroup_Size_Z"))
+        nm = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", ""))[:60]
+        print(f"{(s - last) / 1e3:10.1f} {(int(r['End_Timestamp']) - s) / 1e3:8.1f}  {g:>14} {wg:>8}  {nm}")
