@@ -192,6 +192,17 @@ int tb_dice_sums_f32(const float* x, const float* t, double* sums, int64_t NC, i
 int tb_dice_metric_sums_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, void* stream);
 int tb_dice_sums_bwd_f32(const float* x, const float* t, const float* g, float* dx, int64_t NC, int64_t S, int sigmoid,
                          int squared, void* stream);
+/*
+ * DiceLoss's finalize from those sums (MONAI formula of the reference's DiceLoss, stylized_gibbs12p5.py:201):
+ * f = 1 - (2 I + smooth_nr) / (G + P + smooth_dr) per instance (batch != 0: per channel, the sums added over
+ * the NC / C samples); reduction 1: loss[0] = mean f, 2: loss[0] = sum f, 0: loss[i] = f[i] (DEVICE float).
+ * The backward writes gsums [NC][3] (DEVICE float, the input of tb_dice_sums_bwd_f32) from the loss gradient
+ * gloss (DEVICE float: one value, or one per f for reduction 0).  float64 arithmetic, one launch each.
+ */
+int tb_dice_loss_f32(const double* sums, float* loss, int64_t NC, int64_t C, int batch, int reduction, float smooth_nr,
+                     float smooth_dr, void* stream);
+int tb_dice_loss_bwd_f32(const double* sums, const float* gloss, float* gsums, int64_t NC, int64_t C, int batch,
+                         int reduction, float smooth_nr, float smooth_dr, void* stream);
 
 /*
  * out[c] = sum over n < N, s < S of x[n][c][s] (x contiguous [N][C][S], device; out DEVICE float[C],

@@ -676,6 +676,54 @@ __global__ __launch_bounds__(NT) void k_adn_fin_bias(const AdnArgs a) {
   if (threadIdx.x == 0) a.dbias[c] = (float)all[0];
 }
 
+// DiceLoss finalize (MONAI's formula, the reference's DiceLoss(sigmoid, squared_pred), stylized_gibbs12p5.py:201):
+// f = 1 - (2 I + nr) / (G + P + dr) per instance -- per channel with `batch`, the sums added over the samples
+// in sample order -- then mean / sum (red 1 / 2) or f itself (red 0).  One block, float64 throughout: the
+// sigmoid / products / reductions / division chain of ~10 ATen launches forward and ~15 backward as one each.
+struct DiceFinArgs {
+  const double* sums;  // [NC][3] {I, G, P}
+  const float* gl;     // backward: the loss gradient (1 value, or one per f for red 0)
+  float* out;          // forward: loss (1 value, or M for red 0); backward: gsums [NC][3]
+  int64_t NC, C;
+  int batch, red;
+  double nr, dr;
+};
+__device__ __forceinline__ void dice_isum(const DiceFinArgs& a, int64_t i, double& I, double& G, double& P) {
+  I = G = P = 0.0;
+  const int64_t N = a.batch ? a.NC / a.C : 1;
+  for (int64_t n = 0; n < N; ++n) {
+    const double* q = a.sums + 3 * (a.batch ? n * a.C + i : i);
+    I += q[0], G += q[1], P += q[2];
+  }
+}
+__global__ __launch_bounds__(NT) void k_dice_loss(const DiceFinArgs a) {
+  const int64_t M = a.batch ? a.C : a.NC;
+  double v[1] = {0.0}, tot[1];
+  for (int64_t i = threadIdx.x; i < M; i += NT) {
+    double I, G, P;
+    dice_isum(a, i, I, G, P);
+    const double f = 1.0 - (2.0 * I + a.nr) / (G + P + a.dr);
+    if (a.red == 0) a.out[i] = (float)f;
+    v[0] += f;
+  }
+  block_sum<1>(v, tot);
+  if (a.red != 0 && threadIdx.x == 0) a.out[0] = (float)(a.red == 1 ? tot[0] / (double)M : tot[0]);
+}
+__global__ __launch_bounds__(NT) void k_dice_loss_bwd(const DiceFinArgs a) {
+  const int64_t M = a.batch ? a.C : a.NC;
+  for (int64_t nc = (int64_t)blockIdx.x * NT + threadIdx.x; nc < a.NC; nc += (int64_t)gridDim.x * NT) {
+    const int64_t i = a.batch ? nc % a.C : nc;
+    double I, G, P;
+    dice_isum(a, i, I, G, P);
+    double g = a.red == 0 ? (double)a.gl[i] : (double)a.gl[0];
+    if (a.red == 1) g /= (double)M;
+    const double den = G + P + a.dr, dgp = g * (2.0 * I + a.nr) / (den * den);
+    a.out[3 * nc] = (float)(-2.0 * g / den);
+    a.out[3 * nc + 1] = (float)dgp;
+    a.out[3 * nc + 2] = (float)dgp;
+  }
+}
+
 inline bool vec_ok(const void* a, const void* b, const void* c, int64_t S) {
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return S % 4 == 0 && al(a) && al(b) && al(c);
@@ -758,6 +806,25 @@ int tb_dice_sums_bwd_f32(const float* x, const float* t, const float* g, float* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)((S + CHUNK - 1) / CHUNK), (unsigned)NC);
   hipLaunchKernelGGL(k_dice_sums_bwd, grid, dim3(NT), 0, st, x, t, g, dx, S, (sigmoid ? 1 : 0) | (squared ? 2 : 0));
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+int tb_dice_loss_f32(const double* sums, float* loss, int64_t NC, int64_t C, int batch, int reduction, float smooth_nr,
+                     float smooth_dr, void* stream) {
+  if (!sums || !loss || NC < 1 || C < 1 || NC % C != 0 || reduction < 0 || reduction > 2) return TB_ERR_INVALID_ARG;
+  DiceFinArgs a{sums, nullptr, loss, NC, C, batch ? 1 : 0, reduction, (double)smooth_nr, (double)smooth_dr};
+  hipLaunchKernelGGL(k_dice_loss, dim3(1), dim3(NT), 0, reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+int tb_dice_loss_bwd_f32(const double* sums, const float* gloss, float* gsums, int64_t NC, int64_t C, int batch,
+                         int reduction, float smooth_nr, float smooth_dr, void* stream) {
+  if (!sums || !gloss || !gsums || NC < 1 || C < 1 || NC % C != 0 || reduction < 0 || reduction > 2)
+    return TB_ERR_INVALID_ARG;
+  DiceFinArgs a{sums, gloss, gsums, NC, C, batch ? 1 : 0, reduction, (double)smooth_nr, (double)smooth_dr};
+  const int64_t nb = (NC + NT - 1) / NT;
+  hipLaunchKernelGGL(k_dice_loss_bwd, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(NT), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 

@@ -68,6 +68,8 @@ def _proto(L):
         "tb_dice_sums_f32": (I, [P, P, P, I64, I64, I, I, P]),
         "tb_dice_sums_bwd_f32": (I, [P, P, P, P, I64, I64, I, I, P]),
         "tb_dice_metric_sums_f32": (I, [P, P, P, I64, I64, P]),
+        "tb_dice_loss_f32": (I, [P, P, I64, I64, I, I, F, F, P]),
+        "tb_dice_loss_bwd_f32": (I, [P, P, P, I64, I64, I, I, F, F, P]),
         "tb_set_compiled_plans": (I, [I]),
         "tb_set_chain_chunk": (I, [I]),
         "tb_set_pass_timing": (I, [I]),
