@@ -417,16 +417,20 @@ struct F16Args {
   int flip;    // 1: W is the layer's weight and the call its input gradient: A = W[c][m][26 - t]
 };
 
-template <int YB, int NXT, int NTH, bool ADD = false>  // output rows per block; 16-column tiles per row (W = 16
-__global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); threads; `add` summed into the store
+// NS: plane-ring slots.  3: a step's MFMAs read planes z - 1 .. z + 1, plane z + 2 goes over plane z - 1's
+// slot after a barrier; 4 (when it fits): plane z + 2 goes into the slot plane z - 2 held, which no wave
+// reads in step z -- one barrier per step instead of two.
+template <int YB, int NXT, int NTH, bool ADD = false, bool PF = false, int NS = 3>  // output rows per block;
+__global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column tiles per row (W = 16 NXT);
+                                            // threads; `add` summed into the store; PF: B reads a tap ahead
   constexpr int NWV = NTH / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NR = YB + 2, W4 = 4 * NXT;  // staged rows; float4 per row
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int D = a.D, H = a.H, Wd = a.Wd, PX = a.PX, RX = a.RX, SS = 16 * RX;
-  float* ring = smem;  // [3][16 c][NR][PX]
-  for (int i = tid; i < 3 * SS; i += NTH) ring[i] = 0.f;
+  float* ring = smem;  // [NS][16 c][NR][PX]
+  for (int i = tid; i < NS * SS; i += NTH) ring[i] = 0.f;
   int b = (int)blockIdx.x;
   const int zs = b % a.ZS;
   b /= a.ZS;
@@ -468,7 +472,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
     }
   };
   auto store = [&](int zi) {
-    float* d = ring + ((zi + 3) % 3) * SS;
+    float* d = ring + ((zi + NS) % NS) * SS;
     const bool in = zi >= 0 && zi < D;
 #pragma unroll
     for (int j = 0; j < NL; ++j)
@@ -500,9 +504,9 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
   for (int z = z0; z < z1; ++z) {
     const bool more = z + 1 < z1;
     if (more) load(z + 2);
-    const float* s0 = ring + ((z + 2) % 3) * SS + bl;  // tz = 0: plane z - 1
-    const float* s1 = ring + (z % 3) * SS + bl;
-    const float* s2 = ring + ((z + 1) % 3) * SS + bl;
+    const float* s0 = ring + ((z + NS - 1) % NS) * SS + bl;  // tz = 0: plane z - 1
+    const float* s1 = ring + (z % NS) * SS + bl;
+    const float* s2 = ring + ((z + 1) % NS) * SS + bl;
     f32x4 acc[NIT][2];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {  // tiles t0 and t0 + NWV of this wave
@@ -513,6 +517,34 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
       const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
       const int o0 = yy0 * PX + x00, o1 = yy1 * PX + x01;
       f32x4 acc0 = {bm[0], bm[1], bm[2], bm[3]}, acc1 = acc0;
+      if constexpr (PF) {  // the next tap's 8 B fragments read while this tap's 8 MFMAs run
+        float bq[2][8];
+        auto ldb = [&](int t, float (&q)[8]) {
+          const int tz = t / 9, ty = (t / 3) % 3, tx = t % 3;
+          const float* sl = tz == 0 ? s0 : tz == 1 ? s1 : s2;
+#pragma unroll
+          for (int cq = 0; cq < 4; ++cq) {
+            const int off = 4 * cq * RX + ty * PX + tx;
+            q[2 * cq] = sl[o0 + off], q[2 * cq + 1] = sl[o1 + off];
+          }
+        };
+        ldb(0, bq[0]);
+#pragma unroll
+        for (int t = 0; t < 27; ++t) {
+          if (t + 1 < 27) ldb(t + 1, bq[(t + 1) & 1]);
+#pragma unroll
+          for (int cq = 0; cq < 4; ++cq) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], bq[t & 1][2 * cq], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], bq[t & 1][2 * cq + 1], acc1, 0, 0, 0);
+          }
+        }
+        // schedule: one MFMA, then one LDS read (the next tap's), alternating
+#pragma unroll
+        for (int i = 0; i < 216; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      } else {
 #pragma unroll
       for (int tz = 0; tz < 3; ++tz) {
         const float* sl = tz == 0 ? s0 : tz == 1 ? s1 : s2;
@@ -530,9 +562,10 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // NXT); thr
             }
           }
       }
+      }
       acc[it][0] = acc0, acc[it][1] = acc1;
     }
-    __syncthreads();
+    if constexpr (NS == 3) __syncthreads();
     store(z + 2);  // unconditionally (after the last step a dead slot): no path skips the loads' wait
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {  // C: column x = li, rows m = 4 ks + r
@@ -960,7 +993,12 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
   a.RX = (YB + 2) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;
   a.nyb = (H + YB - 1) / YB;
-  const size_t lds = (size_t)3 * 4 * 16 * a.RX;
+  static const int ring4 = [] {
+    const char* e = std::getenv("TEXBIAS_CONV16_RING");
+    return e && std::atoi(e) == 3 ? 0 : 1;
+  }();
+  const int NS = ring4 && (size_t)4 * 4 * 16 * a.RX <= 163840 ? 4 : 3;
+  const size_t lds = (size_t)NS * 4 * 16 * a.RX;
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
   const int per_cu = 163840 / (int)lds >= 2 ? 2 : 1;
   a.zlen = zseg(D, N * a.nyb, per_cu, 2);
@@ -972,20 +1010,34 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
     const char* e = std::getenv("TEXBIAS_CONV16_NT");
     return e && std::atoi(e) == 256 ? 512 : 512;
   }();
+  // the B fragments read a tap ahead of their MFMAs, interleaved one LDS read per MFMA (sched_group_barrier)
+  // and a 4-slot plane ring, one barrier per step (TEXBIAS_CONV16_PF=0 / TEXBIAS_CONV16_RING=3 off; C3, by
+  // scripts/diag/conv_kern_bench.py: forward 385 -> 374 us, input gradient 361 -> 353 us)
+  static const bool PFv = [] {
+    const char* e = std::getenv("TEXBIAS_CONV16_PF");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (PFv && !add && YB == 3 && NTv == 512 && Wd == 80) {
+    kern = NS == 4 ? k_conv3d_fwd16<3, 5, 512, false, true, 4> : k_conv3d_fwd16<3, 5, 512, false, true, 3>;
+  } else
+#define TB_F16C(Y, X, T) \
+  kern = add ? (NS == 4 ? k_conv3d_fwd16<Y, X, T, true, false, 4> : k_conv3d_fwd16<Y, X, T, true, false, 3>) \
+             : (NS == 4 ? k_conv3d_fwd16<Y, X, T, false, false, 4> : k_conv3d_fwd16<Y, X, T, false, false, 3>);
 #define TB_F16(Y, T)                                                                                   \
   if (YB == Y && NTv == T) switch (Wd / 16) {                                                          \
-      case 1: kern = add ? k_conv3d_fwd16<Y, 1, T, true> : k_conv3d_fwd16<Y, 1, T>; break;             \
-      case 2: kern = add ? k_conv3d_fwd16<Y, 2, T, true> : k_conv3d_fwd16<Y, 2, T>; break;             \
-      case 3: kern = add ? k_conv3d_fwd16<Y, 3, T, true> : k_conv3d_fwd16<Y, 3, T>; break;             \
-      case 4: kern = add ? k_conv3d_fwd16<Y, 4, T, true> : k_conv3d_fwd16<Y, 4, T>; break;             \
-      case 5: kern = add ? k_conv3d_fwd16<Y, 5, T, true> : k_conv3d_fwd16<Y, 5, T>; break;             \
-      case 6: kern = add ? k_conv3d_fwd16<Y, 6, T, true> : k_conv3d_fwd16<Y, 6, T>; break;             \
-      case 7: kern = add ? k_conv3d_fwd16<Y, 7, T, true> : k_conv3d_fwd16<Y, 7, T>; break;             \
-      case 8: kern = add ? k_conv3d_fwd16<Y, 8, T, true> : k_conv3d_fwd16<Y, 8, T>; break;             \
+      case 1: TB_F16C(Y, 1, T) break;                                                                  \
+      case 2: TB_F16C(Y, 2, T) break;                                                                  \
+      case 3: TB_F16C(Y, 3, T) break;                                                                  \
+      case 4: TB_F16C(Y, 4, T) break;                                                                  \
+      case 5: TB_F16C(Y, 5, T) break;                                                                  \
+      case 6: TB_F16C(Y, 6, T) break;                                                                  \
+      case 7: TB_F16C(Y, 7, T) break;                                                                  \
+      case 8: TB_F16C(Y, 8, T) break;                                                                  \
       default: return TB_ERR_UNSUPPORTED_SIZE;                                                         \
     }
   TB_F16(3, 512)
 #undef TB_F16
+#undef TB_F16C
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;

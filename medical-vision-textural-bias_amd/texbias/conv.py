@@ -494,12 +494,11 @@ class Route:
     # -- input gradient (x only for its shape on the ATen path; ``add`` summed in, as in forward)
     def input_grad(self, gy, x, w, add=None):
         k = self.dx
-        if add is not None:
-            add = add.contiguous()
-            if k == "small":
-                return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None, add)
+        if add is not None:  # (a strided add -- a channel slice of the skip concatenation's gradient -- is
+            if k == "small":  # copied only for the kernels that read it)
+                return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None, add.contiguous())
             if k == "gemm" and not self.transposed and self.stride[0] == 1:
-                return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2], add=add)
+                return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2], add=add.contiguous())
             return self.input_grad(gy, x, w).add_(add)
         if k == "fwd16":
             return conv_fwd16_dgrad(gy, w)

@@ -56,9 +56,9 @@ class _ConvADNFn(torch.autograd.Function):
     """y = prelu(instance_norm(conv(x))) (+ res): MONAI Convolution "NDA" (+ the ResidualUnit's sum)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, a, route, eps, res, res_is_x):
+    def forward(ctx, x, w, b, a, route, eps, res, res_is_x, out=None):
         z = route.forward(x.contiguous(), w, b)
-        y, mean, rstd = adn_forward(z, a, eps, res=res)
+        y, mean, rstd = adn_forward(z, a, eps, res=res, out=out)
         ctx.save_for_backward(x, w, a, z, mean, rstd)
         ctx.route, ctx.has_b, ctx.has_res, ctx.res_is_x = route, b is not None, res is not None, res_is_x
         return y
@@ -67,14 +67,14 @@ class _ConvADNFn(torch.autograd.Function):
     def backward(ctx, g):
         x, w, a, z, mean, rstd = ctx.saved_tensors
         n = ctx.needs_input_grad
-        g = g.contiguous()
+        g = _norm._plain(g)  # a channel slice of the skip concatenation's gradient is read in place
         dz, da, db = adn_backward(z, g, mean, rstd, a, need_w=n[3], need_bias=ctx.has_b and n[2])
         gw = ctx.route.weight_grad(dz, x, w) if n[1] else None
         if ctx.res_is_x:  # identity residual: dX = dconv(dZ) + dY in the input-gradient kernel's store
             gx = ctx.route.input_grad(dz, x, w, add=g) if n[0] else None
-            return gx, gw, db, da, None, None, None, None
+            return gx, gw, db, da, None, None, None, None, None
         gx = ctx.route.input_grad(dz, x, w) if n[0] else None
-        return gx, gw, db, da, None, None, (g if ctx.has_res and n[6] else None), None
+        return gx, gw, db, da, None, None, (g if ctx.has_res and n[6] else None), None, None
 
 
 class _ConvResFn(torch.autograd.Function):
@@ -168,13 +168,14 @@ class Convolution(nn.Sequential):
         if not conv_only:
             self.add_module("adn", ADN(cout, dropout))
 
-    def fused(self, x, res=None):
-        """conv -> ADN (+ res) as one autograd function, or None when the fused path does not apply."""
+    def fused(self, x, res=None, out=None):
+        """conv -> ADN (+ res) as one autograd function, or None when the fused path does not apply.
+        ``out``: storage to write the result into (an alias, see ``_alias``)."""
         adn = getattr(self, "adn", None)
         if adn is None or not _fusable(x, self.conv, adn):
             return None
         return _ConvADNFn.apply(x, self.conv.weight, self.conv.bias, adn.A.weight, _conv.route_of(self.conv, x),
-                                adn.N.eps, res, res is x)
+                                adn.N.eps, res, res is x, out)
 
     def forward(self, x):
         y = self.fused(x)
@@ -211,7 +212,11 @@ class ResidualUnit(nn.Module):
                 return _StackedUnitFn.apply(x, u0.conv.weight, u0.conv.bias, r.weight, r.bias, u0.adn.A.weight,
                                             u1.conv.weight, u1.conv.bias, u1.adn.A.weight, self, u0.adn.N.eps)
         if isinstance(self.residual, nn.Identity) and len(units) == 1 and hasattr(units[0], "adn"):
-            y = units[0].fused(x, res=x)
+            out = self.__dict__.pop("_tb_out", None)
+            if out is not None and tuple(out.shape) != tuple(x.shape[:1]) + (units[0].conv.out_channels,) + \
+                    tuple(x.shape[2:]):
+                out = None
+            y = units[0].fused(x, res=x, out=out)
             if y is not None:
                 return y
         if isinstance(self.residual, nn.Identity) and len(units) == 1 and not hasattr(units[0], "adn") and \
@@ -233,12 +238,59 @@ class ResidualUnit(nn.Module):
         return rt
 
 
+def _alias(buf: torch.Tensor, c0: int, c1: int) -> torch.Tensor:
+    """Channels [c0, c1) of ``buf`` as a tensor of its own that shares the storage but is not an autograd
+    view (its own version counter): a kernel writes into it through the raw pointer."""
+    sh = (buf.shape[0], c1 - c0) + tuple(buf.shape[2:])
+    return torch.empty(0, dtype=buf.dtype, device=buf.device).set_(
+        buf.untyped_storage(), buf.storage_offset() + c0 * buf.stride(1), sh, buf.stride())
+
+
+class _SkipCatFn(torch.autograd.Function):
+    """cat([x, s], 1) where s already sits in channels [c, c + cs) of ``buf``: only x is copied."""
+
+    @staticmethod
+    def forward(ctx, x, s, buf):
+        c = x.shape[1]
+        _alias(buf, 0, c).copy_(x)
+        ctx.c = c
+        return _alias(buf, 0, buf.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:, :ctx.c], g[:, ctx.c:], None
+
+
 class SkipConnection(nn.Module):
     def __init__(self, submodule: nn.Module):
         super().__init__()
         self.submodule = submodule
 
+    def _tail_unit(self):
+        """The identity-residual unit whose output ends the submodule (``_up``'s ResidualUnit), if any."""
+        m = self.submodule
+        if isinstance(m, nn.Sequential) and len(m) > 0 and isinstance(m[-1], nn.Sequential) and len(m[-1]) == 2:
+            ru = m[-1][1]
+            if isinstance(ru, ResidualUnit) and isinstance(ru.residual, nn.Identity):
+                return ru
+        return None
+
     def forward(self, x):
+        # On the fused HIP path the submodule's last unit writes its output straight into the concatenation's
+        # upper channels (one copy instead of two)
+        ru = self._tail_unit() if (FUSED and x.is_cuda and x.dtype == torch.float32) else None
+        if ru is not None:
+            cs = list(ru.conv.children())[0].conv.out_channels
+            buf = torch.empty((x.shape[0], x.shape[1] + cs) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device)
+            tail = _alias(buf, x.shape[1], x.shape[1] + cs)
+            ru._tb_out = tail
+            try:
+                s = self.submodule(x)
+            finally:
+                ru.__dict__.pop("_tb_out", None)
+            if s.data_ptr() == tail.data_ptr() and s.shape == tail.shape:
+                return _SkipCatFn.apply(x, s, buf)
+            return torch.cat([x, s], dim=1)
         return torch.cat([x, self.submodule(x)], dim=1)
 
 

@@ -107,3 +107,32 @@ def test_adn_strided_residual_bias(gpu, shape):
     assert torch.equal(y2, y) and torch.equal(m2, mean) and torch.equal(s2, rstd)
     from texbias.norm import counters
     assert int(counters(z.device, 1).abs().sum().item()) == 0   # every counter left at zero
+
+
+def test_skip_buffer_matches_cat(gpu, monkeypatch):
+    """The skip concatenation written in place (the submodule's last unit stores into the buffer's upper
+    channels, only x copied; strided gradient slices read in place) gives the same loss and parameter
+    gradients as torch.cat of separate tensors."""
+    from texbias import unet
+    from texbias.losses import DiceLoss
+    torch.manual_seed(2)
+    m = unet.UNet(3, 4, 3, (16, 32, 64, 128, 256), (2, 2, 2, 2), num_res_units=2).to(gpu)
+    x = torch.randn(2, 4, 32, 32, 32, device=gpu)
+    lab = (torch.rand(2, 3, 32, 32, 32, device=gpu) > 0.7).float()
+    loss_fn = DiceLoss(sigmoid=True, squared_pred=True)
+    skips = [mod for mod in m.modules() if isinstance(mod, unet.SkipConnection)]
+    assert sum(s._tail_unit() is not None for s in skips) == 3   # every level but the bottom
+    outs = []
+    for inplace in (True, False):
+        if not inplace:
+            monkeypatch.setattr(unet.SkipConnection, "_tail_unit", lambda self: None)
+        m.zero_grad(set_to_none=True)
+        y = m(x)
+        loss = loss_fn(y, lab)
+        loss.backward()
+        outs.append((y.detach().clone(), loss.detach(), [p.grad.detach().clone() for p in m.parameters()]))
+    (y1, l1, g1), (y2, l2, g2) = outs
+    torch.testing.assert_close(y1, y2, rtol=1e-6, atol=1e-6)
+    assert abs(l1.item() - l2.item()) <= 1e-6
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * max(b.abs().max().item(), 1e-3))
