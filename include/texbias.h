@@ -333,9 +333,11 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
  * per-sample batch strides (a channel slice of a wider tensor: *sn = floats between samples, 0 =
  * contiguous C S), the ResidualUnit's sum fused into the forward store (y = prelu(norm(x)) + res; res
  * may be NULL), and in the backward the preceding convolution's bias gradient dbias[c] = sum over n and
- * voxels of dx (NULL: not computed) and the PReLU weight gradient dw (NULL: not computed).  No
- * accumulator memsets and no float atomics: every block stores partial sums, a one-block-per-instance
- * (channel) finalize kernel sums them in block order -- results are deterministic.  `counters`: DEVICE
+ * voxels of dx, taken in float64 from the backward statistics as -rstd mean(g z) sum(z) (the exact value
+ * is zero: the norm removes a bias; NULL: not computed), and the PReLU weight gradient dw (NULL: not
+ * computed).  No accumulator memsets and no float atomics: every block stores partial sums, reduced in
+ * block order (forward: by every apply block; backward: one block per instance) -- results are
+ * deterministic; two launches forward, three backward.  `counters`: DEVICE
  * uint32[tb_adn_counters(N, C)], zero before the first call, left zero by every call (one set per
  * stream); ws: tb_adn_workspace_bytes(N, C, S) bytes of device scratch.
  */

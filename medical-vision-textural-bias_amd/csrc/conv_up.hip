@@ -1358,6 +1358,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
     f32x4 acc[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (B reads a k-step ahead with per-step scheduling barriers measured no change, 209 / 120 us)
 #pragma unroll
     for (int tz = 0; tz < 3; ++tz)
 #pragma unroll

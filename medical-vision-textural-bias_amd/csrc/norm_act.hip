@@ -385,8 +385,8 @@ struct AdnArgs {
   const float* aw;
   float* dw;
   float* dbias;
-  double* part;   // [NC][nblk][3]
-  double* inst;   // [NC][4]: per-instance results (backward: mg, mgz, sa)
+  double* part;   // [NC][nblk][2 | 4]: block partials (forward: sum x, x^2; backward: g, g z, dy z [z<=0], z)
+  double* inst;   // [NC][4]: per-instance results (backward: mg, mgz, sa, the bias-gradient share)
   uint32_t* cnt;  // [2 NC + C + 1]
   int64_t S;
   int C, NC, nblk;
@@ -492,22 +492,17 @@ __global__ __launch_bounds__(NT) void k_adn_stats(const AdnArgs a) {
   if (threadIdx.x < 2) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 2 + threadIdx.x] = tot[threadIdx.x];
 }
 
-// one block per instance: the instance's block partials summed in block order -> mean, rstd
-__global__ __launch_bounds__(NT) void k_adn_fin_fwd(const AdnArgs a) {
-  const int nc = blockIdx.x;
-  double all[2];
-  reduce_partials<2>(a.part + (int64_t)nc * a.nblk * 2, a.nblk, all);
-  if (threadIdx.x == 0) {
-    float mean, rstd;
-    stats_of(all[0], all[1], a.S, a.eps, mean, rstd);
-    a.mean[nc] = mean;
-    a.rstd[nc] = rstd;
-  }
-}
-
+// every block first sums its instance's statistics partials (the same fixed-order reduction in every
+// block, so every block gets the same mean / rstd -- the separate finalize launch folded in); block
+// (0, nc) stores them for the backward
 __global__ __launch_bounds__(NT) void k_adn_apply(const AdnArgs a) {
   const int nc = blockIdx.y;
-  const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
+  double all[2];
+  reduce_partials<2>(a.part + (int64_t)nc * a.nblk * 2, a.nblk, all);
+  float mean, rstd;
+  stats_of(all[0], all[1], a.S, a.eps, mean, rstd);
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.mean[nc] = mean, a.rstd[nc] = rstd;
+  const float aw = *a.aw;
   const int64_t b = (int64_t)blockIdx.x * CHUNK;
   const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
   const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
@@ -551,14 +546,15 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
   const int nc = blockIdx.y;
   const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
   const double md = mean, rd = rstd;
-  double s1 = 0.0, s2 = 0.0, sa = 0.0;
-  auto visit = [&](float xv, float gv) {
+  double s1 = 0.0, s2 = 0.0, sa = 0.0, sz = 0.0;
+  auto visit = [&](float xv, float gv, bool in = true) {  // (in: a real voxel, not a zero-padded lane)
     const bool pos = (xv - mean) * rstd > 0.f;
     const double z = ((double)xv - md) * rd;
     const double g = pos ? (double)gv : (double)aw * (double)gv;
     s1 += g;
     s2 += g * z;
     sa += pos ? 0.0 : (double)gv * z;
+    sz += in ? z : 0.0;
   };
   const int64_t b = (int64_t)blockIdx.x * CHUNK;
   const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
@@ -579,32 +575,46 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        visit(vx[k].x, vg[k].x);
-        visit(vx[k].y, vg[k].y);
-        visit(vx[k].z, vg[k].z);
-        visit(vx[k].w, vg[k].w);
+        const bool in = (int)threadIdx.x + (h * U + k) * NT < n4;
+        visit(vx[k].x, vg[k].x, in);
+        visit(vx[k].y, vg[k].y, in);
+        visit(vx[k].z, vg[k].z, in);
+        visit(vx[k].w, vg[k].w, in);
       }
     }
   } else {
     for (int64_t i = threadIdx.x; i < e - b; i += NT) visit(xp[i], gp[i]);
   }
-  double in[3] = {s1, s2, sa}, tot[3];
-  block_sum<3>(in, tot);
-  if (threadIdx.x < 3) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 3 + threadIdx.x] = tot[threadIdx.x];
+  double in[4] = {s1, s2, sa, sz}, tot[4];
+  block_sum<4>(in, tot);
+  if (threadIdx.x < 4) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 4 + threadIdx.x] = tot[threadIdx.x];
 }
 
-// one block per instance: mg, mgz and the instance's PReLU term; the last instance block to finish sums
-// the PReLU weight gradient over the instances (in instance order)
+// one block per instance: mg, mgz, the instance's PReLU term and its share of the producing conv's bias
+// gradient, sum_voxels dx = rstd (sum g - S mg - mgz sum z) = -rstd mgz sum z (float64, from this sweep:
+// no store-pass partials and no separate finalize); the last instance block to finish sums the PReLU
+// weight gradient over the instances and the bias gradient over the samples (in order)
 __global__ __launch_bounds__(NT) void k_adn_fin_bwd(const AdnArgs a) {
   const int nc = blockIdx.x;
-  double all[3];
-  reduce_partials<3>(a.part + (int64_t)nc * a.nblk * 3, a.nblk, all);
-  double res[3] = {all[0] / (double)a.S, all[1] / (double)a.S, all[2]};
-  if (!publish_last<3>(res, a.inst, nc, a.cnt, a.NC) || !a.dw) return;
-  double v[1] = {0.0}, sw[1];
-  for (int i = threadIdx.x; i < a.NC; i += NT) v[0] += load_d(a.inst + 3 * i + 2);
-  block_sum<1>(v, sw);
-  if (threadIdx.x == 0) *a.dw = (float)sw[0];
+  double all[4];
+  reduce_partials<4>(a.part + (int64_t)nc * a.nblk * 4, a.nblk, all);
+  const double mgz = all[1] / (double)a.S;
+  double res[4] = {all[0] / (double)a.S, mgz, all[2], -(double)a.rstd[nc] * mgz * all[3]};
+  if (!publish_last<4>(res, a.inst, nc, a.cnt, a.NC)) return;
+  if (a.dw) {
+    double v[1] = {0.0}, sw[1];
+    for (int i = threadIdx.x; i < a.NC; i += NT) v[0] += load_d(a.inst + 4 * i + 2);
+    block_sum<1>(v, sw);
+    if (threadIdx.x == 0) *a.dw = (float)sw[0];
+  }
+  if (a.dbias) {
+    const int N = a.NC / a.C;
+    for (int c = threadIdx.x; c < a.C; c += NT) {
+      double v = 0.0;
+      for (int n = 0; n < N; ++n) v += load_d(a.inst + 4 * (n * a.C + c) + 3);
+      a.dbias[c] = (float)v;
+    }
+  }
 }
 
 // dx = rstd (g - mg - z mgz); dbias[c] = sum over n and voxels of dx (partials + per-channel counter)
@@ -612,7 +622,7 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
   const int nc = blockIdx.y;
   const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
   const double md = mean, rd = rstd;
-  const double mg = load_d(a.inst + 3 * nc), mgz = load_d(a.inst + 3 * nc + 1);
+  const double mg = load_d(a.inst + 4 * nc), mgz = load_d(a.inst + 4 * nc + 1);
   auto f = [&](float xv, float gv) {
     const bool pos = (xv - mean) * rstd > 0.f;
     const double z = ((double)xv - md) * rd;
@@ -624,7 +634,6 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
   const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
   const float* gp = a.dy + inst_base(nc, a.C, a.dysn, a.S) + b;
   float* qp = a.y + inst_base(nc, a.C, a.ysn, a.S) + b;
-  double sb = 0.0;
   if (a.vec) {
     const int n4 = (int)((e - b) >> 2);
     constexpr int U = VPT / 2;
@@ -649,31 +658,12 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
           o.z = f(vx[k].z, vg[k].z);
           o.w = f(vx[k].w, vg[k].w);
           reinterpret_cast<float4*>(qp)[i] = o;
-          sb += ((double)o.x + (double)o.y) + ((double)o.z + (double)o.w);
         }
       }
     }
   } else {
-    for (int64_t i = threadIdx.x; i < e - b; i += NT) {
-      const float o = f(xp[i], gp[i]);
-      qp[i] = o;
-      sb += o;
-    }
+    for (int64_t i = threadIdx.x; i < e - b; i += NT) qp[i] = f(xp[i], gp[i]);
   }
-  if (!a.dbias) return;
-  // partial slot (n, block) of channel c
-  const int n = nc / a.C, c = nc % a.C, N = a.NC / a.C;
-  double in[1] = {sb}, tot[1];
-  block_sum<1>(in, tot);
-  if (threadIdx.x == 0) a.part[(int64_t)c * N * a.nblk + n * a.nblk + blockIdx.x] = tot[0];
-}
-
-// one block per channel: dbias[c] = the channel's (n, block) partials summed in order
-__global__ __launch_bounds__(NT) void k_adn_fin_bias(const AdnArgs a) {
-  const int c = blockIdx.x, N = a.NC / a.C;
-  double all[1];
-  reduce_partials<1>(a.part + (int64_t)c * N * a.nblk, N * a.nblk, all);
-  if (threadIdx.x == 0) a.dbias[c] = (float)all[0];
 }
 
 // DiceLoss finalize (MONAI's formula, the reference's DiceLoss(sigmoid, squared_pred), stylized_gibbs12p5.py:201):
@@ -836,7 +826,7 @@ inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintp
 
 size_t tb_adn_workspace_bytes(int64_t N, int64_t C, int64_t S) {
   const int64_t NC = N * C, nb = adn_nblk(S);
-  return (size_t)(NC * nb * 3 + NC * 3 + 64) * sizeof(double);
+  return (size_t)(NC * nb * 4 + NC * 4 + 64) * sizeof(double);
 }
 
 int64_t tb_adn_counters(int64_t N, int64_t C) { return 1 + 0 * N * C; }
@@ -852,15 +842,14 @@ int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const flo
   a.xsn = xsn > 0 ? xsn : C * S, a.ysn = ysn > 0 ? ysn : C * S, a.rsn = rsn > 0 ? rsn : C * S;
   a.mean = mean, a.rstd = rstd, a.aw = prelu_w;
   a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  a.inst = a.part + N * C * adn_nblk(S) * 3;
+  a.inst = a.part + N * C * adn_nblk(S) * 4;
   a.cnt = counters;
   a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S), a.eps = eps;
   a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.rsn % 4 == 0 && al16(x) && al16(y) && al16(res);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)a.nblk, (unsigned)a.NC);
   hipLaunchKernelGGL(k_adn_stats, grid, dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(k_adn_fin_fwd, dim3((unsigned)a.NC), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(k_adn_apply, grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(k_adn_apply, grid, dim3(NT), 0, st, a);  // (the statistics finalize folded in)
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
@@ -876,7 +865,7 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
   a.xsn = xsn > 0 ? xsn : C * S, a.dysn = dysn > 0 ? dysn : C * S, a.ysn = dxsn > 0 ? dxsn : C * S;
   a.mean = const_cast<float*>(mean), a.rstd = const_cast<float*>(rstd), a.aw = prelu_w, a.dw = dw, a.dbias = dbias;
   a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  a.inst = a.part + N * C * adn_nblk(S) * 3;
+  a.inst = a.part + N * C * adn_nblk(S) * 4;
   a.cnt = counters;
   a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S);
   a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.dysn % 4 == 0 && al16(x) && al16(dy) && al16(dx);
@@ -885,6 +874,5 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
   hipLaunchKernelGGL(k_adn_bwd_stats, grid, dim3(NT), 0, st, a);
   hipLaunchKernelGGL(k_adn_fin_bwd, dim3((unsigned)a.NC), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(k_adn_bwd_apply, grid, dim3(NT), 0, st, a);
-  if (dbias) hipLaunchKernelGGL(k_adn_fin_bias, dim3((unsigned)C), dim3(NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }

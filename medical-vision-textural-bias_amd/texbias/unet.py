@@ -99,6 +99,17 @@ class _ConvResFn(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+def _adjacent(a: torch.Tensor, b: torch.Tensor):
+    """[a; b] along dim 0 without a copy when b's storage directly follows a's (``ResidualUnit`` keeps the
+    unit-0 and residual parameters of a strided unit that way), else None."""
+    if not (a.is_contiguous() and b.is_contiguous() and a.shape[1:] == b.shape[1:] and a.dtype == b.dtype and
+            a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr() and
+            b.storage_offset() == a.storage_offset() + a.numel()):
+        return None
+    return torch.empty(0, dtype=a.dtype, device=a.device).set_(
+        a.untyped_storage(), a.storage_offset(), (a.shape[0] + b.shape[0],) + tuple(a.shape[1:]))
+
+
 class _StackedUnitFn(torch.autograd.Function):
     """A strided ResidualUnit: [unit0 | residual] = conv(x, [W0; Wr], stride 2) as one convolution,
     a0 = ADN0(unit0), out = ADN1(conv1(a0)) + residual."""
@@ -106,8 +117,14 @@ class _StackedUnitFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w0, b0, wr, br, a0w, w1, b1, a1w, unit, eps):
         c = w0.shape[0]
-        w_st = torch.cat([w0, wr], 0)
-        b_st = torch.cat([b0, br], 0) if b0 is not None and br is not None else None
+        w_st = _adjacent(w0, wr)
+        if w_st is None:
+            w_st = torch.cat([w0, wr], 0)
+        b_st = None
+        if b0 is not None and br is not None:
+            b_st = _adjacent(b0, br)
+            if b_st is None:
+                b_st = torch.cat([b0, br], 0)
         x = x.contiguous()
         r_st = unit.stacked_route(x, w_st)
         y2 = r_st.forward(x, w_st, b_st)                      # [N, 2c, ...]
@@ -209,6 +226,7 @@ class ResidualUnit(nn.Module):
                     and isinstance(u0.conv, Conv3d) and _fusable(x, u0.conv, u0.adn) and _fusable(x, r, None) and \
                     _fusable(x, u1.conv, u1.adn) and (r.bias is None) == (u0.conv.bias is None) and \
                     u0.adn.N.eps == u1.adn.N.eps and r.padding_mode == "zeros":
+                self._stack_params(u0.conv, r)
                 return _StackedUnitFn.apply(x, u0.conv.weight, u0.conv.bias, r.weight, r.bias, u0.adn.A.weight,
                                             u1.conv.weight, u1.conv.bias, u1.adn.A.weight, self, u0.adn.N.eps)
         if isinstance(self.residual, nn.Identity) and len(units) == 1 and hasattr(units[0], "adn"):
@@ -225,6 +243,19 @@ class ResidualUnit(nn.Module):
             return _ConvResFn.apply(x, c.weight, c.bias, _conv.route_of(c, x))
         res = self.residual(x)
         return self.conv(x) + res
+
+    @staticmethod
+    def _stack_params(c0: nn.Module, r: nn.Module):
+        """Once: move unit 0's and the residual conv's weights (and biases) into one storage each, unit 0's
+        first, so that the stacked convolution reads them as one tensor with no per-step concatenation.
+        The Parameter objects stay the same (optimizers and state dicts are unaffected)."""
+        with torch.no_grad():
+            for n in ("weight", "bias"):
+                a, b = getattr(c0, n), getattr(r, n)
+                if a is None or b is None or _adjacent(a, b) is not None:
+                    continue
+                st = torch.cat([a.detach(), b.detach()], 0)
+                a.data, b.data = st[:a.shape[0]], st[a.shape[0]:]
 
     def stacked_route(self, x: torch.Tensor, w_st: torch.Tensor) -> "_conv.Route":
         """The route of the stacked [unit0; residual] convolution for this input (cached per shape)."""

@@ -1,6 +1,8 @@
 """Fused InstanceNorm3d + PReLU (tb_instnorm_prelu_{fwd,bwd}_f32) against torch's own
 instance_norm -> prelu in float64 on the same inputs: y, dx and the PReLU weight gradient.
 Tolerance: max-abs error <= 2e-5 x max|ref| (float32 arithmetic, different summation order)."""
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -100,7 +102,10 @@ def test_adn_strided_residual_bias(gpu, shape):
     (yr * g.double()).sum().backward()
     _close(dx, zr.grad)
     _close(dw, wr.grad, tol=1e-5)
-    torch.testing.assert_close(db.double(), dx.double().sum(dim=(0, 2, 3, 4)), rtol=1e-6, atol=1e-6)
+    # the bias gradient's exact value is 0 (the norm removes a bias): the float64 value from the statistics
+    # and the float32 dx summed agree to dx's rounding (6e-8 |dx| per voxel, random: ~sqrt(N S) of them)
+    tol = 6e-8 * dx.abs().max().item() * (N * math.prod(shape[2:])) ** 0.5 * 4
+    torch.testing.assert_close(db.double(), dx.double().sum(dim=(0, 2, 3, 4)), rtol=0, atol=tol)
     dx2, dw2, db2 = adn_backward(z, g, mean, rstd, w, need_w=True, need_bias=True)
     assert torch.equal(dx2, dx) and torch.equal(dw2, dw) and torch.equal(db2, db)
     y2, m2, s2 = adn_forward(z, w, 1e-5, res=r)
