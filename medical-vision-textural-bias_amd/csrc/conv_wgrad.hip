@@ -360,13 +360,12 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
   }
   float4 rx[NXL], rg[NGL];
   const int64_t plane4 = plane / 4;
+  // (zero-selects at the LDS store, not at the load: a select right after a load makes the wave wait
+  // for it there, and the next plane's loads would not overlap this plane's MFMAs)
   auto load_x = [&](int zi) {
     const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)zi * plane4;
 #pragma unroll
-    for (int j = 0; j < NXL; ++j) {
-      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
-      rx[j] = xg[j] < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
-    }
+    for (int j = 0; j < NXL; ++j) rx[j] = src[xg[j] < 0 ? 0 : xg[j]];
   };
   auto store_x = [&](int slot) {
     float* d = xsl + slot * XS;
@@ -378,23 +377,22 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
         p[1] = make_float2(rx[j].z, rx[j].w);
       }
   };
+  bool gin = false;             // the G plane in rg lies inside [0, D) (else stored as zeros)
   auto load_g = [&](int pz) {  // G plane pz (zero outside [0, D))
-    const bool in = pz >= 0 && pz < D;
-    const float4* src = reinterpret_cast<const float4*>(Gb) + (int64_t)(in ? pz : 0) * plane4;
+    gin = pz >= 0 && pz < D;
+    const float4* src = reinterpret_cast<const float4*>(Gb) + (int64_t)(gin ? pz : 0) * plane4;
 #pragma unroll
-    for (int j = 0; j < NGL; ++j) {
-      const float4 v = src[gg[j] < 0 ? 0 : gg[j]];
-      rg[j] = (in && gg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int j = 0; j < NGL; ++j) rg[j] = src[gg[j] < 0 ? 0 : gg[j]];
   };
   auto store_g = [&](int slot) {
     float* d = gsl + slot * GS;
 #pragma unroll
     for (int j = 0; j < NGL; ++j)
       if (gg[j] >= 0) {
+        const float4 v = gin ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         float2* p = reinterpret_cast<float2*>(d + gl[j]);
-        p[0] = make_float2(rg[j].x, rg[j].y);
-        p[1] = make_float2(rg[j].z, rg[j].w);
+        p[0] = make_float2(v.x, v.y);
+        p[1] = make_float2(v.z, v.w);
       }
   };
   __syncthreads();  // the zero fill is done before any slab store
@@ -417,10 +415,11 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
     store_x(zi & 1);
     store_g((zi + 1) & 3);
     __syncthreads();  // slabs of this step visible; every wave is past the step that last read these slots
-    if (zi + 1 < z1) {  // next step's slabs fly during this step's MFMAs
-      load_x(zi + 1);
-      load_g(zi + 2);
-    }
+    // next step's slabs fly during this step's MFMAs -- unconditionally (after the last step a clamped,
+    // never-stored plane): a conditional load leaves a register merge at the loop edge whose copies wait
+    // for the loads before the MFMAs
+    load_x(zi + 1 < D ? zi + 1 : zi);
+    load_g(zi + 2);
     const float* g0 = gsl + ((zi + 1) & 3) * GS + aoff;  // tz = 0: plane zi + 1
     const float* g1 = gsl + (zi & 3) * GS + aoff;        // tz = 1: plane zi
     const float* g2 = gsl + ((zi + 3) & 3) * GS + aoff;  // tz = 2: plane zi - 1
@@ -539,30 +538,28 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   }
   const int64_t iplane4 = iplane / 4, oplane4 = oplane / 4;
   float4 rx0[NXL], rx1[NXL], rg[NGL];
-  auto load_x = [&](int zi, float4 (&rx)[NXL]) {  // input plane zi (zero outside [0, Di))
+  auto load_x = [&](int zi, float4 (&rx)[NXL]) {  // input plane zi (zero outside [0, Di), at the store)
     const bool in = zi >= 0 && zi < Di;
     const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(in ? zi : 0) * iplane4;
 #pragma unroll
-    for (int j = 0; j < NXL; ++j) {
-      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
-      rx[j] = (in && xg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int j = 0; j < NXL; ++j) rx[j] = src[xg[j] < 0 ? 0 : xg[j]];
   };
   auto store_x = [&](int zi, const float4 (&rx)[NXL]) {
     float* d = xsl + ((zi + 5) % 5) * XS;
+    const bool in = zi >= 0 && zi < Di;
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
+        const float4 v = in ? rx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         float2* p = reinterpret_cast<float2*>(d + xl[j]);
-        p[0] = make_float2(rx[j].x, rx[j].y);
-        p[1] = make_float2(rx[j].z, rx[j].w);
+        p[0] = make_float2(v.x, v.y);
+        p[1] = make_float2(v.z, v.w);
       }
   };
   auto load_g = [&](int z) {
 #pragma unroll
     for (int j = 0; j < NGL; ++j) {
-      const float4 v = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
-      rg[j] = gg[j] >= 0 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      rg[j] = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
     }
   };
   auto store_g = [&](int z) {
@@ -595,11 +592,9 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
     store_x(2 * z + 1, rx1);
     store_g(z);
     __syncthreads();
-    if (z + 1 < z1) {
-      load_x(2 * z + 2, rx0);
-      load_x(2 * z + 3, rx1);
-      load_g(z + 1);
-    }
+    load_x(2 * z + 2, rx0);  // unconditionally (see k_conv3d_wgrad_zm)
+    load_x(2 * z + 3, rx1);
+    load_g(z + 1 < z1 ? z + 1 : z);
     const float* ga = gsl + (z & 1) * GS + aoff;
     const float* xp[3] = {xsl + ((2 * z - 1 + 5) % 5) * XS + boff, xsl + ((2 * z) % 5) * XS + boff,
                           xsl + ((2 * z + 1) % 5) * XS + boff};
@@ -719,30 +714,28 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
   }
   const int64_t iplane4 = iplane / 4, oplane4 = oplane / 4;
   float4 rx0[NXL], rx1[NXL], rg[NGL];
-  auto load_x = [&](int zi, float4 (&rx)[NXL]) {
+  auto load_x = [&](int zi, float4 (&rx)[NXL]) {  // (zero outside [0, Di) at the store)
     const bool in = zi >= 0 && zi < Di;
     const float4* src = reinterpret_cast<const float4*>(Xb) + (int64_t)(in ? zi : 0) * iplane4;
 #pragma unroll
-    for (int j = 0; j < NXL; ++j) {
-      const float4 v = src[xg[j] < 0 ? 0 : xg[j]];
-      rx[j] = (in && xg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int j = 0; j < NXL; ++j) rx[j] = src[xg[j] < 0 ? 0 : xg[j]];
   };
   auto store_x = [&](int zi, const float4 (&rx)[NXL]) {
     float* d = xsl + ((zi + 5) % 5) * XS;
+    const bool in = zi >= 0 && zi < Di;
 #pragma unroll
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) {
+        const float4 v = in ? rx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         float2* p = reinterpret_cast<float2*>(d + xl[j]);
-        p[0] = make_float2(rx[j].x, rx[j].y);
-        p[1] = make_float2(rx[j].z, rx[j].w);
+        p[0] = make_float2(v.x, v.y);
+        p[1] = make_float2(v.z, v.w);
       }
   };
   auto load_g = [&](int z) {
 #pragma unroll
     for (int j = 0; j < NGL; ++j) {
-      const float4 v = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
-      rg[j] = gg[j] >= 0 ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      rg[j] = (reinterpret_cast<const float4*>(Gb) + (int64_t)z * oplane4)[gg[j] < 0 ? 0 : gg[j]];
     }
   };
   auto store_g = [&](int z) {
@@ -775,11 +768,9 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
     store_x(2 * z + 1, rx1);
     store_g(z);
     __syncthreads();
-    if (z + 1 < z1) {
-      load_x(2 * z + 2, rx0);
-      load_x(2 * z + 3, rx1);
-      load_g(z + 1);
-    }
+    load_x(2 * z + 2, rx0);  // unconditionally (see k_conv3d_wgrad_zm)
+    load_x(2 * z + 3, rx1);
+    load_g(z + 1 < z1 ? z + 1 : z);
     const float* ga = gsl + (z & 1) * GS + li * a.MS + lk;
     const float* xp[3] = {xsl + ((2 * z - 1 + 5) % 5) * XS + boff, xsl + ((2 * z) % 5) * XS + boff,
                           xsl + ((2 * z + 1) % 5) * XS + boff};
@@ -910,6 +901,8 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf1(Zf1Args a) {
     for (int j = 0; j < NXL; ++j)
       if (xg[j] >= 0) *reinterpret_cast<float4*>(xsl + slot * a.XS + xl[j]) = r[j];
   };
+  // (zero-selects at the load here: with three steps' slabs in flight the early wait costs nothing, and
+  // the store-side selects of k_conv3d_wgrad_zm measured slower for this kernel, 410 -> 430 us)
   auto load_g = [&](int pz, float4 (&r)[NGL]) {  // G plane pz (zero outside [0, D))
     const bool in = pz >= 0 && pz < D;
     const float4* src = reinterpret_cast<const float4*>(Gb) + (int64_t)(in ? pz : 0) * plane4;
@@ -919,16 +912,16 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf1(Zf1Args a) {
       r[j] = (in && gg[j] >= 0) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store_g = [&](int slot, const float4 (&r)[NGL]) {
+  auto store_g = [&](int slot, const float4 (&r)[NGL], int) {
 #pragma unroll
     for (int j = 0; j < NGL; ++j)
       if (gg[j] >= 0) *reinterpret_cast<float4*>(gsl + slot * a.GS + gl[j]) = r[j];
   };
   __syncthreads();
   load_g(z0 - 1, rg[0]);
-  store_g((z0 + 3) & 3, rg[0]);
+  store_g((z0 + 3) & 3, rg[0], z0 - 1);
   load_g(z0, rg[0]);
-  store_g(z0 & 3, rg[0]);
+  store_g(z0 & 3, rg[0], z0);
 #pragma unroll
   for (int p = 0; p < ZP; ++p) {
     load_x(z0 + p, rx[p]);
@@ -955,7 +948,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf1(Zf1Args a) {
   for (int t = 0; t < 2; ++t) acc[0][t] = acc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto step = [&](int zi, float4 (&rxp)[NXL], float4 (&rgp)[NGL]) {
     store_x(zi & 1, rxp);
-    store_g((zi + 1) & 3, rgp);
+    store_g((zi + 1) & 3, rgp, zi + 1);
     __syncthreads();
     if (zi + ZP < z1) {
       load_x(zi + ZP, rxp);
