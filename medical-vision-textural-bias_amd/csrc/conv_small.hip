@@ -173,9 +173,32 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
   const int r = tid / tpr, w0 = (tid - r * tpr) * WPT;
   const bool act = r < ROWS && h0 + r < H;
   const int zend = z0 + ZB < D ? z0 + ZB : D;
+  const int h = h0 + r;
+  // step z: fetch plane z + 2 | store step z - 1's outputs | FMAs of plane z into registers | wait, barrier.
+  // The outputs leave one step late, so the wait for the fetch never waits for the step's own stores
+  // (the residual `add` values are loaded at the start of their step, used a step later).
+  float prev[CO][WPT], padd[CO][WPT];
+  auto put = [&](int zp) {
+#pragma unroll
+    for (int co = 0; co < CO; ++co) {
+      const int64_t o = ((int64_t)n * CO + co) * vol + (int64_t)zp * plane + (int64_t)h * W + w0;
+#pragma unroll
+      for (int k = 0; k < WPT; ++k)
+        if (w0 + k < W) y[o + k] = ADD ? prev[co][k] + padd[co][k] : prev[co][k];
+    }
+  };
   for (int z = z0; z < zend; ++z) {
     if (z + 2 < zend + 1) stage(z + 2);  // the next plane's fetch overlaps this plane's FMAs
     if (act) {
+      if (z > z0) put(z - 1);
+      if (ADD) {
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+          const int64_t o = ((int64_t)n * CO + co) * vol + (int64_t)z * plane + (int64_t)h * W + w0;
+#pragma unroll
+          for (int k = 0; k < WPT; ++k) padd[co][k] = w0 + k < W ? add[o + k] : 0.f;
+        }
+      }
       float acc[CO][WPT];
 #pragma unroll
       for (int co = 0; co < CO; ++co) {
@@ -205,24 +228,15 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
           }
         }
       }
-      const int h = h0 + r;
 #pragma unroll
-      for (int co = 0; co < CO; ++co) {
-        const int64_t o = ((int64_t)n * CO + co) * vol + (int64_t)z * plane + (int64_t)h * W + w0;
-        float* dst = y + o;
-        if (ADD) {  // the ResidualUnit's identity sum (forward) / its gradient's pass-through (backward)
+      for (int co = 0; co < CO; ++co)
 #pragma unroll
-          for (int k = 0; k < WPT; ++k)
-            if (w0 + k < W) acc[co][k] += add[o + k];
-        }
-#pragma unroll
-        for (int k = 0; k < WPT; ++k)
-          if (w0 + k < W) dst[k] = acc[co][k];
-      }
+        for (int k = 0; k < WPT; ++k) prev[co][k] = acc[co][k];
     }
-    __builtin_amdgcn_s_waitcnt(0);  // plane z + 2 landed (this wave's share)
+    __builtin_amdgcn_s_waitcnt(0);  // plane z + 2 landed (this wave's share; the stores were issued a step ago)
     __syncthreads();                // ... and every wave's; slot of z - 1 free for plane z + 3
   }
+  if (act && zend > z0) put(zend - 1);
 }
 
 template <int CI, int CO>
