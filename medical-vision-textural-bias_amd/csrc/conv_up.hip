@@ -116,14 +116,29 @@ __global__ __launch_bounds__(NTH) void k_conv_s2_fewin(S2Args a) {
   }
   const int64_t oplane = (int64_t)a.Ho * Wo;
   float* outb = a.out + (int64_t)n * MOUT * a.Do * oplane + (int64_t)(y0 + oy) * Wo + ox;
+  // LATE (the 256-thread form): outputs leave one step late (pend), after the next planes' loads, so the
+  // wait for those loads at the next step's LDS store never includes a store issued in the same step
+  // (3 -> 32: 225 -> 212 us; the 512-thread 4 -> 32 form measured 278 -> 317 us with it: immediate stores)
+  constexpr bool LATE = NTH == 256;
+  f2v pend[MP];
+  auto put = [&](int zp) {
+    float* o = outb + (int64_t)zp * oplane;
+#pragma unroll
+    for (int mm = 0; mm < MP; ++mm) {
+      const int m = mh * MP + mm;
+      o[(int64_t)(2 * m) * a.Do * oplane] = pend[mm].x;
+      o[(int64_t)(2 * m + 1) * a.Do * oplane] = pend[mm].y;
+    }
+  };
   for (int z = z0; z < z1; ++z) {
     store(2 * z, ra);
     store(2 * z + 1, rb);
     __syncthreads();
-    if (z + 1 < z1) {
+    if (LATE || z + 1 < z1) {  // (LATE: unconditionally; past the segment: never stored)
       load(2 * z + 2, ra);
       load(2 * z + 3, rb);
     }
+    if (LATE && act && z > z0) put(z - 1);
     if (act) {
       // the position's 27 CIN inputs into registers, then one packed FMA chain per output pair
       float v[CIN * 27];
@@ -138,19 +153,24 @@ __global__ __launch_bounds__(NTH) void k_conv_s2_fewin(S2Args a) {
             for (int tx = 0; tx < 3; ++tx) v[c * 27 + tz * 9 + ty * 3 + tx] = sl[(c * NR + ty) * PX + tx];
       }
       const cf2v_p kp = (cf2v_p)(cfloat_p)a.K;
-      float* o = outb + (int64_t)z * oplane;
 #pragma unroll
       for (int mm = 0; mm < MP; ++mm) {
         const int m = mh * MP + mm;
         f2v acc = bias2[mm];
 #pragma unroll
         for (int k = 0; k < CIN * 27; ++k) acc = __builtin_elementwise_fma(f2v{v[k], v[k]}, kp[m * CIN * 27 + k], acc);
-        o[(int64_t)(2 * m) * a.Do * oplane] = acc.x;
-        o[(int64_t)(2 * m + 1) * a.Do * oplane] = acc.y;
+        if (LATE) {
+          pend[mm] = acc;
+        } else {
+          float* o = outb + (int64_t)z * oplane;
+          o[(int64_t)(2 * m) * a.Do * oplane] = acc.x;
+          o[(int64_t)(2 * m + 1) * a.Do * oplane] = acc.y;
+        }
       }
     }
     __syncthreads();  // every wave is done with this step's slots before the next step's stores
   }
+  if (LATE && act && z1 > z0) put(z1 - 1);
 }
 
 // --------------------------------------------------------------- ConvTranspose3d, few outputs
@@ -227,6 +247,7 @@ __global__ __launch_bounds__(NTH) void k_convT_fewout(TArgs a) {
 #pragma unroll
   for (int m = 0; m < MO; ++m) bia[m] = a.bias ? a.bias[m] : 0.f;
   float* yb0 = a.y + (int64_t)n * MO * Do * oplane + (int64_t)(2 * (y0 + jy)) * Wo + 2 * jx;
+  // (outputs one step late, as k_conv_s2_fewin's 256-thread form: 291 -> 317 us here, not taken)
   for (int z = z0; z < z1; ++z) {
     store(z + 1);  // plane z + 1 (zero past Di)
     __syncthreads();
