@@ -436,6 +436,7 @@ struct F16Args {
   int ZS, zlen, nyb;
   int PX, RX;  // row pitch (data at column x + 4), channel pitch (= 16 mod 32)
   int flip;    // 1: W is the layer's weight and the call its input gradient: A = W[c][m][26 - t]
+  int persist, ncol;  // k_conv3d_fwd16: persistent shares of the ncol = N nyb columns' steps
 };
 
 // NS: plane-ring slots.  3: a step's MFMAs read planes z - 1 .. z + 1, plane z + 2 goes over plane z - 1's
@@ -452,12 +453,6 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
   const int D = a.D, H = a.H, Wd = a.Wd, PX = a.PX, RX = a.RX, SS = 16 * RX;
   float* ring = smem;  // [NS][16 c][NR][PX]
   for (int i = tid; i < NS * SS; i += NTH) ring[i] = 0.f;
-  int b = (int)blockIdx.x;
-  const int zs = b % a.ZS;
-  b /= a.ZS;
-  const int yb = b % a.nyb, n = b / a.nyb;
-  const int y0 = yb * YB;
-  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
   // A fragments: lane (m = l & 15, ks = l >> 4); k-step kk = 4 t + cq covers channel 4 cq + ks at tap t
   const int li = lane & 15, ks = lane >> 4;
   float af[108];
@@ -466,6 +461,28 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
     const int c = 4 * (kk & 3) + ks, t = kk >> 2;
     af[kk] = a.flip ? a.W[(c * 16 + li) * 27 + 26 - t] : a.W[(li * 16 + c) * 27 + t];
   }
+  const float bm[4] = {a.bias ? a.bias[4 * ks] : 0.f, a.bias ? a.bias[4 * ks + 1] : 0.f,
+                       a.bias ? a.bias[4 * ks + 2] : 0.f, a.bias ? a.bias[4 * ks + 3] : 0.f};
+  // the block's steps: (n, row block, plane) linearised as column (n, yb) major, plane minor.  a.persist: a
+  // contiguous 1/gridDim share of all of them (one block per CU, every CU busy, a share spans at most a
+  // few columns, each marched on its own); else the (n, yb, z segment) of blockIdx
+  int64_t s_beg, s_end;
+  if (a.persist) {
+    const int64_t T = (int64_t)a.ncol * D;
+    s_beg = T * blockIdx.x / gridDim.x, s_end = T * (blockIdx.x + 1) / gridDim.x;
+  } else {
+    int b = (int)blockIdx.x;
+    const int zs = b % a.ZS;
+    b /= a.ZS;
+    const int zb = zs * a.zlen;
+    s_beg = (int64_t)b * D + zb, s_end = (int64_t)b * D + min(D, zb + a.zlen);
+  }
+  for (int64_t sg = s_beg; sg < s_end;) {
+  const int col = (int)(sg / D), z0 = (int)(sg - (int64_t)col * D);
+  const int z1 = (int)min((int64_t)D, z0 + (s_end - sg));
+  sg += z1 - z0;
+  const int yb = col % a.nyb, n = col / a.nyb;
+  const int y0 = yb * YB;
   const int64_t plane = (int64_t)H * Wd, plane4 = plane / 4;
   const float4* xb = reinterpret_cast<const float4*>(a.x + (int64_t)n * 16 * D * plane);
   constexpr int NL = (16 * NR * W4 + NTH - 1) / NTH;
@@ -499,8 +516,6 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
     for (int j = 0; j < NL; ++j)
       *reinterpret_cast<float4*>(d + lof[j]) = in && gof[j] >= 0 ? rg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  const float bm[4] = {a.bias ? a.bias[4 * ks] : 0.f, a.bias ? a.bias[4 * ks + 1] : 0.f,
-                       a.bias ? a.bias[4 * ks + 2] : 0.f, a.bias ? a.bias[4 * ks + 3] : 0.f};
   __syncthreads();
   load(z0 - 1);
   store(z0 - 1);
@@ -605,6 +620,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
       }
     }
     __syncthreads();
+  }
   }
 }
 }  // namespace
@@ -1062,7 +1078,16 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
     return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(NTv), lds, reinterpret_cast<hipStream_t>(stream), a);
+  // persistent shares when the (n, yb, z segment) grid leaves CUs idle (C3: 240 blocks of 256)
+  static const int persist_env = [] {
+    const char* e = std::getenv("TEXBIAS_CONV16_PERSIST");
+    return e ? std::atoi(e) : 1;
+  }();
+  a.ncol = N * a.nyb;
+  unsigned nblk = (unsigned)(N * a.nyb * a.ZS);
+  a.persist = persist_env && per_cu == 1 && (int64_t)a.ncol * D >= 8LL * ncu_count() && nblk % ncu_count() != 0;
+  if (a.persist) nblk = (unsigned)ncu_count();
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(NTv), lds, reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 

@@ -392,7 +392,6 @@ struct AdnArgs {
   int C, NC, nblk;  // nblk: statistics partials per instance (blocks of the statistics sweeps)
   float eps;
   int vec;
-  int spb;          // CHUNK sub-chunks per statistics block (the sweep sized to one round of the GPU)
 };
 
 __device__ __forceinline__ void store_d(double* p, double v) {
@@ -464,9 +463,7 @@ __device__ __forceinline__ int64_t inst_base(int nc, int C, int64_t sn, int64_t 
 __global__ __launch_bounds__(NT) void k_adn_stats(const AdnArgs a) {
   double s1 = 0.0, s2 = 0.0;
   const int nc = blockIdx.y;
-  for (int sc = 0; sc < a.spb; ++sc) {
-  const int64_t b = ((int64_t)blockIdx.x * a.spb + sc) * CHUNK;
-  if (b >= a.S) break;
+  const int64_t b = (int64_t)blockIdx.x * CHUNK;
   const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
   const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
   if (a.vec) {
@@ -489,7 +486,6 @@ __global__ __launch_bounds__(NT) void k_adn_stats(const AdnArgs a) {
       s1 += v;
       s2 += v * v;
     }
-  }
   }
   double in[2] = {s1, s2}, tot[2];
   block_sum<2>(in, tot);
@@ -560,9 +556,7 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
     sa += pos ? 0.0 : (double)gv * z;
     sz += in ? z : 0.0;
   };
-  for (int sc = 0; sc < a.spb; ++sc) {
-  const int64_t b = ((int64_t)blockIdx.x * a.spb + sc) * CHUNK;
-  if (b >= a.S) break;
+  const int64_t b = (int64_t)blockIdx.x * CHUNK;
   const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
   const float* xp = a.x + inst_base(nc, a.C, a.xsn, a.S) + b;
   const float* gp = a.dy + inst_base(nc, a.C, a.dysn, a.S) + b;
@@ -590,7 +584,6 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
     }
   } else {
     for (int64_t i = threadIdx.x; i < e - b; i += NT) visit(xp[i], gp[i]);
-  }
   }
   double in[4] = {s1, s2, sa, sz}, tot[4];
   block_sum<4>(in, tot);
@@ -828,10 +821,8 @@ int tb_dice_loss_bwd_f32(const double* sums, const float* gloss, float* gsums, i
 // ------------------------------------------------------------------ strided, memset-free ADN: host
 namespace {
 inline int adn_nblk(int64_t S) { return (int)((S + CHUNK - 1) / CHUNK); }
-// CHUNK sub-chunks per statistics block.  One (measured: sizing the sweep to one round of <= 2048
-// multi-chunk blocks took the C3 statistics sweeps from 17.4 / 35.0 to 23.6 / 36.9 us per call -- fewer
-// loads in flight)
-inline int adn_spb(int64_t, int64_t) { return 1; }
+// (one statistics block per CHUNK: sizing the sweep to one round of <= 2048 multi-chunk blocks measured
+// 17.4 / 35.0 -> 23.6 / 36.9 us per C3 call -- fewer loads in flight)
 inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 }  // namespace
 
@@ -855,8 +846,7 @@ int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const flo
   a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
   a.inst = a.part + N * C * adn_nblk(S) * 4;
   a.cnt = counters;
-  a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.eps = eps;
-  a.spb = adn_spb(N * C, S), a.nblk = (adn_nblk(S) + a.spb - 1) / a.spb;
+  a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S), a.eps = eps;
   a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.rsn % 4 == 0 && al16(x) && al16(y) && al16(res);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_adn_stats, dim3((unsigned)a.nblk, (unsigned)a.NC), dim3(NT), 0, st, a);
@@ -879,8 +869,7 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
   a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
   a.inst = a.part + N * C * adn_nblk(S) * 4;
   a.cnt = counters;
-  a.S = S, a.C = (int)C, a.NC = (int)(N * C);
-  a.spb = adn_spb(N * C, S), a.nblk = (adn_nblk(S) + a.spb - 1) / a.spb;
+  a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S);
   a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.dysn % 4 == 0 && al16(x) && al16(dy) && al16(dx);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)adn_nblk(S), (unsigned)a.NC);
