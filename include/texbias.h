@@ -254,9 +254,10 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
 int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D,
                             int H, int Wd, void* stream);
 /* The layer's input gradient dX = conv(dY, W') (+ add) with W' = W[c][m][26 - t] read in the kernel from the
- * layer's own weight W [16][16][3][3][3] (no flipped copy); gy, add, dx [N][16][D][H][W]. */
-int tb_conv3d_fwd16_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int D, int H, int Wd,
-                              void* stream);
+ * layer's own weight W [16][16][3][3][3] (no flipped copy); gy, dx [N][16][D][H][W]; add (or NULL) the same
+ * per sample, add_sn floats apart (0: contiguous; a channel slice of a wider tensor otherwise). */
+int tb_conv3d_fwd16_dgrad_f32(const float* gy, const float* W, const float* add, int64_t add_sn, float* dx, int N, int D,
+                              int H, int Wd, void* stream);
 
 /* ConvTranspose3d(64 -> 16, 3, stride 2, padding 1, output_padding 1) forward on the f32 matrix cores
  * (sub-pixel form, all 27 taps real): x [N][64][Di][Hi][Wi] -> y [N][16][2Di][2Hi][2Wi], weight

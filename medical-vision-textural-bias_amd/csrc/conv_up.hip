@@ -437,6 +437,7 @@ struct F16Args {
   int PX, RX;  // row pitch (data at column x + 4), channel pitch (= 16 mod 32)
   int flip;    // 1: W is the layer's weight and the call its input gradient: A = W[c][m][26 - t]
   int persist, ncol;  // k_conv3d_fwd16: persistent shares of the ncol = N nyb columns' steps
+  int64_t addsn;      // floats between samples of `add` (0: 16 D H W, contiguous)
 };
 
 // NS: plane-ring slots.  3: a step's MFMAs read planes z - 1 .. z + 1, plane z + 2 goes over plane z - 1's
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
   const int bl = ks * RX + li + 3;
   const int64_t oplane = plane;
   float* yb0 = a.y + (int64_t)n * 16 * D * oplane;
-  const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * oplane : nullptr;
+  const float* ab0 = ADD ? a.add + (int64_t)n * (a.addsn ? a.addsn : 16 * D * oplane) : nullptr;
   constexpr int NT = YB * NXT;                        // tiles per step
   constexpr int NIT = (NT + 2 * NWV - 1) / (2 * NWV);  // tile pairs per wave
   // step z: fetch plane z + 2 (registers) | MFMAs over planes z - 1 .. z + 1 | barrier | plane z + 2 into
@@ -540,6 +541,26 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
   for (int z = z0; z < z1; ++z) {
     const bool more = z + 1 < z1;
     if (more) load(z + 2);
+    // ADD: the step's `add` values fetched now, summed at the stores after the MFMAs (loaded at the store
+    // they would be waited for there)
+    float av[NIT][2][4];
+    if constexpr (ADD) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int t0 = wave + 2 * NWV * it;
+        if (t0 >= NT) break;
+        const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
+        const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
+        const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
+        const int ya = min(y0 + yy0, H - 1), yc = min(y0 + yy1, H - 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 4 * ks + r;
+          av[it][0][r] = ab0[((int64_t)m * D + z) * oplane + (int64_t)ya * Wd + x00 + li];
+          av[it][1][r] = ab0[((int64_t)m * D + z) * oplane + (int64_t)yc * Wd + x01 + li];
+        }
+      }
+    }
     const float* s0 = ring + ((z + NS - 1) % NS) * SS + bl;  // tz = 0: plane z - 1
     const float* s1 = ring + (z % NS) * SS + bl;
     const float* s2 = ring + ((z + 1) % NS) * SS + bl;
@@ -615,8 +636,8 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
         const int m = 4 * ks + r;
         const int64_t o0 = ((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy0) * Wd + x00 + li;
         const int64_t o1 = ((int64_t)m * D + z) * oplane + (int64_t)(y0 + yy1) * Wd + x01 + li;
-        if (y0 + yy0 < H) yb0[o0] = ADD ? acc[it][0][r] + ab0[o0] : acc[it][0][r];
-        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc[it][1][r] + ab0[o1] : acc[it][1][r];
+        if (y0 + yy0 < H) yb0[o0] = ADD ? acc[it][0][r] + av[it][0][r] : acc[it][0][r];
+        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc[it][1][r] + av[it][1][r] : acc[it][1][r];
       }
     }
     __syncthreads();
@@ -992,20 +1013,20 @@ int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float
 }
 
 static int fwd16_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
-                      int Wd, int flip, void* stream);
+                      int Wd, int flip, void* stream, int64_t add_sn = 0);
 
 int tb_conv3d_fwd16_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D,
                             int H, int Wd, void* stream) {
   return fwd16_call(x, W, bias, add, y, N, D, H, Wd, 0, stream);
 }
 
-int tb_conv3d_fwd16_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int D, int H, int Wd,
-                              void* stream) {
-  return fwd16_call(gy, W, nullptr, add, dx, N, D, H, Wd, 1, stream);
+int tb_conv3d_fwd16_dgrad_f32(const float* gy, const float* W, const float* add, int64_t add_sn, float* dx, int N, int D,
+                              int H, int Wd, void* stream) {
+  return fwd16_call(gy, W, nullptr, add, dx, N, D, H, Wd, 1, stream, add_sn);
 }
 
 static int fwd16_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
-                      int Wd, int flip, void* stream) {
+                      int Wd, int flip, void* stream, int64_t add_sn) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
   if (conv_x3_on() && Wd <= 112 && !flip)
@@ -1026,6 +1047,7 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
   F16Args a{};
   a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.flip = flip;
+  a.addsn = add_sn;
   a.PX = Wd + 8;
   a.RX = (YB + 2) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;

@@ -124,6 +124,9 @@ GEMM_1 = os.environ.get("TEXBIAS_CONVGEMM_1X1", "0") != "0"
 # ConvTranspose3d input gradient (a stride-2 Conv3d of dY) on the GEMM kernel while its forward stays on MIOpen
 # (off: up2 128 -> 32 at C3 measured 2 x 100 us + reduce in the step vs MIOpen/CK's 152 us)
 GEMM_TDX = os.environ.get("TEXBIAS_CONVGEMM_TDX", "0") != "0"
+# the identity-residual unit's input gradient dconv(dY) + dY summed in the 16-channel kernel's store (its add
+# values fetched at the start of each step), instead of a separate add pass
+FWD16_DX_ADD = os.environ.get("TEXBIAS_FWD16_DX_ADD", "1") != "0"
 
 
 def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:
@@ -299,14 +302,23 @@ def conv_fwd16(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
     return y
 
 
-def conv_fwd16_dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def conv_fwd16_dgrad(gy: torch.Tensor, w: torch.Tensor, add=None) -> torch.Tensor:
     """The input gradient of Conv3d(16 -> 16, 3, 1, 1) with weight ``w``: the forward kernel reading
-    W[c][m][26 - t] in place of a flipped, transposed copy (tb_conv3d_fwd16_dgrad_f32)."""
+    W[c][m][26 - t] in place of a flipped, transposed copy (tb_conv3d_fwd16_dgrad_f32); ``add`` (the
+    output's shape; a channel slice of a wider tensor is read in place) summed into the store."""
     gy = gy.contiguous()
     N, _, D, H, W = gy.shape
     dx = torch.empty_like(gy)
+    sn = 0
+    if add is not None:
+        S = D * H * W
+        if not (tuple(add.shape) == tuple(gy.shape) and add.stride(1) == S and add[0, 0].is_contiguous() and
+                add.data_ptr() % 4 == 0):
+            add = add.contiguous()
+        sn = add.stride(0)
     with torch.cuda.device(gy.device):
-        check(lib().tb_conv3d_fwd16_dgrad_f32(gy.data_ptr(), w.contiguous().data_ptr(), None, dx.data_ptr(),
+        check(lib().tb_conv3d_fwd16_dgrad_f32(gy.data_ptr(), w.contiguous().data_ptr(),
+                                              add.data_ptr() if add is not None else None, sn, dx.data_ptr(),
                                               N, D, H, W, _stream(gy)), "tb_conv3d_fwd16_dgrad_f32")
     return dx
 
@@ -495,7 +507,9 @@ class Route:
     def input_grad(self, gy, x, w, add=None):
         k = self.dx
         if add is not None:  # (a strided add -- a channel slice of the skip concatenation's gradient -- is
-            if k == "small":  # copied only for the kernels that read it)
+            if k == "fwd16" and FWD16_DX_ADD:  # copied only for the kernels that need it contiguous)
+                return conv_fwd16_dgrad(gy, w, add)
+            if k == "small":
                 return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None, add.contiguous())
             if k == "gemm" and not self.transposed and self.stride[0] == 1:
                 return conv_gemm(gy, w, None, "dgrad", 1, w.shape[2], add=add.contiguous())
