@@ -282,9 +282,9 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
 int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C,
                            int D, int H, int Wd, void* stream);
 /* The layer's input gradient with the flipped, transposed weight read in the kernel from W [C][C][3][3][3]
- * (as tb_conv3d_fwd16_dgrad_f32). */
-int tb_conv3d_mfma_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int C, int D, int H,
-                             int Wd, void* stream);
+ * (as tb_conv3d_fwd16_dgrad_f32, `add` add_sn floats apart per sample). */
+int tb_conv3d_mfma_dgrad_f32(const float* gy, const float* W, const float* add, int64_t add_sn, float* dx, int N, int C,
+                             int D, int H, int Wd, void* stream);
 
 /*
  * The U-Net's channel-deep convolutions as implicit GEMMs on the f32 matrix cores (csrc/conv_gemm.hip;

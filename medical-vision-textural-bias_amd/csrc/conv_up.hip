@@ -1335,6 +1335,7 @@ struct S1Args {
   int ZS, zlen, nyb, MG;  // z segments, row blocks, output-tile groups
   int PX, RX;             // row pitch (data at column x + 4), channel pitch (16 mod 32)
   int flip;               // 1: W is the layer's weight and the call its input gradient (W[c][m][26 - t])
+  int64_t addsn;          // floats between samples of `add` (0: contiguous)
 };
 
 template <int G, int NC, int NL, int NTH, bool ADD = false>  // NTH 512: two waves per role, alternate tiles
@@ -1410,7 +1411,8 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
   // the host sizes YB so that a step's positions fit the block's NWG x NC chains: one tile round per step
   const int npos = YB * Wd;
   float* ybase = a.y + (int64_t)n * COUT * cstride;
-  const float* abase = ADD ? a.add + (int64_t)n * COUT * cstride : nullptr;
+  const float* abase = ADD ? a.add + (int64_t)n * (a.addsn ? a.addsn : COUT * cstride) : nullptr;
+  constexpr int NK = (MTB * NWG * NC + NTH / 64 - 1) / (NTH / 64);  // sum-phase combos per wave
   int bl[NC];  // chain c of this wave: position tile NWG c + h
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -1422,6 +1424,22 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
   // z + 2 over plane z - 1's slot, the partials summed and stored | barrier
   for (int z = z0; z < z1; ++z) {
     if (z + 1 < z1) load(z + 2);
+    // ADD: the step's `add` values fetched now, summed in the store phase (as in k_conv3d_fwd16)
+    float av[NK][4];
+    if constexpr (ADD) {
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int k = w + kk * (NTH / 64);
+        if (k >= MTB * NWG * NC) break;
+        const int mq = k / (NWG * NC), r2 = k - mq * (NWG * NC), hq = r2 / NC, c = r2 - hq * NC;
+        const int p = 16 * (NWG * c + hq) + li, pc = p < npos ? p : npos - 1;
+        const int yy = pc / Wd, xx = pc - yy * Wd, yr = min(y0 + yy, H - 1);
+        const int mb = (mg * MTB + mq) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          av[kk][r] = abase[(int64_t)(mb + 4 * ks + r) * cstride + (int64_t)z * plane + (int64_t)yr * Wd + xx];
+      }
+    }
     const float* sp[3] = {ring + ((z + 2) % 3) * SS, ring + (z % 3) * SS, ring + ((z + 1) % 3) * SS};
     f32x4 acc[NC];
 #pragma unroll
@@ -1449,7 +1467,9 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
     __syncthreads();
     store(z + 2);  // unconditionally (after the last step a dead slot)
     // (output tile mt', phase h', chain c) combos over the waves: the G groups' partials summed + bias
-    for (int k = w; k < MTB * NWG * NC; k += NTH / 64) {
+    // (k, kk): sum-phase combo k = w + kk * waves; kk indexes the prefetched add values (ADD only: the
+    // unrolled form keeps them in registers; the plain form keeps the runtime loop and its register count)
+    auto combo = [&](int k, int kk) {
       const int mq = k / (NWG * NC), r2 = k - mq * (NWG * NC), hq = r2 / NC, c = r2 - hq * NC;
       const int p = 16 * (NWG * c + hq) + li;
       const int yy = p / Wd, xx = p - yy * Wd;
@@ -1462,8 +1482,18 @@ __global__ __launch_bounds__(NTH) void k_conv3d_mfma_s1(S1Args a) {  // (NWG pha
 #pragma unroll
         for (int gg = 0; gg < G; ++gg) v += part[((hq * 4 + mq * G + gg) * NC + c) * 256 + m * 16 + li];
         const int64_t o = (int64_t)(mb + m) * cstride + (int64_t)z * plane + (int64_t)(y0 + yy) * Wd + xx;
-        if (ok) ybase[o] = ADD ? v + abase[o] : v;
+        if (ok) ybase[o] = ADD ? v + av[kk][r] : v;
       }
+    };
+    if constexpr (ADD) {
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int k = w + kk * (NTH / 64);
+        if (k >= MTB * NWG * NC) break;
+        combo(k, kk);
+      }
+    } else {
+      for (int k = w; k < MTB * NWG * NC; k += NTH / 64) combo(k, 0);
     }
     __syncthreads();
   }
@@ -1478,20 +1508,20 @@ int tb_conv3d_mfma_f32(const float* x, const float* W, const float* bias, float*
 }
 
 static int mfma_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C, int D,
-                     int H, int Wd, int flip, void* stream);
+                     int H, int Wd, int flip, void* stream, int64_t add_sn = 0);
 
 int tb_conv3d_mfma_add_f32(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C,
                            int D, int H, int Wd, void* stream) {
   return mfma_call(x, W, bias, add, y, N, C, D, H, Wd, 0, stream);
 }
 
-int tb_conv3d_mfma_dgrad_f32(const float* gy, const float* W, const float* add, float* dx, int N, int C, int D, int H,
-                             int Wd, void* stream) {
-  return mfma_call(gy, W, nullptr, add, dx, N, C, D, H, Wd, 1, stream);
+int tb_conv3d_mfma_dgrad_f32(const float* gy, const float* W, const float* add, int64_t add_sn, float* dx, int N, int C,
+                             int D, int H, int Wd, void* stream) {
+  return mfma_call(gy, W, nullptr, add, dx, N, C, D, H, Wd, 1, stream, add_sn);
 }
 
 static int mfma_call(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int C, int D,
-                     int H, int Wd, int flip, void* stream) {
+                     int H, int Wd, int flip, void* stream, int64_t add_sn) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if ((C != 32 && C != 64) || Wd % 4 != 0 || Wd > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
@@ -1508,6 +1538,7 @@ static int mfma_call(const float* x, const float* W, const float* bias, const fl
   S1Args a{};
   a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.flip = flip;
+  a.addsn = add_sn;
   a.PX = Wd + 8;
   a.MG = G == 2 ? 1 : 4;  // 32: both output tiles in the block; 64: one tile per block, 4 block groups
   size_t lds = 0;

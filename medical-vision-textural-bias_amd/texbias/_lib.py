@@ -54,7 +54,7 @@ def _proto(L):
         "tb_conv3d_small_add_f32": (I, [P, P, P, P, P] + [I] * 6 + [P]),
         "tb_conv3d_fwd16_add_f32": (I, [P, P, P, P, P] + [I] * 4 + [P]),
         "tb_conv3d_mfma_add_f32": (I, [P, P, P, P, P] + [I] * 5 + [P]),
-        "tb_conv3d_mfma_dgrad_f32": (I, [P, P, P, P] + [I] * 5 + [P]),
+        "tb_conv3d_mfma_dgrad_f32": (I, [P, P, P, I64, P] + [I] * 5 + [P]),
         "tb_conv3d_fwd16_dgrad_f32": (I, [P, P, P, I64, P] + [I] * 4 + [P]),
         "tb_conv3d_s2_fewin_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
         "tb_convT3d_fewout_f32": (I, [P, P, P, P] + [I] * 6 + [P]),

@@ -127,6 +127,9 @@ GEMM_TDX = os.environ.get("TEXBIAS_CONVGEMM_TDX", "0") != "0"
 # the identity-residual unit's input gradient dconv(dY) + dY summed in the 16-channel kernel's store (its add
 # values fetched at the start of each step), instead of a separate add pass
 FWD16_DX_ADD = os.environ.get("TEXBIAS_FWD16_DX_ADD", "1") != "0"
+# the same for the 32 / 64-channel kernel: off (its add form holds 256 VGPRs, one wave per SIMD at 32 -> 32
+# instead of two, for a 6-19 us add pass)
+MFMA_DX_ADD = os.environ.get("TEXBIAS_MFMA_DX_ADD", "0") != "0"
 
 
 def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:
@@ -344,14 +347,21 @@ def conv_mfma(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
     return y
 
 
-def conv_mfma_dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def conv_mfma_dgrad(gy: torch.Tensor, w: torch.Tensor, add=None) -> torch.Tensor:
     """The input gradient of Conv3d(C -> C, 3, 1, 1), C = 32 / 64, reading the flipped weight in the
-    kernel (tb_conv3d_mfma_dgrad_f32)."""
+    kernel (tb_conv3d_mfma_dgrad_f32); ``add`` summed into the store (a channel slice read in place)."""
     gy = gy.contiguous()
     N, C, D, H, W = gy.shape
     dx = torch.empty_like(gy)
+    sn = 0
+    if add is not None:
+        S = D * H * W
+        if not (tuple(add.shape) == tuple(gy.shape) and add.stride(1) == S and add[0, 0].is_contiguous()):
+            add = add.contiguous()
+        sn = add.stride(0)
     with torch.cuda.device(gy.device):
-        check(lib().tb_conv3d_mfma_dgrad_f32(gy.data_ptr(), w.contiguous().data_ptr(), None, dx.data_ptr(),
+        check(lib().tb_conv3d_mfma_dgrad_f32(gy.data_ptr(), w.contiguous().data_ptr(),
+                                             add.data_ptr() if add is not None else None, sn, dx.data_ptr(),
                                              N, C, D, H, W, _stream(gy)), "tb_conv3d_mfma_dgrad_f32")
     return dx
 
@@ -509,6 +519,8 @@ class Route:
         if add is not None:  # (a strided add -- a channel slice of the skip concatenation's gradient -- is
             if k == "fwd16" and FWD16_DX_ADD:  # copied only for the kernels that need it contiguous)
                 return conv_fwd16_dgrad(gy, w, add)
+            if k == "mfma" and MFMA_DX_ADD:
+                return conv_mfma_dgrad(gy, w, add)
             if k == "small":
                 return small_conv(gy, w.flip(2, 3, 4).transpose(0, 1).contiguous(), None, add.contiguous())
             if k == "gemm" and not self.transposed and self.stride[0] == 1:

@@ -180,3 +180,17 @@ def test_s2_dgrad_mfma(conv, shape):
     y64 = F.conv3d(x64, ref.weight.double(), ref.bias.double(), stride=2, padding=1)
     gx64, = torch.autograd.grad(y64, (x64,), g.double())
     close64(gx, gxr, gx64)
+
+
+@pytest.mark.parametrize("C,shape", [(16, (2, 6, 5, 32)), (32, (2, 5, 6, 12)), (64, (2, 4, 5, 8))])
+def test_dgrad_strided_add(conv, C, shape):
+    """The input-gradient kernels with the residual sum in their store, the add read in place from a
+    channel slice of a wider tensor (tb_conv3d_{fwd16,mfma}_dgrad_f32 with add_sn) vs float64."""
+    torch.manual_seed(8)
+    g = torch.randn((shape[0], C) + shape[1:], device="cuda")
+    w = torch.randn((C, C, 3, 3, 3), device="cuda") * (1.0 / (27 * C) ** 0.5)
+    wide = torch.randn((shape[0], 2 * C) + shape[1:], device="cuda")
+    add = wide[:, C:]
+    dx = conv.conv_fwd16_dgrad(g, w, add) if C == 16 else conv.conv_mfma_dgrad(g, w, add)
+    ref = F.conv_transpose3d(g.double(), w.double(), None, padding=1) + add.double()
+    assert (dx.double() - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
