@@ -127,7 +127,9 @@ constexpr int ZB = TB_SMALL_ZB;  // output planes per block
 #endif
 typedef const __attribute__((address_space(4))) float* cfloat_sp;
 
-template <int CI, int CO, bool ADD = false>
+// U: (channel, tz) groups unrolled per iteration of the z-march's FMA loop (the weights of a group are
+// scalar loads, so a deeper unroll lets more of them be issued ahead; TEXBIAS_SMALL_UNROLL 1 / 3 / 9)
+template <int CI, int CO, bool ADD = false, int U = 1>
 __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__ x, const float* __restrict__ wt,
                                                        const float* __restrict__ bias, float* __restrict__ y, int D,
                                                        int H, int W, int XP, int nhb, const float* __restrict__ add) {
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
 #pragma unroll
         for (int k = 0; k < WPT; ++k) acc[co][k] = b;
       }
-#pragma unroll 1
+#pragma unroll U
       for (int ct = 0; ct < CI * 3; ++ct) {
         const int ci = ct / 3, tz = ct - 3 * ci;
         const float* base = xs + ((z - z0 + tz) & 3) * slot_f + (ci * RS + r) * XP + w0;
@@ -252,14 +254,19 @@ int launch(const float* x, const float* w, const float* b, const float* add, flo
   }();
   const size_t lds_z = sizeof(float) * ((size_t)4 * CI * (ROWS + 2) * XP + CO * CI * 27);
   if (zmarch && lds_z <= 65536 * 2) {
-    static const hipError_t attr =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_small_z<CI, CO>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 163840) == hipSuccess
-            ? hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_small_z<CI, CO, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 163840)
-            : hipErrorInvalidValue;
-    if (attr != hipSuccess) return TB_ERR_HIP;
-    auto kern = add ? k_conv3d_small_z<CI, CO, true> : k_conv3d_small_z<CI, CO>;
+    static const int U = [] {
+      // (C3 3 -> 3 at 240 x 240 x 160, in the step: 1 / 3 / 9 = 280 / 268 / 267 us)
+      const char* e = std::getenv("TEXBIAS_SMALL_UNROLL");
+      const int v = e ? std::atoi(e) : 3;
+      return v == 1 || v == 9 ? v : 3;
+    }();
+    void (*kern)(const float*, const float*, const float*, float*, int, int, int, int, int, const float*) =
+        U == 9 ? (add ? k_conv3d_small_z<CI, CO, true, 9> : k_conv3d_small_z<CI, CO, false, 9>)
+        : U == 3 ? (add ? k_conv3d_small_z<CI, CO, true, 3> : k_conv3d_small_z<CI, CO, false, 3>)
+                 : (add ? k_conv3d_small_z<CI, CO, true, 1> : k_conv3d_small_z<CI, CO, false, 1>);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
+        hipSuccess)
+      return TB_ERR_HIP;
     hipLaunchKernelGGL(kern, dim3((unsigned)(nhb * ((D + ZB - 1) / ZB)), (unsigned)N), dim3(NT), lds_z, st, x, w, b, y,
                        D, H, W, XP, nhb, add);
     return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
