@@ -184,7 +184,7 @@ struct TArgs {
   int PX, CS;  // LDS row pitch, channel slab stride (TY + 1 rows)
 };
 
-template <int MO, int TY, int WV, int NTH = 256>
+template <int MO, int TY, int WV, int NTH = 256, int U = 1>  // U: input channels per FMA-loop iteration
 __global__ __launch_bounds__(NTH) void k_convT_fewout(TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(NTH) void k_convT_fewout(TArgs a) {
     if (act) {
       const float* s0 = ring + (z & 1) * SS + roff;
       const float* s1 = ring + ((z + 1) & 1) * SS + roff;
-#pragma unroll 1
+#pragma unroll U
       for (int c = 0; c < Cin; ++c) {
         float v[2][2][2];  // [dz][dy][dx]
         v[0][0][0] = s0[c * CS];
@@ -406,8 +406,19 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
   TB_T(1, 1) TB_T(1, 2) TB_T(1, 3) TB_T(2, 1) TB_T(2, 2) TB_T(2, 3) TB_T(3, 1) TB_T(3, 2) TB_T(3, 3) TB_T(4, 1)
   TB_T(4, 2) TB_T(4, 3)
 #undef TB_T
-  if (big) kern = Mout == 1 ? k_convT_fewout<1, 6, 20, 512> : Mout == 2 ? k_convT_fewout<2, 6, 20, 512>
-                : Mout == 3 ? k_convT_fewout<3, 6, 20, 512> : k_convT_fewout<4, 6, 20, 512>;
+  // (channels per FMA-loop iteration of the 512-thread form: TEXBIAS_CONVT_FEW_UNROLL 1 / 2 / 4 = 296 / 294 /
+  // 311 us for the C3 32 -> 3 layer: one)
+  static const int U = [] {
+    const char* e = std::getenv("TEXBIAS_CONVT_FEW_UNROLL");
+    const int v = e ? std::atoi(e) : 1;
+    return v == 2 || v == 4 ? v : 1;
+  }();
+  if (big && Mout == 3)
+    kern = U == 4 ? k_convT_fewout<3, 6, 20, 512, 4> : U == 2 ? k_convT_fewout<3, 6, 20, 512, 2>
+                                                      : k_convT_fewout<3, 6, 20, 512>;
+  else if (big)
+    kern = Mout == 1 ? k_convT_fewout<1, 6, 20, 512> : Mout == 2 ? k_convT_fewout<2, 6, 20, 512>
+                                                     : k_convT_fewout<4, 6, 20, 512>;
   if (!kern) return TB_ERR_UNSUPPORTED_SIZE;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
       hipSuccess)
