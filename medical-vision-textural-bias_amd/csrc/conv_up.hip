@@ -1087,8 +1087,9 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
     const char* e = std::getenv("TEXBIAS_CONV16_PF");
     return !(e && std::atoi(e) == 0);
   }();
-  if (PFv && !add && YB == 3 && NTv == 512 && Wd == 80) {
-    kern = NS == 4 ? k_conv3d_fwd16<3, 5, 512, false, true, 4> : k_conv3d_fwd16<3, 5, 512, false, true, 3>;
+  if (PFv && YB == 3 && NTv == 512 && Wd == 80) {
+    kern = add ? (NS == 4 ? k_conv3d_fwd16<3, 5, 512, true, true, 4> : k_conv3d_fwd16<3, 5, 512, true, true, 3>)
+               : (NS == 4 ? k_conv3d_fwd16<3, 5, 512, false, true, 4> : k_conv3d_fwd16<3, 5, 512, false, true, 3>);
   } else
 #define TB_F16C(Y, X, T) \
   kern = add ? (NS == 4 ? k_conv3d_fwd16<Y, X, T, true, false, 4> : k_conv3d_fwd16<Y, X, T, true, false, 3>) \
