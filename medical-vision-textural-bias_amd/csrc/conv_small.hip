@@ -19,6 +19,7 @@
 #include <cstdlib>
 
 #include "texbias.h"
+#include "kernels.h"
 
 namespace {
 
@@ -128,7 +129,7 @@ constexpr int ZB = TB_SMALL_ZB;  // output planes per block
 typedef const __attribute__((address_space(4))) float* cfloat_sp;
 
 // U: (channel, tz) groups unrolled per iteration of the z-march's FMA loop (the weights of a group are
-// scalar loads, so a deeper unroll lets more of them be issued ahead; TEXBIAS_SMALL_UNROLL 1 / 3 / 9)
+// scalar loads, so a deeper unroll lets more of them be issued ahead; 1 / 3 / 9 measured 280 / 268 / 267 us: 3)
 template <int CI, int CO, bool ADD = false, int U = 1>
 __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__ x, const float* __restrict__ wt,
                                                        const float* __restrict__ bias, float* __restrict__ y, int D,
@@ -241,6 +242,10 @@ __global__ __launch_bounds__(NT) void k_conv3d_small_z(const float* __restrict__
   if (act && zend > z0) put(zend - 1);
 }
 
+__global__ __launch_bounds__(256) void k_add_inplace(float* __restrict__ y, const float* __restrict__ a, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] += a[i];
+}
+
 template <int CI, int CO>
 int launch(const float* x, const float* w, const float* b, const float* add, float* y, int N, int D, int H, int W,
            hipStream_t st) {
@@ -248,32 +253,22 @@ int launch(const float* x, const float* w, const float* b, const float* add, flo
   const size_t lds = sizeof(float) * ((size_t)CI * 3 * (ROWS + 2) * XP + CO * CI * 27);
   if ((W + WPT - 1) / WPT * ROWS > NT || lds > 65536 || XP > 64 * kSeg) return TB_ERR_UNSUPPORTED_SIZE;
   const int nhb = (H + ROWS - 1) / ROWS;
-  static const bool zmarch = [] {
-    const char* e = std::getenv("TEXBIAS_SMALL_CONV_Z");
-    return !(e && e[0] == '0');
-  }();
   const size_t lds_z = sizeof(float) * ((size_t)4 * CI * (ROWS + 2) * XP + CO * CI * 27);
-  if (zmarch && lds_z <= 65536 * 2) {
-    static const int U = [] {
-      // (C3 3 -> 3 at 240 x 240 x 160, in the step: 1 / 3 / 9 = 280 / 268 / 267 us)
-      const char* e = std::getenv("TEXBIAS_SMALL_UNROLL");
-      const int v = e ? std::atoi(e) : 3;
-      return v == 1 || v == 9 ? v : 3;
-    }();
+  if (lds_z <= 65536 * 2) {  // z-march (3 (channel, tz) groups per FMA-loop iteration)
     void (*kern)(const float*, const float*, const float*, float*, int, int, int, int, int, const float*) =
-        U == 9 ? (add ? k_conv3d_small_z<CI, CO, true, 9> : k_conv3d_small_z<CI, CO, false, 9>)
-        : U == 3 ? (add ? k_conv3d_small_z<CI, CO, true, 3> : k_conv3d_small_z<CI, CO, false, 3>)
-                 : (add ? k_conv3d_small_z<CI, CO, true, 1> : k_conv3d_small_z<CI, CO, false, 1>);
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
-        hipSuccess)
-      return TB_ERR_HIP;
+        add ? k_conv3d_small_z<CI, CO, true, 3> : k_conv3d_small_z<CI, CO, false, 3>;
+    if (tb::allow_full_lds(kern) != hipSuccess) return TB_ERR_HIP;  // once per kernel (kernels.h)
     hipLaunchKernelGGL(kern, dim3((unsigned)(nhb * ((D + ZB - 1) / ZB)), (unsigned)N), dim3(NT), lds_z, st, x, w, b, y,
                        D, H, W, XP, nhb, add);
     return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
   }
-  if (add) return TB_ERR_UNSUPPORTED_SIZE;  // the plane-per-block fallback has no residual epilogue
   hipLaunchKernelGGL((k_conv3d_small<CI, CO>), dim3((unsigned)(nhb * D), (unsigned)N), dim3(NT), lds, st, x, w, b, y,
                      D, H, W, XP, nhb);
+  if (add) {  // the plane-per-block kernel has no residual epilogue: a separate y += add pass
+    const int64_t n = (int64_t)N * CO * D * H * W;
+    hipLaunchKernelGGL(k_add_inplace, dim3((unsigned)((n + 1023) / 1024 < 8192 ? (n + 1023) / 1024 : 8192)), dim3(256),
+                       0, st, y, add, n);
+  }
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 

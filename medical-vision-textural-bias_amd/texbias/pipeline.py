@@ -246,6 +246,8 @@ class FusedChain:
         nst = len(plans[0])
         if any(len(p) != nst or [s[0] for s in p] != [s[0] for s in plans[0]] for p in plans):
             raise ValueError("all samples of a batch must share the stage structure")
+        if out is not None and any(s[0] == "sel" for s in plans[0]):
+            raise ValueError("out= cannot take a chain with a channel selection (its result has fewer channels)")
         if self._mm is None or self._mm.shape[0] < B or self._mm.device != x.device:
             self._mm = torch.empty((max(B, 8), 2), dtype=torch.int32, device=x.device)
         mm = self._mm[:B]
@@ -329,6 +331,8 @@ class FusedChain:
         elif pad and not padded:
             cur = torch.nn.functional.pad(cur, (0, pad))
         if out is not None and cur is not out:
+            if tuple(cur.shape) != tuple(out.shape):  # e.g. a channel-selection stage: no silent broadcast
+                raise ValueError(f"the chain's result {tuple(cur.shape)} does not fit out {tuple(out.shape)}")
             out.copy_(cur)
             cur = out
         return cur

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from .losses import DiceLoss
-from .unet import UNet
+from .unet import UNet, pack_parameters
 
 
 def dist_env() -> Tuple[int, int, int]:
@@ -58,6 +58,7 @@ class TrainStep:
         self.device = device
         self.channels_last = channels_last
         model = model.to(device)
+        pack_parameters(model)  # strided units' [unit0; residual] weights in one storage (unet.py), before DDP/Adam
         if channels_last:
             model = model.to(memory_format=torch.channels_last_3d)
         self.module = model

@@ -216,6 +216,18 @@ class ResidualUnit(nn.Module):
             self.residual = Conv3d(cin, cout, k, stride=strides, padding=p)
         else:
             self.residual = nn.Identity()
+        self._register_state_dict_hook(ResidualUnit._unshare_packed)
+
+    @staticmethod
+    def _unshare_packed(module, state_dict, prefix, local_metadata):
+        """state_dict of a packed unit: its unit-0 / residual tensors as copies of their own, so a checkpoint
+        holds no shared storages (safetensors refuses them); ``keep_vars=True`` callers get the Parameters."""
+        for k in ("conv.unit0.conv.weight", "conv.unit0.conv.bias", "residual.weight", "residual.bias"):
+            v = state_dict.get(prefix + k)
+            if v is not None and not isinstance(v, nn.Parameter) and v.untyped_storage().nbytes() != \
+                    v.numel() * v.element_size():
+                state_dict[prefix + k] = v.clone()
+        return state_dict
 
     def forward(self, x):
         units = list(self.conv.children())
@@ -226,7 +238,6 @@ class ResidualUnit(nn.Module):
                     and isinstance(u0.conv, Conv3d) and _fusable(x, u0.conv, u0.adn) and _fusable(x, r, None) and \
                     _fusable(x, u1.conv, u1.adn) and (r.bias is None) == (u0.conv.bias is None) and \
                     u0.adn.N.eps == u1.adn.N.eps and r.padding_mode == "zeros":
-                self._stack_params(u0.conv, r)
                 return _StackedUnitFn.apply(x, u0.conv.weight, u0.conv.bias, r.weight, r.bias, u0.adn.A.weight,
                                             u1.conv.weight, u1.conv.bias, u1.adn.A.weight, self, u0.adn.N.eps)
         if isinstance(self.residual, nn.Identity) and len(units) == 1 and hasattr(units[0], "adn"):
@@ -244,18 +255,35 @@ class ResidualUnit(nn.Module):
         res = self.residual(x)
         return self.conv(x) + res
 
-    @staticmethod
-    def _stack_params(c0: nn.Module, r: nn.Module):
-        """Once: move unit 0's and the residual conv's weights (and biases) into one storage each, unit 0's
-        first, so that the stacked convolution reads them as one tensor with no per-step concatenation.
-        The Parameter objects stay the same (optimizers and state dicts are unaffected)."""
+    def pack_parameters(self) -> bool:
+        """Explicit setup, never called by ``forward``: move a strided unit's unit-0 and residual conv
+        weights (and biases) into one storage each, unit 0's first, so the stacked convolution reads them as
+        one tensor with no per-step concatenation (``_adjacent``; without packing ``forward`` concatenates).
+        The Parameter objects stay the same (optimizer state is unaffected), but afterwards the two pairs
+        share a storage (``state_dict`` returns copies of those four tensors, so checkpoints -- torch.save or
+        safetensors -- hold no shared storage).  Skipped (returns False) under inference mode or when
+        a tensor is not a plain leaf Parameter.  ``TrainStep`` calls it once, before DDP and the optimizer."""
+        units = list(self.conv.children())
+        if not (isinstance(self.residual, Conv3d) and len(units) == 2 and hasattr(units[0], "conv")):
+            return False
+        c0, r = units[0].conv, self.residual
+        if torch.is_inference_mode_enabled() or not isinstance(c0, Conv3d) or r.stride != c0.stride or \
+                r.kernel_size != c0.kernel_size or r.padding != c0.padding:
+            return False  # only the units forward runs as one stacked convolution
+        packed = False
         with torch.no_grad():
             for n in ("weight", "bias"):
                 a, b = getattr(c0, n), getattr(r, n)
-                if a is None or b is None or _adjacent(a, b) is not None:
+                if a is None or b is None or a.shape[1:] != b.shape[1:] or a.dtype != b.dtype or a.device != b.device:
                     continue
-                st = torch.cat([a.detach(), b.detach()], 0)
-                a.data, b.data = st[:a.shape[0]], st[a.shape[0]:]
+                if not (isinstance(a, nn.Parameter) and isinstance(b, nn.Parameter) and a.is_leaf and b.is_leaf) \
+                        or a.is_inference() or b.is_inference():
+                    continue
+                if _adjacent(a, b) is None:
+                    st = torch.cat([a.detach(), b.detach()], 0)
+                    a.data, b.data = st[:a.shape[0]], st[a.shape[0]:]
+                packed = True
+        return packed
 
     def stacked_route(self, x: torch.Tensor, w_st: torch.Tensor) -> "_conv.Route":
         """The route of the stacked [unit0; residual] convolution for this input (cached per shape)."""
@@ -267,6 +295,11 @@ class ResidualUnit(nn.Module):
             rt = _conv.Route(x, w_st, r.stride, r.padding, (0, 0, 0), False)
             cache[key] = rt
         return rt
+
+
+def pack_parameters(model: nn.Module) -> int:
+    """``ResidualUnit.pack_parameters`` on every strided unit of ``model``; returns how many were packed."""
+    return sum(1 for m in model.modules() if isinstance(m, ResidualUnit) and m.pack_parameters())
 
 
 def _alias(buf: torch.Tensor, c0: int, c1: int) -> torch.Tensor:

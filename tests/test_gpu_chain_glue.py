@@ -59,6 +59,9 @@ def test_select_and_multimodal_slices(F):
     for b in range(B):
         ref = O.fourier_disk(x[b, 2:3].cpu().numpy(), 5.0)
         assert relerr(out["image"][b].cpu().numpy(), ref) < 1e-5
+    # out= of the input's shape cannot take a one-channel result: an error, not a broadcast copy
+    with pytest.raises(ValueError):
+        FusedChain([sel, disk])(x, out=torch.empty_like(x))
     # 127_*: filters on all four channels, then one random modality and the label's channel 1
     wrap = F.WrapArtifactd("image", 0.5)
     mm = F.MultimodalSlicesd(keys=["image", "label"], img_chan_indices=[0, 1, 2, 3], label_idx=1, seed=4)

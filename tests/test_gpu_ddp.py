@@ -3,8 +3,12 @@
 Two ranks share cuda:0 (spawned child processes, each initialising the GPU itself), process group over
 gloo (the RCCL path cannot put two ranks on one device; DDP's bucketing, static graph and
 ``gradient_as_bucket_view`` -- texbias/train.py:55-68 -- are the same code either way).  Every rank runs
-``TrainStep(distributed=True)`` on the reference U-Net(4 -> 3) with the texbias conv / InstanceNorm+PReLU /
-Dice kernels, its own batch of 2.  Checked:
+BASELINE config 4's workload at the reference drivers' crop size (2 x 4 x 128 x 128 x 64,
+…_3modalities.py:163-165,231): its own ``reference_c3_chain(rank)`` with bench.py's per-batch random
+filter draws (r, I, wrap alpha, S&P p) on its own batch, then ``TrainStep(distributed=True)`` on the
+reference U-Net(4 -> 3) with the texbias conv / InstanceNorm+PReLU / Dice kernels.  Checked:
+  * the ranks' filter draws differ, and every non-transposed 3x3x3 convolution routed to a texbias
+    kernel (no ``aten`` route), the full- and half-resolution layers' weight gradients too;
   * after 3 steps the replicas are bit-identical (every parameter and Adam state);
   * the first step's averaged gradients equal ONE process's batch-of-4 step (the two ranks' batches
     concatenated) -- the whole-step bar of tests/test_gpu_norm.py (per tensor, vs the largest gradient
@@ -23,7 +27,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "medical-vision-textural-bias_amd")
-SHAPE = (32, 32, 32)
+SHAPE = (128, 128, 64)
 
 
 def _batch(rank: int, dev):
@@ -46,18 +50,37 @@ def _rank_main(rank: int, world: int, port: int, out_dir: str):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import numpy as np
+    from texbias.pipeline import reference_c3_chain
     torch.manual_seed(0)
     step = TrainStep(reference_model(4, 3), dev, distributed=True)
-    x, lab = _batch(rank, dev)
+    x_raw, lab = _batch(rank, dev)
+    chain, tr = reference_c3_chain(rank)
+    prs = np.random.RandomState(12345 + rank)
+    draws = []
+
+    def filtered():  # bench.py randomize_filters(), then the fused chain on this rank's batch
+        tr["disk"].r = float(prs.uniform(10.0, 25.1))
+        tr["planes"].intensity_value = float(prs.uniform(10.0, 17.0))
+        tr["wrap"].transform.alpha = float(prs.choice([0.0, 0.25, 0.5, 0.75]))
+        tr["sap"].p = float(prs.uniform(0.05, 0.35))
+        draws.append((tr["disk"].r, tr["planes"].intensity_value, tr["wrap"].transform.alpha, tr["sap"].p))
+        return chain(x_raw)
+
+    x = filtered()
     # step 1 by hand to capture the averaged gradients before the optimizer moves the weights
     step.opt.zero_grad(set_to_none=True)
     loss = step.loss_fn(step.model(x), lab)
     loss.backward()
     grads = [p.grad.detach().clone().cpu() for p in step.module.parameters()]
     step.opt.step()
+    x1st = x.cpu()
     for _ in range(2):
-        step(x, lab)
+        step(filtered(), lab)
     torch.cuda.synchronize()
+    routes = [(key[1] if key[0] == "stacked" else key[0], r.k, r.transposed, r.kind, r.dx, r.fast_w)
+              for m in step.module.modules()
+              for key, r in m.__dict__.get("_tb_routes", {}).items()]
     params = [p.detach().cpu() for p in step.module.parameters()]
     st = step.opt.state_dict()["state"]
     adam = [(v["exp_avg"].cpu(), v["exp_avg_sq"].cpu(), v["max_exp_avg_sq"].cpu()) for v in st.values()]
@@ -72,7 +95,8 @@ def _rank_main(rank: int, world: int, port: int, out_dir: str):
     gibbs_gd(x1, l1, gstep.model, DiceLoss(sigmoid=True, squared_pred=True))
     torch.cuda.synchronize()
     alpha = gm.gibbs.alpha.detach().cpu().clone()
-    torch.save({"grads": grads, "params": params, "adam": adam, "alpha": alpha},
+    torch.save({"grads": grads, "params": params, "adam": adam, "alpha": alpha, "x": x1st, "draws": draws,
+                "routes": routes},
                os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -108,12 +132,24 @@ def test_ddp_two_ranks_hip_kernels(gpu, heartbeat):
             assert torch.equal(a, b)
     for a, b in zip(r0["grads"], r1["grads"]):
         assert torch.equal(a, b)
-    # the averaged first-step gradients == one process's batch-of-4 step
+    # C4: each rank drew its own filters and filtered its own batch
+    assert r0["draws"] != r1["draws"] and len(r0["draws"]) == 3
+    assert not torch.equal(r0["x"], r1["x"])
+    # the HIP kernels ran: no non-transposed 3x3x3 convolution on ATen; the top two resolutions' weight
+    # gradients on the texbias MFMA kernels
+    print("routes:", r0["routes"])
+    assert r0["routes"] and r0["routes"] == r1["routes"]
+    conv3 = [r for r in r0["routes"] if r[1] == 3 and not r[2]]
+    assert conv3 and all(r[3] != "aten" for r in conv3), conv3
+    top = [r for r in r0["routes"] if r[1] == 3 and min(r[0][2:]) >= SHAPE[2] // 2]
+    assert top and all(r[5] for r in top), top
+    # the averaged first-step gradients == one process's batch-of-4 step on the ranks' filtered batches
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     single = TrainStep(reference_model(4, 3), dev)
-    x0, l0 = _batch(0, dev)
-    x1, l1 = _batch(1, dev)
+    _, l0 = _batch(0, dev)
+    _, l1 = _batch(1, dev)
+    x0, x1 = r0["x"].to(dev), r1["x"].to(dev)
     single.opt.zero_grad(set_to_none=True)
     loss = single.loss_fn(single.model(torch.cat([x0, x1])), torch.cat([l0, l1]))
     loss.backward()

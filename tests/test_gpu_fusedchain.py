@@ -143,9 +143,10 @@ def test_fused_chain_mixed_batch_vs_oracle(F, FC, order, probs, wrap):
     assert len({(d, i is not None, s) for d, i, s in draws}) > 1
 
 
-def test_fused_chain_c3_full_size(F, FC):
-    """bench.py's configuration at full C3 size (2 x 4 x 240 x 240 x 155, pad 5): one channel vs
-    the oracle with the golden phase hook, S&P class map from the explicit u, pass-C min/max."""
+def test_fused_chain_c3_full_size(F, FC, heartbeat):
+    """bench.py's configuration at full C3 size (2 x 4 x 240 x 240 x 155, pad 5): every (sample,
+    channel) pair vs the oracle (one oracle pass per sample) with the golden phase hook, the S&P class
+    map from the explicit u, the pass-C min/max of each sample."""
     torch.manual_seed(3)
     B, C, spatial = 2, 4, (240, 240, 155)
     x = torch.randn((B, C) + spatial, device="cuda")
@@ -160,19 +161,24 @@ def test_fused_chain_c3_full_size(F, FC):
     u = torch.rand((B, C) + spatial, device="cuda")
     cls = torch.empty(x.shape, dtype=torch.int8, device="cuda")
     chain = FC([disk, planes, wrap, sap])
-    plans = chain.plan(B, spatial, phases)
-    idx1 = planes.idx   # the second sample's ellipsoid point
+    plans, idxs = [], []
+    for b in range(B):   # the same draws as one plan(B) call, each sample's ellipsoid point recorded
+        plans += chain.plan(1, spatial, [phases[b]])
+        idxs.append(tuple(planes.idx))
+    assert idxs[0] != idxs[1]
     y = chain(x, pad=PAD, plans=plans, u=u, cls=cls)
     assert y.shape == (B, C, 240, 240, 160) and torch.all(y[..., 155:] == 0)
-    b, c = 1, 2
-    ref3 = O.wrap_artifact(O.plane_waves(O.fourier_disk(x[b].cpu().numpy(), 12.5), idx1, 15.0,
-                                         phase=np.float32(phases[b])), 0.5)
-    mn, mx = chain.last_minmax[b]
-    np.testing.assert_allclose([mn, mx], [ref3.min(), ref3.max()], rtol=0, atol=1e-5 * np.abs(ref3).max())
-    z, cref = O.salt_and_pepper(ref3[c][None], 0.05, u[b, c][None].cpu().numpy())
-    np.testing.assert_array_equal(cls[b, c].cpu().numpy(), cref[0])
-    # S&P values come from the whole sample's min/max (all channels), not the channel's
-    zc = ref3[c].copy()
-    zc[cref[0] == 1] = np.float32(ref3.min()) / 2
-    zc[cref[0] == 2] = np.float32(ref3.max()) / 2
-    assert relerr(y[b, c, ..., :155].cpu().numpy(), zc) < TOL
+    yh, ch, uh = y[..., :155].cpu().numpy(), cls.cpu().numpy(), u.cpu().numpy()
+    for b in range(B):
+        ref3 = O.wrap_artifact(O.plane_waves(O.fourier_disk(x[b].cpu().numpy(), 12.5), idxs[b], 15.0,
+                                             phase=np.float32(phases[b])), 0.5)
+        mn, mx = chain.last_minmax[b]
+        np.testing.assert_allclose([mn, mx], [ref3.min(), ref3.max()], rtol=0, atol=1e-5 * np.abs(ref3).max())
+        for c in range(C):
+            z, cref = O.salt_and_pepper(ref3[c][None], 0.05, uh[b, c][None])
+            np.testing.assert_array_equal(ch[b, c], cref[0], err_msg=f"class map ({b}, {c})")
+            # S&P values come from the whole sample's min/max (all channels), not the channel's
+            zc = ref3[c].copy()
+            zc[cref[0] == 1] = np.float32(ref3.min()) / 2
+            zc[cref[0] == 2] = np.float32(ref3.max()) / 2
+            assert relerr(yh[b, c], zc) < TOL, (b, c)
