@@ -89,7 +89,11 @@ struct BandFwdArgs {
   const float* tbt; // [2][KSd][2][64] B fragments of the folded D product (plan table)
   FwdSplit split;   // set by launch_band_fwd
   int vec;          // contiguous 16-B aligned rows (sw == D, 16-B aligned base and slab strides)
+  const void* tbt16;  // compiled D: [KS16][cos/sin][hi/lo][64][8 halves] split-f16 D-product B fragments
 };
+// Pass A' D product in split f16 (compiled D): 32-wide k-steps of the folded d in [0, D/2]
+TB_HD constexpr int band_fwd16_ks(int D) { return (D / 2 + 1 + 31) / 32; }
+constexpr float BAND_FWD16_TSCALE = 256.f;  // the table is stored x 2^8 (no f16 subnormals)
 
 struct BandMidArgs {
   tb_plan_dev pl;

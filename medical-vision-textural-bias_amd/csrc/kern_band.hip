@@ -32,6 +32,13 @@ __device__ __forceinline__ float2 ld2(const cf* p) {
 
 // ----------------------------------------------------------------------------- pass A'
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+
+// x = h + l with h = f16(x), l = f16(x - h): 22 significant bits (|x| < 2^15 after scaling)
+__device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
+  h = (_Float16)x;
+  l = (_Float16)(x - (float)h);
+}
 
 // Global -> LDS copy of n elements of T by the whole workgroup with U loads in flight per thread
 // (a plain loop would wait for every load before its LDS store: one memory round trip per
@@ -144,8 +151,14 @@ __device__ __forceinline__ void strip_copy(float* Xw, int P, const StripSrc& s, 
 //              leaves the registers.
 // At the end of the wave's part of a slab, O goes through the wave's LDS region into the slab's
 // partial-sum slot P[bc][h][seg] (seg = this wave's rank among the slab's waves).
-template <int NT2, int KWT, int DC>
+// F16 (compiled D, NT2 = 1, 16-B staged strips): the D product in split f16 on mfma_f32_16x16x32_f16 --
+// per strip the folded values s, t scaled by a power of two from the strip's max |x| (|s|, |t| < 2^15),
+// split into f16 pairs, three products (sh Th + sh Tl + sl Th) against the plan's split table (x 2^8),
+// 32 folded d per k-step: 18 MFMAs of 16 cycles per strip instead of 40 of 32 (f32 16x16x4).  The
+// scale is undone in the W product's A operand (cos, sin x 2^-(8 + scale exponent), exact).
+template <int NT2, int KWT, int DC, bool F16 = false>
 __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * KWT == 1 ? 3 : NT2 * KWT == 2 ? 2 : 1, 4))) void k_band_fwd(BandFwdArgs) {
+  static_assert(!F16 || (DC > 0 && NT2 == 1), "split-f16 D product: compiled D, one kd tile");
   const BandFwdArgs& a = kargs<BandFwdArgs>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
@@ -159,8 +172,12 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
   constexpr int KSC = DC > 0 ? (DC / 2 + 1 + 3) / 4 : 1;
   const int XW = band_fwd_xw(P, NT2, KWT);
   float2* twW = reinterpret_cast<float2*>(smem);                               // (cos, -sin)(2 pi t / W)
-  float* Bt = reinterpret_cast<float*>(smem + ((W * 8 + 15) & ~15));           // [NT2][KSd][2][64] (DC == 0)
-  float* Xw = Bt + (DC > 0 ? 0 : NT2 * KSd * 128) + wv * XW;                    // this wave's region
+  // (F16: no W twiddles in LDS -- read per strip from the plan, which keeps three workgroups per CU)
+  float* Bt = reinterpret_cast<float*>(smem + (F16 ? 0 : ((W * 8 + 15) & ~15)));  // [NT2][KSd][2][64] (DC == 0)
+  constexpr int KS16 = DC > 0 ? band_fwd16_ks(DC) : 1;
+  // F16: the split-f16 D-product B fragments [k-step][cos/sin][hi/lo][64 lanes] (16 B each) in the Bt region
+  float* Xw = Bt + (F16 ? KS16 * 4 * 64 * 4 : DC > 0 ? 0 : NT2 * KSd * 128) + wv * XW;  // this wave's region
+  const h16x8* T16s = reinterpret_cast<const h16x8*>(Bt);
   const FastDiv fd = FastDiv::make(D);
   const FwdSplit sp = a.split;
   const uint32_t nst = sp.nst;
@@ -170,7 +187,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
     t = fwd_start(sp, gw);
     t1 = fwd_start(sp, gw + 1);
   }
-  const bool pre = a.vec && (BAND_FWD_ROWS * D + 6) <= 4 * 64 * FWD_PF;
+  const bool pre = F16 || (a.vec && (BAND_FWD_ROWS * D + 6) <= 4 * 64 * FWD_PF);  // F16: host-checked
   const int diag = a.diag;
   auto strip_src = [&](uint32_t tt) {
     StripSrc s;
@@ -191,8 +208,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
     ss = strip_src(t);
     if (pre) Strip<DC>::load(pf, ss, lane);
   }
-  float btr[NT2][KSC][2];  // compiled D: the D-product B fragments live in registers
-  if (DC > 0) {
+  float btr[F16 ? 1 : NT2][F16 ? 1 : KSC][2];  // compiled D: the D-product B fragments live in registers
+  if constexpr (DC > 0 && !F16) {
 #pragma unroll
     for (int nt = 0; nt < NT2; ++nt)
 #pragma unroll
@@ -201,9 +218,10 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
         btr[nt][k][1] = a.tbt[((nt * KSC + k) * 2 + 1) * 64 + lane];
       }
   }
-  lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
+  if (!F16) lds_fill<4>(twW, reinterpret_cast<const float2*>(a.pl.tw[1]), W, tid);
   // plan table (host double precision); 8-B pieces
   if (DC == 0) lds_fill<8>(reinterpret_cast<float2*>(Bt), reinterpret_cast<const float2*>(a.tbt), NT2 * KSd * 64, tid);
+  if (F16) lds_fill<3>(reinterpret_cast<float4*>(Bt), reinterpret_cast<const float4*>(a.tbt16), KS16 * 4 * 64, tid);
   __syncthreads();  // the only workgroup barrier: tables in LDS
   if (t >= t1) return;
   // O accumulators: [cos/sin][re/im][kw tile][kd tile]
@@ -221,7 +239,36 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
   for (;;) {
     const uint32_t slab = t / nst, st = t - slab * nst;
     const int w0 = (int)st * BAND_FWD_ROWS, nr = ss.nr;
-    // 1. this strip into the wave's LDS region
+    // 1. this strip into the wave's LDS region (F16: and its scale from max |x| of the loaded vectors)
+    float wsc = 1.f;  // F16: the W product's twiddle factor 2^-(8 + e)
+    float ssc = 1.f;  // F16: the strip's scale 2^(14 - e), max |x| < 2^e
+    float2 twr[F16 ? KWT : 1][4];  // F16: this strip's W twiddles, loaded before the next strip's vectors
+    if (F16) {
+      const int wl = w0 + 4 * l4;
+#pragma unroll
+      for (int kt = 0; kt < KWT; ++kt) {
+        const int kw = 16 * kt + l15;
+        int tw = (int)(((int64_t)kw * wl) % W);
+        const int step = kw % W;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          twr[kt][j] = reinterpret_cast<const float2*>(a.pl.tw[1])[tw];
+          tw += step;
+          tw = tw >= W ? tw - W : tw;
+        }
+      }
+      float mx = 0.f;
+#pragma unroll
+      for (int u = 0; u < FWD_PF; ++u) {  // branch-free: vectors past the strip count as 0
+        const float m4 = fmaxf(fmaxf(fabsf(pf[u][0]), fabsf(pf[u][1])), fmaxf(fabsf(pf[u][2]), fabsf(pf[u][3])));
+        mx = fmaxf(mx, lane + 64 * u < ss.nq ? m4 : 0.f);
+      }
+      mx = wave_max(mx);
+      int ex;
+      (void)frexpf(mx, &ex);  // mx < 2^ex (0 for a zero strip)
+      ssc = ldexpf(1.f, 14 - ex);
+      wsc = ldexpf(1.f, ex - 14) * (1.f / BAND_FWD16_TSCALE);
+    }
     const float* xs = Xw;
     if (diag & 2)
       xs = Xw;
@@ -248,7 +295,35 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
       for (int j = 0; j < 4; ++j) accc[nt][j] = accs[nt][j] = 0.f;
     if (!(diag & 4)) {
       const float* row = xs + l15 * P;
-      if (DC > 0) {
+      if constexpr (F16) {  // lane (row l15, quarter l4): folded d = 32 k + 8 l4 + i of its row
+#pragma unroll
+        for (int k = 0; k < KS16; ++k) {
+          h16x8 sh, sl, th, tl;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int d = 32 * k + 8 * l4 + i;  // < 96 <= D - 32: both reads inside the row
+            const bool has = d < Ld;
+            const bool pair = d >= 1 && 2 * d < D;
+            const float xa = has ? row[d] : 0.f;
+            const float xm = pair ? row[D - d] : 0.f;
+            _Float16 a0, a1, b0, b1;
+            split_f16((xa + xm) * ssc, a0, a1);
+            split_f16(pair ? (xm - xa) * ssc : 0.f, b0, b1);
+            sh[i] = a0;
+            sl[i] = a1;
+            th[i] = b0;
+            tl[i] = b1;
+          }
+          const h16x8* tk = T16s + (k * 4) * 64 + lane;  // [cos hi, cos lo, sin hi, sin lo]
+          const h16x8 ch = tk[0], cl = tk[64], sh2 = tk[128], sl2 = tk[192];
+          accc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sh, ch, accc[0], 0, 0, 0);
+          accs[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(th, sh2, accs[0], 0, 0, 0);
+          accc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sh, cl, accc[0], 0, 0, 0);
+          accs[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(th, sl2, accs[0], 0, 0, 0);
+          accc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sl, ch, accc[0], 0, 0, 0);
+          accs[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tl, sh2, accs[0], 0, 0, 0);
+        }
+      } else if (DC > 0) {
 #pragma unroll
         for (int k = 0; k < KSC; ++k) {
           const int d = 4 * k + l4;
@@ -300,8 +375,8 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bool ok = wl + j < W && kw <= KW;
-          const float2 c = twW[tw];
-          const float ca = ok ? c.x : 0.f, sa = ok ? -c.y : 0.f;
+          const float2 c = F16 ? twr[F16 ? kt : 0][j] : twW[tw];
+          const float ca = ok ? c.x * wsc : 0.f, sa = ok ? -c.y * wsc : 0.f;
 #pragma unroll
           for (int nt = 0; nt < NT2; ++nt) {
             oacc[0][0][kt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ca, accc[nt][j], oacc[0][0][kt][nt], 0, 0, 0);
@@ -926,13 +1001,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(VT == 1
 // 2^-22 relative, so Y matches the f32 synthesis to a few 1e-7 of max |y|.  The accumulator has
 // the image row w in its registers and the column d on the lane, so each register is stored
 // straight to HBM as two whole 128-B row segments: no LDS staging, no mirror stores.
-typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 constexpr float BAND_T16_SCALE = 256.f;
-
-__device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
-  h = (_Float16)x;
-  l = (_Float16)(x - (float)h);
-}
 
 // One thread per (column tile, 16-row chunk, lane): the lane's 8 B-fragment entries of T, k-permuted
 // to match the accumulator-as-A-operand order of V^T (element j of lane half h is V row
@@ -1466,9 +1535,9 @@ int band_grid(K kern, int units, size_t lds, int ncu, int cap = 4) {
   return units < g ? units : g;
 }
 
-template <int NT2, int KWT, int DC>
+template <int NT2, int KWT, int DC, bool F16 = false>
 hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
-  auto kern = k_band_fwd<NT2, KWT, DC>;
+  auto kern = k_band_fwd<NT2, KWT, DC, F16>;
   hipError_t e = allow_lds(kern, lds);
   if (e != hipSuccess) return e;
   // waves: as many as are resident at once (LDS / register occupancy), but at most T / ceil(nst / 2)
@@ -1526,12 +1595,30 @@ bool band_fwd_use_ct(int D, int NT2) {
   return ct_on && band_fwd_ct(D, NT2);
 }
 
+// the split-f16 D product (k_band_fwd<..., true>) where it applies; TEXBIAS_BAND_FWD16=0: the f32 one
+bool band_fwd16_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TEXBIAS_BAND_FWD16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
   const bool n1 = a.g.NDk <= 16, k1 = a.g.KW < 16;
   const bool ct = band_fwd_use_ct(a.pl.D, n1 ? 1 : 2);
   const size_t lds = band_lds_fwd(a.g, a.pl.W, a.pl.D, ct);
   if (ct) {
-    if (a.pl.D == 155) return k1 ? launch_fwd_t<1, 1, 155>(a, lds, ncu, st) : launch_fwd_t<1, 2, 155>(a, lds, ncu, st);
+    const bool f16 = band_fwd16_on() && a.tbt16 && a.vec;
+    // + the split-f16 table, - the W twiddles (read from the plan)
+    const size_t lds16 = lds + (size_t)band_fwd16_ks(a.pl.D) * 4 * 64 * 16 - (((size_t)a.pl.W * 8 + 15) & ~(size_t)15);
+    if (f16) {
+      if (a.pl.D == 155) return k1 ? launch_fwd_t<1, 1, 155, true>(a, lds16, ncu, st) : launch_fwd_t<1, 2, 155, true>(a, lds16, ncu, st);
+      return k1 ? launch_fwd_t<1, 1, 128, true>(a, lds16, ncu, st) : launch_fwd_t<1, 2, 128, true>(a, lds16, ncu, st);
+    }
+    if (a.pl.D == 155) {
+      return k1 ? launch_fwd_t<1, 1, 155>(a, lds, ncu, st) : launch_fwd_t<1, 2, 155>(a, lds, ncu, st);
+    }
     return k1 ? launch_fwd_t<1, 1, 128>(a, lds, ncu, st) : launch_fwd_t<1, 2, 128>(a, lds, ncu, st);
   }
   if (n1) return k1 ? launch_fwd_t<1, 1, 0>(a, lds, ncu, st) : launch_fwd_t<1, 2, 0>(a, lds, ncu, st);

@@ -274,6 +274,7 @@ struct tb_plan {
   bool ct_half = false;  // (H, W, D) has half-unit passes A / C and the split pass B (slab_ct.h HalfPlan)
   float* tds = nullptr;  // band pass C': [D/2 + 1][2][NCOLS] cos / sin(2 pi kd d / D), d < D/2 + 1, else 0
   float* tbt = nullptr;  // band pass A': [2][KSd][2][64] B fragments of the folded D product
+  void* tbt16 = nullptr;  // band pass A', compiled D: split-f16 B fragments [KS16][cos/sin][hi/lo][64][8]
   bool generic = false;  // full-spectrum route on the direct-DFT fallback (kern_generic.hip)
   double* wrapq = nullptr;  // odd D <= WRAP_MAX_COLS: the wrap route's D circulant table q[D] (wrap.h)
 };
@@ -417,6 +418,30 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
             const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)kd * d) % D) / (double)D;
             tb[(((size_t)nt * KSd + ks) * 2 + part) * 64 + ln] = (float)(part ? std::sin(ang) : std::cos(ang));
           }
+    if (D == 155 || D == 128) {  // the compiled pass-A' kernels' split-f16 table (x 2^8, hi / lo halves)
+      const int KS16 = tb::band_fwd16_ks(D);
+      std::vector<_Float16> t16((size_t)KS16 * 2 * 2 * 64 * 8);
+      for (int ks = 0; ks < KS16; ++ks)
+        for (int part = 0; part < 2; ++part)
+          for (int ln = 0; ln < 64; ++ln)
+            for (int i = 0; i < 8; ++i) {  // B[k = 8 (ln / 16) + i][n = ln % 16]: folded d, kd
+              const int d = 32 * ks + 8 * (ln >> 4) + i, kd = ln & 15;
+              double v = 0.0;
+              if (d < Dh && kd < Dh) {
+                const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)kd * d) % D) / (double)D;
+                v = (part ? std::sin(ang) : std::cos(ang)) * (double)tb::BAND_FWD16_TSCALE;
+              }
+              const float vf = (float)v;
+              const _Float16 h = (_Float16)vf, l = (_Float16)(vf - (float)h);
+              t16[((((size_t)ks * 2 + part) * 2 + 0) * 64 + ln) * 8 + i] = h;
+              t16[((((size_t)ks * 2 + part) * 2 + 1) * 64 + ln) * 8 + i] = l;
+            }
+      if (hipMalloc(&p->tbt16, t16.size() * 2) != hipSuccess ||
+          hipMemcpy(p->tbt16, t16.data(), t16.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+        tb_plan_destroy(p);
+        return hip_fail(hipGetLastError());
+      }
+    }
     if (hipMalloc(reinterpret_cast<void**>(&p->tds), ts.size() * 4) != hipSuccess ||
         hipMemcpy(p->tds, ts.data(), ts.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&p->tbt), tb.size() * 4) != hipSuccess ||
@@ -445,6 +470,7 @@ int tb_plan_destroy(tb_plan* plan) {
   if (plan->dmem) (void)hipFree(plan->dmem);
   if (plan->tds) (void)hipFree(plan->tds);
   if (plan->tbt) (void)hipFree(plan->tbt);
+  if (plan->tbt16) (void)hipFree(plan->tbt16);
   if (plan->wrapq) (void)hipFree(plan->wrapq);
   delete plan;
   return TB_OK;
@@ -789,6 +815,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     // 16-B vector strips: contiguous rows, and 16-B aligned strips where the compiled even-D staging needs them
     const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (xs[0] & 3) == 0 && (xs[1] & 3) == 0;
     fa.vec = xs[2] == D && ((D & 1) || al || !tb::band_fwd_use_ct(D, g.NDk <= 16 ? 1 : 2));
+    fa.tbt16 = p->tbt16;
     TB_HIP(tb::launch_band_fwd(fa, p->ncu, st));
     split = fa.split;
   }
