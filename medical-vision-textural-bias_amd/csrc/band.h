@@ -132,6 +132,7 @@ struct BandInvArgs {
   const void* T16;  // g.cat: split-f16 synthesis-table fragments (k_band_tab16)
   uint32_t* cnt;    // g.cat: arrival counter (zeroed by pass B'); the last workgroup writes the keys
   int stagger;      // g.cat: start offset of wave w, (w / 4) * stagger * 512 cycles (TEXBIAS_INV16_STAGGER)
+  int slots;        // g.cat: slab slots per fragment batch (set by launch_band_inv)
 };
 
 // Pass A': LDS row pitch of a staged strip.  Odd D: D (the strip is one contiguous run, 16-B
@@ -239,7 +240,7 @@ TB_HD BandWs band_ws(const BandGeo& g, int H, int bcn) {
 hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st);  // sets a.split
 bool band_fwd_use_ct(int D, int NT2);  // the compiled-D pass-A' kernel runs for this D
 hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st);
-hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st);  // g.cat: k_band_inv16
+hipError_t launch_band_inv(BandInvArgs& a, int ncu, hipStream_t st);  // g.cat: k_band_inv16 (sets a.slots)
 hipError_t launch_band_minmax(const float2* mmp, uint32_t* mm, int bc0, int C, int nbc, int H, int W, hipStream_t st);
 
 // identity samples (empty program): strided copy + zero D-padding + min/max

@@ -1143,7 +1143,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int nch = band_nch(a.g);       // 16-row chunks of V in use
   const int ntd = a.g.NTD;             // 32-column tiles of the output row (D + pad)
   const int fsz = VT * KV * 64;
-  constexpr int NT = 64 * NW, SLOTS = band_slots16(NW);
+  constexpr int NT = 64 * NW;
+  const int SLOTS = a.slots;  // slabs per fragment batch (launch_inv16_t: the workgroup's whole range where LDS allows)
   const BandInv16Carve cv = band_inv16_carve(a.g, W, SLOTS);
   const h16x8* Tab = reinterpret_cast<const h16x8*>(smem + cv.tab);  // [nt][c][hi/lo][64]
   float2* twW = reinterpret_cast<float2*>(smem + cv.tww);
@@ -1557,8 +1558,23 @@ hipError_t launch_fwd_t(BandFwdArgs& a, size_t lds, int ncu, hipStream_t st) {
 }
 
 template <int VT, int NW>
-hipError_t launch_inv16_t(const BandInvArgs& a, int ncu, hipStream_t st) {
-  const size_t lds = band_inv16_carve(a.g, a.pl.W, band_slots16(NW)).total;
+hipError_t launch_inv16_t(BandInvArgs& a, int ncu, hipStream_t st) {
+  // slab slots: a 16-wave workgroup (one per CU) holds every slab of its unit range when LDS allows,
+  // so its units run after ONE fragment batch (C2: 32 slabs per workgroup, 3 batches of 12 before)
+  int slots = band_slots16(NW);
+  static const int env_slots = [] {  // measurement: TEXBIAS_INV16_SLOTS=n caps the 16-wave slots
+    const char* e = std::getenv("TEXBIAS_INV16_SLOTS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (NW == 16 && env_slots <= 0) {
+    const int ntw = (a.pl.W + 31) / 32, nslab = a.pl.H * a.nbc;
+    const int grid = nslab < ncu ? nslab : ncu;
+    const int per = (nslab * ntw + grid - 1) / grid;
+    const int want = (per + ntw - 1) / ntw + 1;  // a range may start and end inside a slab
+    while (slots < want && band_inv16_carve(a.g, a.pl.W, slots + 1).total <= 160000) ++slots;
+  }
+  a.slots = slots;
+  const size_t lds = band_inv16_carve(a.g, a.pl.W, slots).total;
   // output orientation: tile rows = image columns.  With 16-B aligned rows the tile is regrouped
   // into whole-line stores (tile_rows8), which beat the image-row orientation at every row stride
   // (C2, 512-B rows: 77 -> 69 us).  Without them the 32 x 32-B pieces of a store pile onto one
@@ -1609,13 +1625,11 @@ hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
   const bool ct = band_fwd_use_ct(a.pl.D, n1 ? 1 : 2);
   const size_t lds = band_lds_fwd(a.g, a.pl.W, a.pl.D, ct);
   if (ct) {
-    const bool f16 = band_fwd16_on() && a.tbt16 && a.vec;
-    // + the split-f16 table, - the W twiddles (read from the plan)
+    // split-f16 D product for D = 155 (C3: 63.2 -> 61.6 us with flushed caches, level in the train-step
+    // bench); D = 128 (C2) keeps the f32 product (its 8 KB strips: 57.9 vs 59.6 us in the C2 bench)
+    const bool f16 = band_fwd16_on() && a.tbt16 && a.vec && a.pl.D == 155;
     const size_t lds16 = lds + (size_t)band_fwd16_ks(a.pl.D) * 4 * 64 * 16 - (((size_t)a.pl.W * 8 + 15) & ~(size_t)15);
-    if (f16) {
-      if (a.pl.D == 155) return k1 ? launch_fwd_t<1, 1, 155, true>(a, lds16, ncu, st) : launch_fwd_t<1, 2, 155, true>(a, lds16, ncu, st);
-      return k1 ? launch_fwd_t<1, 1, 128, true>(a, lds16, ncu, st) : launch_fwd_t<1, 2, 128, true>(a, lds16, ncu, st);
-    }
+    if (f16) return k1 ? launch_fwd_t<1, 1, 155, true>(a, lds16, ncu, st) : launch_fwd_t<1, 2, 155, true>(a, lds16, ncu, st);
     if (a.pl.D == 155) {
       return k1 ? launch_fwd_t<1, 1, 155>(a, lds, ncu, st) : launch_fwd_t<1, 2, 155>(a, lds, ncu, st);
     }
@@ -1645,7 +1659,7 @@ hipError_t launch_band_mid(const BandMidArgs& a, hipStream_t st) {
 
 
 
-hipError_t launch_band_inv(const BandInvArgs& a, int ncu, hipStream_t st) {
+hipError_t launch_band_inv(BandInvArgs& a, int ncu, hipStream_t st) {
   if (a.g.cat) {
     if (TB_INV16_NW == 16 && band_inv16_carve(a.g, a.pl.W, band_slots16(16)).total <= 160000)
       return band_vt(a.g) == 1 ? launch_inv16_t<1, 16>(a, ncu, st) : launch_inv16_t<2, 16>(a, ncu, st);

@@ -418,7 +418,7 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
             const double ang = 2.0 * 3.14159265358979323846 * (double)(((int64_t)kd * d) % D) / (double)D;
             tb[(((size_t)nt * KSd + ks) * 2 + part) * 64 + ln] = (float)(part ? std::sin(ang) : std::cos(ang));
           }
-    if (D == 155 || D == 128) {  // the compiled pass-A' kernels' split-f16 table (x 2^8, hi / lo halves)
+    if (D == 155) {  // the compiled pass-A' kernel's split-f16 table (x 2^8, hi / lo halves)
       const int KS16 = tb::band_fwd16_ks(D);
       std::vector<_Float16> t16((size_t)KS16 * 2 * 2 * 64 * 8);
       for (int ks = 0; ks < KS16; ++ks)
