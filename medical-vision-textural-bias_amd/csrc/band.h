@@ -131,7 +131,6 @@ struct BandInvArgs {
   const float* tds; // [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   const void* T16;  // g.cat: split-f16 synthesis-table fragments (k_band_tab16)
   uint32_t* cnt;    // g.cat: arrival counter (zeroed by pass B'); the last workgroup writes the keys
-  int stagger;      // g.cat: start offset of wave w, (w / 4) * stagger * 512 cycles (TEXBIAS_INV16_STAGGER)
   int slots;        // g.cat: slab slots per fragment batch (set by launch_band_inv)
 };
 

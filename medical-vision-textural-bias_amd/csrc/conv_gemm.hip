@@ -412,13 +412,8 @@ int make_plan(int mode, int N, int Cin, int M, int D, int H, int Wd, int stride,
   a.ysc = a.ymul == 2 ? 8 * a.OD * a.OH * a.OW : a.OD * a.OH * a.OW;
   if ((int64_t)N * M * a.ysc >= (int64_t)1 << 31) return TB_ERR_UNSUPPORTED_SIZE;
   a.P = N * a.OD * a.OH * a.OW;
-  // tile: M <= 32 -> 32 x 128; M <= 64 -> 64 x 64; else 128 x 128 (TEXBIAS_CG_TILE=1..5 overrides)
-  static const int tile_env = [] {
-    const char* e = std::getenv("TEXBIAS_CG_TILE");
-    return e ? std::atoi(e) : 0;
-  }();
-  int tile = tile_env;
-  if (tile < 1 || tile > 5) tile = M <= 32 ? 1 : (M <= 64 ? 2 : 5);
+  // tile: M <= 32 -> 32 x 128; M <= 64 -> 64 x 64; else 128 x 128
+  const int tile = M <= 32 ? 1 : (M <= 64 ? 2 : 5);
   static const int cfg[6][3] = {{0, 0, 0}, {32, 128, 1}, {64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2}};
   pl.BM = cfg[tile][0], pl.BP = cfg[tile][1], pl.WGM = cfg[tile][2];
   a.mtiles = (M + pl.BM - 1) / pl.BM;

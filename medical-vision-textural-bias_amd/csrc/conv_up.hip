@@ -406,13 +406,9 @@ int tb_convT3d_fewout_f32(const float* x, const float* W, const float* bias, flo
   TB_T(1, 1) TB_T(1, 2) TB_T(1, 3) TB_T(2, 1) TB_T(2, 2) TB_T(2, 3) TB_T(3, 1) TB_T(3, 2) TB_T(3, 3) TB_T(4, 1)
   TB_T(4, 2) TB_T(4, 3)
 #undef TB_T
-  // (channels per FMA-loop iteration of the 512-thread form: TEXBIAS_CONVT_FEW_UNROLL 1 / 2 / 4 = 296 / 294 /
-  // 311 us for the C3 32 -> 3 layer: one)
-  static const int U = [] {
-    const char* e = std::getenv("TEXBIAS_CONVT_FEW_UNROLL");
-    const int v = e ? std::atoi(e) : 1;
-    return v == 2 || v == 4 ? v : 1;
-  }();
+  // (channels per FMA-loop iteration of the 512-thread form: 1 / 2 / 4 = 296 / 294 / 311 us for the C3
+  // 32 -> 3 layer: one)
+  constexpr int U = 1;
   if (big && Mout == 3)
     kern = U == 4 ? k_convT_fewout<3, 6, 20, 512, 4> : U == 2 ? k_convT_fewout<3, 6, 20, 512, 2>
                                                       : k_convT_fewout<3, 6, 20, 512>;
@@ -657,367 +653,12 @@ __global__ __launch_bounds__(NTH) void k_conv3d_fwd16(F16Args a) {  // 16-column
 }
 }  // namespace
 
-// ------------------------------------------------- the same kernel with DMA-staged planes
-// k_conv3d_fwd16 stages the next plane through registers, and hipcc puts `s_waitcnt vmcnt(0)` before the
-// first MFMA of every step (it cannot tell the A fragments' start-up loads from the plane loads), so the
-// fetch of plane z + 2 never overlaps step z's MFMAs.  Here the planes arrive by global -> LDS DMA (no
-// registers) into a 4-slot ring -- plane z + 2 in flight during step z, drained by the step's closing
-// barrier -- and the weights and bias come through LDS, so no ordinary global load is outstanding in
-// the loop.  Same arithmetic and accumulation order as k_conv3d_fwd16 (bitwise the same results).
-namespace {
-typedef __attribute__((address_space(1))) const void* gptr_tc;
-typedef __attribute__((address_space(3))) void* lptr_tc;
+// (Round 6: the DMA-staged plane variant (439 vs 382 us) and the split-precision bf16 variant
+// k_conv16_x3 (no gain in the step) were measured, rejected and removed; DESIGN.md records them.)
 
-template <int NXT, bool ADD>
-__global__ __launch_bounds__(512) void k_conv3d_fwd16_dma(F16Args a) {
-  constexpr int YB = 3, NTH = 512, NWV = 8, NR = YB + 2, W = 16 * NXT, NSEG = (W + 63) / 64;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = (int)threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int D = a.D, H = a.H, PX = a.PX, RX = a.RX, SS = 16 * RX;
-  float* ring = smem;            // [4][16 c][NR][PX], column x at x + 4
-  float* wl = smem + 4 * SS;     // W [16][16][27], then bias [16]
-  for (int i = tid; i < 4 * SS; i += NTH) ring[i] = 0.f;
-  for (int i = tid; i < 16 * 16 * 27; i += NTH) wl[i] = a.W[i];
-  if (tid < 16) wl[16 * 16 * 27 + tid] = a.bias ? a.bias[tid] : 0.f;
-  int b = (int)blockIdx.x;
-  const int zs = b % a.ZS;
-  b /= a.ZS;
-  const int yb = b % a.nyb, n = b / a.nyb;
-  const int y0 = yb * YB;
-  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
-  const int64_t plane = (int64_t)H * W;
-  const float* xb = a.x + (int64_t)n * 16 * D * plane;
-  __syncthreads();
-  const int li = lane & 15, ks = lane >> 4;
-  float af[108];
-#pragma unroll
-  for (int kk = 0; kk < 108; ++kk) af[kk] = wl[(li * 16 + 4 * (kk & 3) + ks) * 27 + (kk >> 2)];
-  float bm[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bm[r] = wl[16 * 16 * 27 + 4 * ks + r];
-  // plane zi into slot zi & 3: each in-image row by 4-B DMA pieces (one row per wave instruction group);
-  // a plane outside [0, D) zeroes the slot's in-image rows (rows outside the image stay zero)
-  auto stage = [&](int zi) {
-    float* sl = ring + (zi & 3) * SS;
-    const bool in = zi >= 0 && zi < D;
-    for (int row = wave; row < 16 * NR; row += NWV) {
-      const int c = row / NR, r = row - c * NR, yi = y0 - 1 + r;
-      if (yi < 0 || yi >= H) continue;
-      float* dst = sl + c * RX + r * PX + 4;
-      if (in) {
-        const float* src = xb + ((int64_t)c * D + zi) * plane + (int64_t)yi * W;
-#pragma unroll
-        for (int sg = 0; sg < NSEG; ++sg) {
-          const int xx = lane + 64 * sg;
-          if (xx < W) __builtin_amdgcn_global_load_lds((gptr_tc)(src + xx), (lptr_tc)(dst + 64 * sg), 4, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int sg = 0; sg < NSEG; ++sg) {
-          const int xx = lane + 64 * sg;
-          if (xx < W) dst[xx] = 0.f;
-        }
-      }
-    }
-  };
-  stage(z0 - 1);
-  stage(z0);
-  stage(z0 + 1);
-  __syncthreads();  // (drains the DMA)
-  const int bl = ks * RX + li + 3;
-  float* yb0 = a.y + (int64_t)n * 16 * D * plane;
-  const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * plane : nullptr;
-  constexpr int NT = YB * NXT;
-  for (int z = z0; z < z1; ++z) {
-    if (z + 1 < z1) stage(z + 2);  // over plane z - 2 (last read in step z - 1)
-    const float* s0 = ring + ((z + 3) & 3) * SS + bl;  // tz = 0: plane z - 1
-    const float* s1 = ring + (z & 3) * SS + bl;
-    const float* s2 = ring + ((z + 1) & 3) * SS + bl;
-    for (int t0 = wave; t0 < NT; t0 += 2 * NWV) {
-      const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
-      const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
-      const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
-      const int o0 = yy0 * PX + x00, o1 = yy1 * PX + x01;
-      f32x4 acc0 = {bm[0], bm[1], bm[2], bm[3]}, acc1 = acc0;
-#pragma unroll
-      for (int tz = 0; tz < 3; ++tz) {
-        const float* sl = tz == 0 ? s0 : tz == 1 ? s1 : s2;
-#pragma unroll
-        for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-          for (int tx = 0; tx < 3; ++tx) {
-            const int t = tz * 9 + ty * 3 + tx;
-#pragma unroll
-            for (int cq = 0; cq < 4; ++cq) {
-              const int off = 4 * cq * RX + ty * PX + tx;
-              const float b0 = sl[o0 + off], b1 = sl[o1 + off];
-              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], b0, acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[4 * t + cq], b1, acc1, 0, 0, 0);
-            }
-          }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 4 * ks + r;
-        const int64_t o0 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy0) * W + x00 + li;
-        const int64_t o1 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy1) * W + x01 + li;
-        if (y0 + yy0 < H) yb0[o0] = ADD ? acc0[r] + ab0[o0] : acc0[r];
-        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc1[r] + ab0[o1] : acc1[r];
-      }
-    }
-    __syncthreads();  // plane z + 2 landed (vmcnt(0)); every wave is done with plane z - 1's slot
-  }
-}
-
-// TEXBIAS_CONV16_DMA=1: this variant instead of the register-staged k_conv3d_fwd16 (off: 439 vs 382 us
-// at 2 x 16 x 120 x 120 x 80 -- 4-B DMA pieces, 4x the memory instructions of the float4 loads)
-bool conv16_dma_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_CONV16_DMA");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-int launch_fwd16_dma(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
-                     int Wd, hipStream_t st) {
-  F16Args a{};
-  a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
-  a.PX = Wd + 8;
-  a.RX = 5 * a.PX;
-  while ((a.RX & 31) != 16) ++a.RX;
-  a.nyb = (H + 2) / 3;
-  const size_t lds = (size_t)4 * (4 * 16 * a.RX + 16 * 16 * 27 + 16);
-  if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
-  a.zlen = zseg(D, N * a.nyb, 1, 2);
-  a.ZS = (D + a.zlen - 1) / a.zlen;
-  void (*kern)(F16Args) = nullptr;
-#define TB_FD(NX) \
-  case NX: kern = add ? k_conv3d_fwd16_dma<NX, true> : k_conv3d_fwd16_dma<NX, false>; break;
-  switch (Wd / 16) {
-    TB_FD(1) TB_FD(2) TB_FD(3) TB_FD(4) TB_FD(5) TB_FD(6) TB_FD(7) TB_FD(8)
-    default: return TB_ERR_UNSUPPORTED_SIZE;
-  }
-#undef TB_FD
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
-      hipSuccess)
-    return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(512), lds, st, a);
-  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
-}
-}  // namespace
-
-// ------------------------------------------------- the same layer in split precision on the bf16 matrix cores
-// f32 operands as three bf16 parts, x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1):
-// 24 significant bits, exact), and the six products whose magnitude reaches 2^-24 of the leading one,
-// a0 b0 + a0 b1 + a1 b0 + a0 b2 + a2 b0 + a1 b1, accumulated in f32 on mfma_f32_16x16x32_bf16 (8192
-// MACs per 16 cycles against 1024 per 32 for the f32 MFMA: 6 products cost 96 cycles where the f32 form
-// takes 256).  The three dropped terms are below 2^-24 of the leading product, so a dot product's error
-// is that of an f32 FMA chain (the f32 fixtures of tests/test_gpu_conv_up.py hold it to 4x ATen's own).
-// k = (tap, channel): a 32-k MFMA step is two taps x 16 channels; lane group g = lane >> 4 holds tap
-// 2 q + (g >> 1), channels 8 (g & 1) .. + 7, so its B operand is 8 channels of ONE input position: the
-// staged planes are channel-innermost bf16 [split][row][column][16], one 16-B read per split (lanes of a
-// ds_read_b128 group hit distinct banks at the 32-B position pitch).  The block's A operand (14 steps x 3
-// parts) lives in registers for the kernel's life.  Staging: a task (row, column, channel half) loads 8
-// channels (each a coalesced row of the NCDHW plane), splits them and writes 3 x 16 B.
-namespace {
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4b __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void split3(const float* v, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)v[j];
-    const float r1 = v[j] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    const float r2 = r1 - (float)m;
-    p0[j] = h;
-    p1[j] = m;
-    p2[j] = (__bf16)r2;
-  }
-}
-
-struct X3Args {
-  const float* x;
-  const float* W;     // [16 m][16 c][27]
-  const float* bias;  // [16] or null
-  const float* add;   // [N][16][D][H][W] summed into y, or null
-  float* y;
-  int D, H, Wd;
-  int ZS, zlen, nyb;
-  int diag;  // measurement only (TEXBIAS_X3_DIAG): 1 skips the plane loads, 2 the MFMA phase; results invalid
-};
-
-template <int NXT, int NTH, bool ADD>
-__global__ __launch_bounds__(NTH) void k_conv16_x3(X3Args a) {
-  constexpr int YB = 3, NR = YB + 2, W = 16 * NXT, PXP = W + 2, NWV = NTH / 64;
-  constexpr int SPL = NR * PXP * 16;      // bf16 per split of one plane
-  constexpr int SLOT = 3 * SPL;           // bf16 per plane (3 splits)
-  constexpr int NTASK = NR * W * 2;       // (row, column, channel half)
-  constexpr int NL = (NTASK + NTH - 1) / NTH;
-  extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // [3 slots][3 splits][NR][PXP][16]
-  const int tid = (int)threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int D = a.D, H = a.H;
-  for (int i = tid; i < 3 * SLOT / 8; i += NTH) reinterpret_cast<bf16x8*>(ring)[i] = bf16x8{};
-  int b = (int)blockIdx.x;
-  const int zs = b % a.ZS;
-  b /= a.ZS;
-  const int yb = b % a.nyb, n = b / a.nyb;
-  const int y0 = yb * YB;
-  const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
-  // A: lane (m = l & 15, g = l >> 4), step q: tap 2 q + (g >> 1), channels 8 (g & 1) + j
-  const int li = lane & 15, g = lane >> 4;
-  bf16x8 af[14][3];
-#pragma unroll
-  for (int q = 0; q < 14; ++q) {
-    const int t = 2 * q + (g >> 1);
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = t < 27 ? a.W[(li * 16 + 8 * (g & 1) + j) * 27 + (t < 27 ? t : 0)] : 0.f;
-    split3(v, af[q][0], af[q][1], af[q][2]);
-  }
-  const int64_t plane = (int64_t)H * W;
-  const float* xb = a.x + (int64_t)n * 16 * D * plane;
-  // staging tasks of this thread: (row r, column x, channel half hh); goff = -1 for rows outside the image
-  int goff[NL], loff[NL];
-#pragma unroll
-  for (int j = 0; j < NL; ++j) {
-    const int i = tid + NTH * j;
-    const int x = i % W, t = i / W, r = t % NR, hh = t / NR;
-    const int yi = y0 - 1 + r;
-    const bool ok = i < NTASK && yi >= 0 && yi < H;
-    goff[j] = ok ? (int)((int64_t)8 * hh * D * plane + (int64_t)yi * W + x) : -1;
-    loff[j] = (r * PXP + x + 1) * 16 + 8 * hh;
-  }
-  // loads unconditional (clamped to valid addresses), validity applied when the plane is stored: a
-  // select right after a load made the compiler branch on the plane test and wait for every load
-  float rg[NL][8];
-  auto load = [&](int zi) {
-    const float* src = xb + (int64_t)(zi >= 0 && zi < D ? zi : 0) * plane;
-#pragma unroll
-    for (int j = 0; j < NL; ++j)
-#pragma unroll
-      for (int c = 0; c < 8; ++c) rg[j][c] = src[(goff[j] < 0 ? 0 : goff[j]) + (int64_t)c * D * plane];
-  };
-  auto store = [&](int zi) {
-    __bf16* d = ring + ((zi + 3) % 3) * SLOT;
-    const bool in = zi >= 0 && zi < D;
-#pragma unroll
-    for (int j = 0; j < NL; ++j)
-      if (goff[j] >= 0) {
-        bf16x8 p0, p1, p2;
-        if (!in)
-#pragma unroll
-          for (int c = 0; c < 8; ++c) rg[j][c] = 0.f;
-        split3(rg[j], p0, p1, p2);
-        *reinterpret_cast<bf16x8*>(d + loff[j]) = p0;
-        *reinterpret_cast<bf16x8*>(d + SPL + loff[j]) = p1;
-        *reinterpret_cast<bf16x8*>(d + 2 * SPL + loff[j]) = p2;
-      }
-  };
-  __syncthreads();
-  load(z0 - 1);
-  store(z0 - 1);
-  load(z0);
-  store(z0);
-  load(z0 + 1);
-  const float bm[4] = {a.bias ? a.bias[4 * g] : 0.f, a.bias ? a.bias[4 * g + 1] : 0.f,
-                       a.bias ? a.bias[4 * g + 2] : 0.f, a.bias ? a.bias[4 * g + 3] : 0.f};
-  float* yb0 = a.y + (int64_t)n * 16 * D * plane;
-  const float* ab0 = ADD ? a.add + (int64_t)n * 16 * D * plane : nullptr;
-  constexpr int NT = YB * NXT;
-  for (int z = z0; z < z1; ++z) {
-    store(z + 1);
-    __syncthreads();
-    if (z + 1 < z1 && !(a.diag & 1)) load(z + 2);
-    for (int t0 = wave; t0 < NT && !(a.diag & 2); t0 += 2 * NWV) {
-      const int t1 = t0 + NWV < NT ? t0 + NWV : t0;
-      const int yy0 = t0 / NXT, x00 = 16 * (t0 - yy0 * NXT);
-      const int yy1 = t1 / NXT, x01 = 16 * (t1 - yy1 * NXT);
-      f32x4b acc0 = {bm[0], bm[1], bm[2], bm[3]}, acc1 = acc0;
-#pragma unroll
-      for (int q = 0; q < 14; ++q) {
-        const int t = 2 * q + (g >> 1) < 27 ? 2 * q + (g >> 1) : 26;
-        const int tz = t / 9, ty = (t / 3) % 3, tx = t % 3;
-        const __bf16* sl = ring + ((z + tz + 2) % 3) * SLOT + 8 * (g & 1);
-        const int o0 = ((yy0 + ty) * PXP + x00 + li + tx) * 16, o1 = ((yy1 + ty) * PXP + x01 + li + tx) * 16;
-        bf16x8 b0[3], b1[3];
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          b0[s] = *reinterpret_cast<const bf16x8*>(sl + s * SPL + o0);
-          b1[s] = *reinterpret_cast<const bf16x8*>(sl + s * SPL + o1);
-        }
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b0[1], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b1[1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b0[2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b1[2], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][2], b0[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][2], b1[0], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b0[1], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b1[1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b0[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][1], b1[0], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b0[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q][0], b1[0], acc1, 0, 0, 0);
-      }
-      // C: column x = li, rows m = 4 g + r
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 4 * g + r;
-        const int64_t o0 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy0) * W + x00 + li;
-        const int64_t o1 = ((int64_t)m * D + z) * plane + (int64_t)(y0 + yy1) * W + x01 + li;
-        if (y0 + yy0 < H) yb0[o0] = ADD ? acc0[r] + ab0[o0] : acc0[r];
-        if (t1 != t0 && y0 + yy1 < H) yb0[o1] = ADD ? acc1[r] + ab0[o1] : acc1[r];
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// TEXBIAS_CONV_X3=1: the split-precision kernel instead of the f32-MFMA k_conv3d_fwd16 (off: in the C3
-// step it measured no faster, 350-365 vs 352 us -- the layer is not bound by the matrix cores, see DESIGN)
-bool conv_x3_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_CONV_X3");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-int launch_conv16_x3(const float* x, const float* W, const float* bias, const float* add, float* y, int N, int D, int H,
-                     int Wd, hipStream_t st) {
-  X3Args a{};
-  a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
-  static const int diag = [] {
-    const char* e = std::getenv("TEXBIAS_X3_DIAG");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.diag = diag;
-  a.nyb = (H + 2) / 3;
-  const size_t lds = (size_t)3 * 3 * 5 * (Wd + 2) * 16 * 2;
-  if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
-  a.zlen = zseg(D, N * a.nyb, 1, 2);
-  a.ZS = (D + a.zlen - 1) / a.zlen;
-  void (*kern)(X3Args) = nullptr;
-#define TB_X3(NX)                                                                      \
-  case NX: kern = add ? k_conv16_x3<NX, 512, true> : k_conv16_x3<NX, 512, false>; break;
-  switch (Wd / 16) {
-    TB_X3(1) TB_X3(2) TB_X3(3) TB_X3(4) TB_X3(5) TB_X3(6) TB_X3(7)
-    default: return TB_ERR_UNSUPPORTED_SIZE;
-  }
-#undef TB_X3
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 163840) !=
-      hipSuccess)
-    return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(N * a.nyb * a.ZS)), dim3(512), lds, st, a);
-  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
-}
-}  // namespace
 
 // Conv3d(16 -> 16, 3, stride 1, padding 1) forward: x [N][16][D][H][W] -> y [N][16][D][H][W], W % 16 == 0,
-// W <= 128; weight [16][16][27], bias [16] or NULL.  (csrc/conv_up.hip, k_conv16_x3 / k_conv3d_fwd16)
+// W <= 128; weight [16][16][27], bias [16] or NULL.  (csrc/conv_up.hip, k_conv3d_fwd16)
 int tb_conv3d_fwd16_f32(const float* x, const float* W, const float* bias, float* y, int N, int D, int H, int Wd,
                         void* stream) {
   return tb_conv3d_fwd16_add_f32(x, W, bias, nullptr, y, N, D, H, Wd, stream);
@@ -1040,21 +681,10 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
                       int Wd, int flip, void* stream, int64_t add_sn) {
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if (Wd % 16 != 0 || Wd > 128 || (reinterpret_cast<uintptr_t>(x) & 15) != 0) return TB_ERR_UNSUPPORTED_SIZE;
-  if (conv_x3_on() && Wd <= 112 && !flip)
-    return launch_conv16_x3(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
-  if (conv16_dma_on() && !flip) {
-    const int rc = launch_fwd16_dma(x, W, bias, add, y, N, D, H, Wd, reinterpret_cast<hipStream_t>(stream));
-    if (rc != TB_ERR_UNSUPPORTED_SIZE) return rc;
-  }
-  // output rows per block (TEXBIAS_CONV16_YB 2..4; C3, W = 80: YB 2 / 3 / 4 = 478 / 419 / 482 us -- the
-  // YB x 5 tiles of a step over 4 waves x 2 chains: 10 of 16, 15 of 16, 20 of 24 slots used; YB = 2's
-  // second block per CU did not make up for it)
-  static const int YBv = [] {
-    const char* e = std::getenv("TEXBIAS_CONV16_YB");
-    const int v = e ? std::atoi(e) : 3;
-    return v == 3 ? v : 3;  // round 5: only the measured best (YB 3, 512 threads) is instantiated
-  }();
-  const int YB = YBv;
+  // output rows per block (C3, W = 80: YB 2 / 3 / 4 = 478 / 419 / 482 us -- the YB x 5 tiles of a step
+  // over 4 waves x 2 chains: 10 of 16, 15 of 16, 20 of 24 slots used; YB = 2's second block per CU did not
+  // make up for it): only YB = 3 is instantiated
+  constexpr int YB = 3;
   F16Args a{};
   a.x = x, a.W = W, a.bias = bias, a.add = add, a.y = y, a.D = D, a.H = H, a.Wd = Wd;
   a.flip = flip;
@@ -1063,30 +693,20 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
   a.RX = (YB + 2) * a.PX;
   while ((a.RX & 31) != 16) ++a.RX;
   a.nyb = (H + YB - 1) / YB;
-  static const int ring4 = [] {
-    const char* e = std::getenv("TEXBIAS_CONV16_RING");
-    return e && std::atoi(e) == 3 ? 0 : 1;
-  }();
-  const int NS = ring4 && (size_t)4 * 4 * 16 * a.RX <= 163840 ? 4 : 3;
+  const int NS = (size_t)4 * 4 * 16 * a.RX <= 163840 ? 4 : 3;  // 4-slot plane ring where it fits
   const size_t lds = (size_t)NS * 4 * 16 * a.RX;
   if (lds > 163840) return TB_ERR_UNSUPPORTED_SIZE;
   const int per_cu = 163840 / (int)lds >= 2 ? 2 : 1;
   a.zlen = zseg(D, N * a.nyb, per_cu, 2);
   a.ZS = (D + a.zlen - 1) / a.zlen;
   void (*kern)(F16Args) = nullptr;
-  // threads per block (TEXBIAS_CONV16_NT 256 | 512): 8 waves, 2 per SIMD sharing the matrix core, hide
-  // the B-fragment LDS reads the compiler issues only 1-3 ahead (YB = 3: 421 -> 365 us per C3 call)
-  static const int NTv = [] {
-    const char* e = std::getenv("TEXBIAS_CONV16_NT");
-    return e && std::atoi(e) == 256 ? 512 : 512;
-  }();
+  // 512 threads per block: 8 waves, 2 per SIMD sharing the matrix core, hide the B-fragment LDS reads the
+  // compiler issues only 1-3 ahead (YB = 3: 421 -> 365 us per C3 call against 256 threads)
+  constexpr int NTv = 512;
   // the B fragments read a tap ahead of their MFMAs, interleaved one LDS read per MFMA (sched_group_barrier)
-  // and a 4-slot plane ring, one barrier per step (TEXBIAS_CONV16_PF=0 / TEXBIAS_CONV16_RING=3 off; C3, by
-  // scripts/diag/conv_kern_bench.py: forward 385 -> 374 us, input gradient 361 -> 353 us)
-  static const bool PFv = [] {
-    const char* e = std::getenv("TEXBIAS_CONV16_PF");
-    return !(e && std::atoi(e) == 0);
-  }();
+  // and a 4-slot plane ring, one barrier per step (C3, by scripts/diag/conv_kern_bench.py: forward
+  // 385 -> 374 us, input gradient 361 -> 353 us against the earlier form, still the fallback below)
+  constexpr bool PFv = true;
   if (PFv && YB == 3 && NTv == 512 && Wd == 80) {
     kern = add ? (NS == 4 ? k_conv3d_fwd16<3, 5, 512, true, true, 4> : k_conv3d_fwd16<3, 5, 512, true, true, 3>)
                : (NS == 4 ? k_conv3d_fwd16<3, 5, 512, false, true, 4> : k_conv3d_fwd16<3, 5, 512, false, true, 3>);
@@ -1113,10 +733,7 @@ static int fwd16_call(const float* x, const float* W, const float* bias, const f
       hipSuccess)
     return TB_ERR_HIP;
   // persistent shares when the (n, yb, z segment) grid leaves CUs idle (C3: 240 blocks of 256)
-  static const int persist_env = [] {
-    const char* e = std::getenv("TEXBIAS_CONV16_PERSIST");
-    return e ? std::atoi(e) : 1;
-  }();
+  constexpr int persist_env = 1;
   a.ncol = N * a.nyb;
   unsigned nblk = (unsigned)(N * a.nyb * a.ZS);
   a.persist = persist_env && per_cu == 1 && (int64_t)a.ncol * D >= 8LL * ncu_count() && nblk % ncu_count() != 0;
@@ -1541,10 +1158,7 @@ static int mfma_call(const float* x, const float* W, const float* bias, const fl
   // 3 chains -- measured slower here, 245 vs 211 us at 32 -> 32, unlike k_conv3d_fwd16).  (Persistent step
   // shares as in k_conv3d_fwd16 measured no gain at 32 -> 32, 186 vs 184 us, and the loop they need cost
   // the 64 -> 64 kernel 107 -> 144 us: not used.)
-  static const int NTv = [] {
-    const char* e = std::getenv("TEXBIAS_CONVMFMA_NT");
-    return e && std::atoi(e) == 512 ? 256 : 256;  // round 5: only the measured best (256) is instantiated
-  }();
+  constexpr int NTv = 256;  // only the measured best (256 threads) is instantiated
   const int NC = NTv == 512 ? 3 : 5;
   const int G = C / 16;
   S1Args a{};

@@ -1016,12 +1016,8 @@ int launch(const WgArgs& a, int blocks_y, size_t lds, hipStream_t st) {
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_wgrad<S, TX, SEG>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return TB_ERR_HIP;
-  // two blocks per CU over the whole chip (TEXBIAS_WGRAD_BLOCKS overrides, tuning), never more
-  // chunks than exist
-  static const int target = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_BLOCKS");
-    return e ? std::atoi(e) : 512;
-  }();
+  // two blocks per CU over the whole chip, never more chunks than exist
+  constexpr int target = 512;
   int64_t gx = (target + blocks_y - 1) / blocks_y;
   if (gx > a.nchunks) gx = a.nchunks;
   if (gx < 1) gx = 1;
@@ -1053,10 +1049,7 @@ int wg_setup_mz(WgArgs& a, int& seg, int& by, size_t& lds, int N, int M, int Cc,
   seg = (((Wo > a.xcols ? Wo : a.xcols) + 63) / 64);
   if (seg > 4) return TB_ERR_UNSUPPORTED_SIZE;
   a.YB = 0;
-  static const int yb_max = [] {  // TEXBIAS_WGRAD_MZ_YB caps the rows per chunk (tuning)
-    const char* e = std::getenv("TEXBIAS_WGRAD_MZ_YB");
-    return e ? std::atoi(e) : 4;  // 3->3 at 2x240x240x160: YB 8 / 512 blocks 530 us, YB 4 / 1024 blocks 462 us
-  }();
+  constexpr int yb_max = 4;  // 3->3 at 2x240x240x160: YB 8 / 512 blocks 530 us, YB 4 / 1024 blocks 462 us
   for (int yb : {8, 4, 2, 1}) {
     if ((yb > 1 && yb > Ho) || yb > yb_max) continue;
     const int yr = yb + 2;
@@ -1081,10 +1074,7 @@ int launch_mz(const WgArgs& a, size_t lds, hipStream_t st) {
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3d_wgrad_mz<SEG>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return TB_ERR_HIP;
-  static const int target = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_MZ_BLOCKS");
-    return e ? std::atoi(e) : 1024;
-  }();
+  constexpr int target = 1024;
   int64_t gx = target;
   if (gx > a.nchunks) gx = a.nchunks;
   if (gx < 1) gx = 1;
@@ -1093,10 +1083,7 @@ int launch_mz(const WgArgs& a, size_t lds, hipStream_t st) {
 }
 
 bool use_mz(int M, int Cc, int stride) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_MZ");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool on = true;
   return on && stride == 1 && M <= 5 && Cc <= 5;
 }
 
@@ -1119,10 +1106,7 @@ int wg_setup(WgArgs& a, int& seg, int& TX, int& by, size_t& lds, int N, int M, i
   if (seg > 4) return TB_ERR_UNSUPPORTED_SIZE;
   const int prem = TX == 3 ? 3 : 2;                     // plane pitch mod 32 (bank spread of B reads)
   a.YB = 0;
-  static const int yb_max = [] {  // TEXBIAS_WGRAD_YB caps the rows per chunk (tuning)
-    const char* e = std::getenv("TEXBIAS_WGRAD_YB");
-    return e ? std::atoi(e) : 8;
-  }();
+  constexpr int yb_max = 8;
   for (int yb : {8, 4, 2, 1}) {
     if ((yb > 1 && yb > Ho) || yb > yb_max) continue;
     const int yr = stride * (yb - 1) + 3;
@@ -1147,10 +1131,7 @@ int wg_setup(WgArgs& a, int& seg, int& TX, int& by, size_t& lds, int N, int M, i
 // z-marching stride-1 kernel (k_conv3d_wgrad_zm): 16-channel tiles, W % 4 == 0 (16-B rows), W <= 80,
 // at least 8 output and 8 input channels (the few-channel layers keep their own tilings)
 bool use_zm(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZM");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool on = true;
   return on && stride == 1 && M >= 8 && Cc >= 8 && Do == Di && Ho == Hi && Wo == Wi && Wo % 4 == 0 && Wo <= 80 &&
          (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
 }
@@ -1158,10 +1139,7 @@ bool use_zm(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, i
 int zm_setup(ZmArgs& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, int H, int W, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.D = D; a.H = H; a.W = W;
   a.W4 = W;  // W % 4 == 0
-  static const int yb_env = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZM_YB");
-    return e ? std::atoi(e) : 0;
-  }();
+  constexpr int yb_env = 0;  // rows per block: the first tiling that fits (below)
   a.PX = ((W + 3 + 1) / 2) * 2;  // cols 0..W + 2 (data at 2..W + 1), even (8-B stores)
   a.YB = 0;
   for (int yb : {4, 2}) {
@@ -1217,10 +1195,7 @@ int launch_zm(const ZmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
 // stride-2 z-marching kernel (k_conv3d_wgrad_zm2): >= 8 input channels, Wo % 4 == 0, Wo <= 40,
 // input rows of exactly 2 Wo (padding 1)
 bool use_zm2(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZM2");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool on = true;
   return on && stride == 2 && M >= 8 && Cc >= 8 && Wo % 4 == 0 && Wo <= 40 && Wi == 2 * Wo && Hi == 2 * Ho &&
          Di == 2 * Do && (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
 }
@@ -1229,10 +1204,7 @@ int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do,
               int Wi, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.Do = Do; a.Ho = Ho; a.Wo = Wo; a.Di = Di; a.Hi = Hi; a.Wi = Wi;
   a.PX = ((2 * Wo + 3 + 1) / 2) * 2;
-  static const int yb_env = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZM2_YB");
-    return e ? std::atoi(e) : 0;
-  }();
+  constexpr int yb_env = 0;  // rows per block: the first tiling that fits (below)
   a.YB = 0;
   for (int yb : {2, 1}) {  // two output rows per block where the ring fits: twice the MFMAs per staged plane
     if ((yb_env && yb != yb_env) || yb > Ho) continue;
@@ -1282,10 +1254,7 @@ int launch_zm2(const Zm2Args& a, size_t lds, dim3 grid, hipStream_t st) {
 
 // few-channel stride-2 kernel (k_conv3d_wgrad_zf2): Cc <= 5, Wo % 4 == 0, Wo <= 80, 2x input rows
 bool use_zf2(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZF2");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool on = true;
   return on && stride == 2 && Cc <= 5 && Wo % 4 == 0 && Wo <= 80 && Wi == 2 * Wo && Hi == 2 * Ho && Di == 2 * Do &&
          (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
 }
@@ -1342,20 +1311,14 @@ int launch_zf2(const Zf2Args& a, int MT, size_t lds, dim3 grid, hipStream_t st) 
 
 // few-channel stride-1 z-marching kernel (k_conv3d_wgrad_zf1): 9 M <= 32, 3 Cc <= 16, W % 4 == 0
 bool use_zf1(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, int Wi, const void* G, const void* X) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZF1");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool on = true;
   return on && stride == 1 && M <= 3 && Cc <= 5 && Do == Di && Ho == Hi && Wo == Wi && Wo % 4 == 0 && Wo <= 256 &&
          (reinterpret_cast<uintptr_t>(G) & 15) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
 }
 
 int zf1_setup(Zf1Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, int H, int W, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.D = D; a.H = H; a.W = W;
-  static const int yb_env = [] {
-    const char* e = std::getenv("TEXBIAS_WGRAD_ZF1_YB");
-    return e ? std::atoi(e) : 0;
-  }();
+  constexpr int yb_env = 0;  // rows per block: the first tiling that fits (below)
   // pitches: rows of one G channel 4 banks apart, channels and slots spread over the banks
   a.GR = pad_mod32(W, 4);
   a.XR = pad_mod32(W + 8, 4);

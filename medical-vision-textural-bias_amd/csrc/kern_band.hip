@@ -1207,8 +1207,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
     }
     __syncthreads();
     if (diag & 32) return;
-    if (c0 == ub)
-      for (int i = (wv >> 2) * a.stagger; i > 0; --i) __builtin_amdgcn_s_sleep(8);
     for (int un = c0 + ((wv - ((c0 - ub) % NW) + NW) % NW); un < c1; un += NW) {  // (un - ub) % NW == wave
       const int slab = un / ntw, tw_ = un - slab * ntw, slot = slab - s0;
       const int bcl = slab / H, h = slab - bcl * H, bc = a.bc0 + bcl;
@@ -1523,8 +1521,6 @@ int band_occupancy(K kern, size_t lds, int nt, int cap) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, nt, lds) != hipSuccess || occ < 1)
     occ = (int)(163840 / (lds ? lds : 1));
   occ = occ < 1 ? 1 : (occ > cap ? cap : occ);
-  if (std::getenv("TEXBIAS_BAND_VERBOSE"))
-    std::fprintf(stderr, "[texbias] band kernel %p: lds %zu B, %d workgroups/CU\n", key.first, lds, occ);
   cache[key] = occ;
   return occ;
 }
@@ -1562,11 +1558,7 @@ hipError_t launch_inv16_t(BandInvArgs& a, int ncu, hipStream_t st) {
   // slab slots: a 16-wave workgroup (one per CU) holds every slab of its unit range when LDS allows,
   // so its units run after ONE fragment batch (C2: 32 slabs per workgroup, 3 batches of 12 before)
   int slots = band_slots16(NW);
-  static const int env_slots = [] {  // measurement: TEXBIAS_INV16_SLOTS=n caps the 16-wave slots
-    const char* e = std::getenv("TEXBIAS_INV16_SLOTS");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (NW == 16 && env_slots <= 0) {
+  if (NW == 16) {
     const int ntw = (a.pl.W + 31) / 32, nslab = a.pl.H * a.nbc;
     const int grid = nslab < ncu ? nslab : ncu;
     const int per = (nslab * ntw + grid - 1) / grid;
@@ -1604,20 +1596,7 @@ hipError_t launch_inv_t(const BandInvArgs& a, int ncu, hipStream_t st) {
 }  // namespace
 
 bool band_fwd_use_ct(int D, int NT2) {
-  static const bool ct_on = [] {  // TEXBIAS_BAND_FWD_CT=0: the runtime-D kernels (measurement)
-    const char* e = std::getenv("TEXBIAS_BAND_FWD_CT");
-    return !(e && e[0] == '0');
-  }();
-  return ct_on && band_fwd_ct(D, NT2);
-}
-
-// the split-f16 D product (k_band_fwd<..., true>) where it applies; TEXBIAS_BAND_FWD16=0: the f32 one
-bool band_fwd16_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_BAND_FWD16");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  return band_fwd_ct(D, NT2);
 }
 
 hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
@@ -1627,7 +1606,7 @@ hipError_t launch_band_fwd(BandFwdArgs& a, int ncu, hipStream_t st) {
   if (ct) {
     // split-f16 D product for D = 155 (C3: 63.2 -> 61.6 us with flushed caches, level in the train-step
     // bench); D = 128 (C2) keeps the f32 product (its 8 KB strips: 57.9 vs 59.6 us in the C2 bench)
-    const bool f16 = band_fwd16_on() && a.tbt16 && a.vec && a.pl.D == 155;
+    const bool f16 = a.tbt16 && a.vec && a.pl.D == 155;
     const size_t lds16 = lds + (size_t)band_fwd16_ks(a.pl.D) * 4 * 64 * 16 - (((size_t)a.pl.W * 8 + 15) & ~(size_t)15);
     if (f16) return k1 ? launch_fwd_t<1, 1, 155, true>(a, lds16, ncu, st) : launch_fwd_t<1, 2, 155, true>(a, lds16, ncu, st);
     if (a.pl.D == 155) {

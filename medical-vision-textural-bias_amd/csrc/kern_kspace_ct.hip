@@ -214,30 +214,17 @@ bool kspace_ct_supported(int H) {
 // 16 columns on 128-thread workgroups by default (4 per CU by LDS: 196 us per C3 launch), 32 on
 // 256 threads (2 per CU: 206 us), or 8 on 64 threads
 static bool use_pair(int ncols) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_KSPACE_PAIR");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on && ncols % ct::kCtTileT2 == 0;
+  return ncols % ct::kCtTileT2 == 0;
 }
 static int pair_tile() {
-  static const int t = [] {
-    const char* e = std::getenv("TEXBIAS_KSPACE_T2");
-    const int v = e ? std::atoi(e) : 16;
-    return (v == 8 || v == 32) ? v : 16;
-  }();
-  return t;
+  return 16;
 }
 
 int kspace_ct_tile(int ncols) { return use_pair(ncols) ? pair_tile() : ct::kCtTileT; }
 
 // persistent pass B (TEXBIAS_KSPACE_PERSIST=0: the one-tile-per-workgroup grid)
 static bool use_persist() {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_KSPACE_PERSIST");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+  return true;
 }
 
 template <class K>
@@ -258,11 +245,7 @@ bool kspace_ct_persistent(int ncols) { return use_pair(ncols) && use_persist() &
 // the launch's programs all of one mask-op kind -> pass B's unrolled middle phase
 // (TEXBIAS_KSPACE_MASK=0: always the generic one)
 static int launch_mask_kind(const KspaceArgs& a) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_KSPACE_MASK");
-    return !(e && std::atoi(e) == 0);
-  }();
-  if (!on || a.nbc < 1) return ct::MASK_GENERIC;
+  if (a.nbc < 1) return ct::MASK_GENERIC;
   const int s0 = a.cofs / a.C, s1 = (a.cofs + a.nbc - 1) / a.C;
   return ct::mask_kind(a.ops.s + s0, s1 - s0 + 1);
 }

@@ -479,18 +479,10 @@ extern "C" int tb_debug_slab_prof_clear() {
 // variant (slab_ct.h) at 512 threads for plans with odd R0 and D: it holds two butterflies'
 // inputs across a barrier, which fits the register file only at 2 waves per SIMD.
 static int ct_nt() {
-  static const int nt = [] {
-    const char* e = std::getenv("TEXBIAS_CT_NT");
-    return (e && std::atoi(e) == 512) ? 512 : 768;
-  }();
-  return nt;
+  return 768;
 }
 static int ct_fuse() {
-  static const int f = [] {
-    const char* e = std::getenv("TEXBIAS_CT_FUSE");
-    return e ? std::atoi(e) : 2;
-  }();
-  return f;
+  return 2;
 }
 
 bool slab_ct_supported(int W, int D) {
@@ -502,20 +494,12 @@ bool slab_ct_supported(int W, int D) {
 
 // 16-B staged loads when the slabs are contiguous and 16-B aligned (TEXBIAS_SLAB_RAW16=0: off)
 static bool raw16_ok(const SlabFwdArgs& a) {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_SLAB_RAW16");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on && a.sw == a.pl.D && a.sh % 4 == 0 && a.sbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
+  return a.sw == a.pl.D && a.sh % 4 == 0 && a.sbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
          (a.pl.W * a.pl.D) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.S) & 15) == 0;
 }
 
 static bool raw16_early() {
-  static const bool on = [] {
-    const char* e = std::getenv("TEXBIAS_SLAB_EARLY");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+  return true;
 }
 
 hipError_t launch_slab_fwd_ct(const SlabFwdArgs& a, int ncu, hipStream_t st) {
@@ -562,18 +546,8 @@ bool slab_half_supported(int W, int D) {
 // TEXBIAS_HALF_CFG / TEXBIAS_HALF_CFG_INV (tuning, passes A / C): 0 = 256 threads with the fused DU / RE
 // phase, 1 = 256 threads unfused, 2 = 512 threads unfused, 3 = 768 threads unfused.  Measured on the
 // gibbs-aug C3 chain (A / C us): 0: 220 / 207, 1: 224 / 211, 2: 184 / 167, 3: 224 / 151 -> A 2, C 3.
-static int half_cfg_env(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-static int half_cfg() {
-  static const int c = half_cfg_env("TEXBIAS_HALF_CFG", 2);
-  return c;
-}
-static int half_cfg_inv() {
-  static const int c = half_cfg_env("TEXBIAS_HALF_CFG_INV", std::getenv("TEXBIAS_HALF_CFG") ? half_cfg() : 3);
-  return c;
-}
+static int half_cfg() { return 2; }
+static int half_cfg_inv() { return 3; }
 
 template <class K, class A>
 static hipError_t launch_half(K kern, int nt, size_t lds, int units, const A& a, hipStream_t st) {

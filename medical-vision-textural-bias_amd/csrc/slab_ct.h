@@ -584,7 +584,7 @@ TB_HD void c_twiddle_half(const v2* lds, v2* r, int e, int it) {
 }
 
 // Slab shapes (W, D) with a compile-time plan in the device library
-#define TB_CT_SLAB_SHAPES(X) X(240, 155) X(128, 128)
+#define TB_CT_SLAB_SHAPES(X) X(240, 155) X(128, 128) X(128, 64)
 // ... of which these run as half units (split spectrum; W/2 two-stage, half slab <= 80 KB of LDS)
 #define TB_CT_HALF_SHAPES(X) X(240, 155)
 

@@ -69,13 +69,10 @@ hipEvent_t ev_get() {
   }
   // Timing-only events: no system-scope release / acquire around the pass (hipEventDisableSystemFence),
   // so the end stamp is not delayed by an L2 write-back and the pass does not start on invalidated
-  // caches -- the stamps bracket the kernel itself.  TEXBIAS_EVENT_FENCE=1: default events (A/B).
-  static const unsigned flags = [] {
-    const char* e = std::getenv("TEXBIAS_EVENT_FENCE");
-    return (e && e[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence;
-  }();
+  // caches -- the stamps bracket the kernel itself (round 6: every pass 1-2 us shorter than with
+  // default events, which rocprofv3's kernel durations confirm).
   hipEvent_t e = nullptr;
-  if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
   return e;
 }
 struct Timer {  // records [begin, end) of one pass when timing is enabled
@@ -293,11 +290,7 @@ bool needs_all(const tb_axis& ax) {
 
 int pick_tile(int H, int lds_max) {
   // ~32 KB tiles (measured best of 16/32/64 KB at H = 240: 4 workgroups per CU, 128-B rows)
-  // (TEXBIAS_TILE_BYTES overrides the budget for tuning)
-  static const int budget = [] {
-    const char* e = std::getenv("TEXBIAS_TILE_BYTES");
-    return e ? std::atoi(e) : 32768;
-  }();
+  constexpr int budget = 32768;
   int T = budget / (H * 8);
   if (T > 64) T = 64;
   if (T >= 16) T &= ~7;   // whole 64-B segments per tile row
@@ -517,15 +510,8 @@ static bool use_half(const tb_plan* p) { return g_half && use_ct_slab(p) && p->c
 // 2..4 channel-volumes keep the spectrum within the Infinity Cache between passes, but measured
 // slower at C3 (0.99 / 0.94 / 0.89 vs 0.85 ms per step: the passes are latency-bound, not
 // HBM-bound, and smaller launches leave more of the chip idle in their tails).
-static int g_chunk_env = [] {
-  const char* e = std::getenv("TEXBIAS_CHUNK_BC");
-  return e ? std::atoi(e) : 0;
-}();
 static int g_chunk = -1;  // tb_set_chain_chunk
-static int chunk_bc(const tb_plan*) {
-  if (g_chunk >= 0) return g_chunk;
-  return g_chunk_env > 0 ? g_chunk_env : 0;
-}
+static int chunk_bc(const tb_plan*) { return g_chunk > 0 ? g_chunk : 0; }
 
 template <int RS>
 static int launch_slab_fwd(const tb_plan* p, const float* x, const int64_t* xs, cf* S, int bc0, int nbc,
@@ -563,13 +549,6 @@ static bool g_wrap = [] {
 static bool g_inv16 = [] {
   const char* e = std::getenv("TEXBIAS_INV16");
   return !(e && e[0] == '0');
-}();
-// Pass C' (split f16): the 4 waves a SIMD holds start their first unit this many 512-cycle sleeps
-// apart (wave w: (w / 4) * stagger), so their compute and store phases interleave instead of running
-// in lockstep after the prologue barrier.  TEXBIAS_INV16_STAGGER overrides.
-static int g_inv16_stagger = [] {
-  const char* e = std::getenv("TEXBIAS_INV16_STAGGER");
-  return e ? (int)std::strtol(e, nullptr, 0) : 0;
 }();
 // measurement only: TEXBIAS_BAND_DIAG=0xIIFF skips stages of A' (FF) / C' (II); results invalid
 static int g_band_diag = [] {
@@ -874,7 +853,6 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ia.T16 = ws + wl.off_t16;
     ia.g = g;
     ia.diag = (g_band_diag >> 8) & 0xffff;
-    ia.stagger = g_inv16_stagger;
     ia.cnt = g.cat ? reinterpret_cast<uint32_t*>(ws + wl.off_cnt) : nullptr;
     for (int i = 0; i < nb; ++i) ia.sp[i] = sp[i];
     TB_HIP(tb::launch_band_inv(ia, p->ncu, st));
@@ -901,13 +879,9 @@ static int run_generic(const tb_plan* p, const float* x, const int64_t* xs, floa
 // launch group): per-sample chains would let k_point_apply re-read a 142 MB sample from the Infinity
 // Cache, but cost more in launches and smaller grids than they saved.
 static int point_chunk(const tb_plan* p, int C) {
-  static const int env = [] {
-    const char* e = std::getenv("TEXBIAS_POINT_CHUNK");
-    return e ? std::atoi(e) : -1;
-  }();
   (void)p;
   (void)C;
-  return env >= 0 ? env : 0;  // measured: one sample per chain 0.240 vs 0.213 ms per C3 step (planes)
+  return 0;  // measured: one sample per chain 0.240 vs 0.213 ms per C3 step (planes)
 }
 
 static int run_point(const tb_plan* p, const float* x, const int64_t* xs, float* y, const int64_t* ys, int y_pad,

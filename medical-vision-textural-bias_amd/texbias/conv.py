@@ -24,8 +24,9 @@ from ._lib import check, lib
 # TEXBIAS_WGRAD=0 leaves every layer to MIOpen (e.g. to compare with MIOpen's Find choice)
 MIN_K_PER_OUTPUT = 64
 ENABLED = os.environ.get("TEXBIAS_WGRAD", "1") != "0"
-CONVT64 = os.environ.get("TEXBIAS_CONVT64", "1") != "0"
-CONVMFMA = os.environ.get("TEXBIAS_CONVMFMA", "1") != "0"
+CONVT64 = True   # module switches (tests and measurement scripts set them; no environment variables)
+CONVMFMA = True
+CONV16 = True
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -119,17 +120,17 @@ def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, pa
 GEMM = os.environ.get("TEXBIAS_CONVGEMM", "1") != "0"
 # the sub-pixel (ConvTranspose3d forward / stride-2 input gradient) and 1x1x1 forms of the GEMM kernel
 # measured slower than MIOpen at the C3 shapes (scripts/diag/gemm_conv_bench.py): off unless asked for
-GEMM_T = os.environ.get("TEXBIAS_CONVGEMM_T", "0") != "0"
-GEMM_1 = os.environ.get("TEXBIAS_CONVGEMM_1X1", "0") != "0"
+GEMM_T = False
+GEMM_1 = False
 # ConvTranspose3d input gradient (a stride-2 Conv3d of dY) on the GEMM kernel while its forward stays on MIOpen
 # (off: up2 128 -> 32 at C3 measured 2 x 100 us + reduce in the step vs MIOpen/CK's 152 us)
-GEMM_TDX = os.environ.get("TEXBIAS_CONVGEMM_TDX", "0") != "0"
+GEMM_TDX = False
 # the identity-residual unit's input gradient dconv(dY) + dY summed in the 16-channel kernel's store (its add
 # values fetched at the start of each step), instead of a separate add pass
-FWD16_DX_ADD = os.environ.get("TEXBIAS_FWD16_DX_ADD", "1") != "0"
+FWD16_DX_ADD = True
 # the same for the 32 / 64-channel kernel: off (its add form holds 256 VGPRs, one wave per SIMD at 32 -> 32
 # instead of two, for a 6-19 us add pass)
-MFMA_DX_ADD = os.environ.get("TEXBIAS_MFMA_DX_ADD", "0") != "0"
+MFMA_DX_ADD = False
 
 
 def _gemm_geom_ok(x: torch.Tensor, w: torch.Tensor, stride, padding, transposed: bool, output_padding) -> bool:
@@ -286,7 +287,7 @@ def s2_dgrad_applies(gy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride,
 
 def convT64_applies(x: torch.Tensor, w: torch.Tensor, stride, padding, output_padding) -> bool:
     """ConvTranspose3d(64 -> 16, 3, 2, 1, output_padding 1), rows of 4k <= 64 floats: forward on
-    k_convT_mfma64 (TEXBIAS_CONVT64=0: ATen).  Input and weight gradients stay where _ConvFn puts them."""
+    k_convT_mfma64 (CONVT64 = False: ATen).  Input and weight gradients stay where _ConvFn puts them."""
     return CONVT64 and custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape) == (64, 16, 3, 3, 3) and \
         x.shape[1] == 64 and \
         tuple(stride) == (2, 2, 2) and tuple(padding) == (1, 1, 1) and tuple(output_padding) == (1, 1, 1) and \
@@ -331,7 +332,7 @@ def conv16_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     input gradient) + the z-marching weight gradient."""
     return custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape) == (16, 16, 3, 3, 3) and \
         x.shape[1] == 16 and tuple(stride) == (1, 1, 1) and tuple(padding) == (1, 1, 1) and x.shape[-1] % 16 == 0 and \
-        x.shape[-1] <= 80 and x.data_ptr() % 16 == 0 and os.environ.get("TEXBIAS_CONV16", "1") != "0"
+        x.shape[-1] <= 80 and x.data_ptr() % 16 == 0 and CONV16
 
 
 def conv_mfma(x: torch.Tensor, w: torch.Tensor, b, add=None) -> torch.Tensor:
@@ -369,7 +370,7 @@ def conv_mfma_dgrad(gy: torch.Tensor, w: torch.Tensor, add=None) -> torch.Tensor
 def conv_mfma_applies(x: torch.Tensor, w: torch.Tensor, stride, padding) -> bool:
     """Conv3d(32 -> 32) with rows of 4k <= 64 floats, or Conv3d(64 -> 64) with rows <= 48, stride 1,
     padding 1: k_conv3d_mfma_s1 (forward and input gradient) + the z-marching weight gradient
-    (TEXBIAS_CONVMFMA=0: _ConvFn)."""
+    (CONVMFMA = False: _ConvFn)."""
     if not (custom_backward_applies(x, w) and x.dim() == 5 and tuple(w.shape[2:]) == (3, 3, 3) and
             x.shape[1] == w.shape[1]):
         return False

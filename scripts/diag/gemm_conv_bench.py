@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """HIP-event timings of the implicit-GEMM convolutions (csrc/conv_gemm.hip) at the U-Net's C3 layer
-shapes, MIOpen's forward / input gradient for the same layer beside them.  TEXBIAS_CG_TILE picks a tile."""
+shapes, MIOpen's forward / input gradient for the same layer beside them."""
 import os
 import sys
 

@@ -175,7 +175,7 @@ def test_residual_add_epilogues(conv, kind, c, sp):
 @pytest.mark.parametrize("cin,cout,shape", [(128, 32, (1, 6, 4, 6)), (128, 32, (2, 30, 30, 20)), (64, 16, (2, 3, 5, 4))])
 def test_convT_input_grad_route(conv, cin, cout, shape, monkeypatch):
     """ConvTranspose3d whose forward stays on MIOpen (the sub-pixel GEMM form is off by default): with
-    TEXBIAS_CONVGEMM_TDX its input gradient runs on the GEMM kernel as a stride-2 Conv3d of dY (Route.dx
+    conv.GEMM_TDX its input gradient runs on the GEMM kernel as a stride-2 Conv3d of dY (Route.dx
     "gemm"), vs ATen and float64;
     the C3 up2 shape (128 -> 32 at 30 x 30 x 20) included."""
     monkeypatch.setattr(conv, "GEMM_TDX", True)

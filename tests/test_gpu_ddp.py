@@ -8,7 +8,7 @@ BASELINE config 4's workload at the reference drivers' crop size (2 x 4 x 128 x 
 filter draws (r, I, wrap alpha, S&P p) on its own batch, then ``TrainStep(distributed=True)`` on the
 reference U-Net(4 -> 3) with the texbias conv / InstanceNorm+PReLU / Dice kernels.  Checked:
   * the ranks' filter draws differ, and every non-transposed 3x3x3 convolution routed to a texbias
-    kernel (no ``aten`` route), the full- and half-resolution layers' weight gradients too;
+    kernel (no ``aten`` route), with the direct kernels' weight gradients on texbias too;
   * after 3 steps the replicas are bit-identical (every parameter and Adam state);
   * the first step's averaged gradients equal ONE process's batch-of-4 step (the two ranks' batches
     concatenated) -- the whole-step bar of tests/test_gpu_norm.py (per tensor, vs the largest gradient
@@ -141,8 +141,13 @@ def test_ddp_two_ranks_hip_kernels(gpu, heartbeat):
     assert r0["routes"] and r0["routes"] == r1["routes"]
     conv3 = [r for r in r0["routes"] if r[1] == 3 and not r[2]]
     assert conv3 and all(r[3] != "aten" for r in conv3), conv3
-    top = [r for r in r0["routes"] if r[1] == 3 and min(r[0][2:]) >= SHAPE[2] // 2]
-    assert top and all(r[5] for r in top), top
+    # the direct / z-march kernels take their layers' weight gradients too (the stacked stride-2 and
+    # transposed GEMM-route layers keep MIOpen's, as in the C3 step)
+    direct = [r for r in r0["routes"] if r[3] in ("fwd16", "mfma", "small", "fewin", "fewout")]
+    assert direct and all(r[5] for r in direct), direct
+    kinds = {(r[0][1:], r[2]): r[3] for r in r0["routes"]}
+    assert kinds[((4,) + SHAPE, False)] == "fewin" and kinds[((3,) + SHAPE, False)] == "small"
+    assert kinds[((16,) + tuple(n // 2 for n in SHAPE), False)] in ("fwd16", "gemm")
     # the averaged first-step gradients == one process's batch-of-4 step on the ranks' filtered batches
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -157,7 +162,10 @@ def test_ddp_two_ranks_hip_kernels(gpu, heartbeat):
     scale = max(g.abs().max().item() for g in g4)
     for a, b in zip(r0["grads"], g4):
         err = (a.double() - b.double()).abs().max().item()
-        assert err <= 2e-3 * max(b.abs().max().item(), 1e-4 * scale), (err, b.abs().max().item())
+        # + floor: tensors whose true gradient is exactly zero (conv biases in front of an InstanceNorm) hold
+        # float32 rounding sums whose order differs between the two runs -- up to ~5e-6 of the largest
+        # gradient at 2 x 4 x 128 x 128 x 64
+        assert err <= 2e-3 * b.abs().max().item() + 1e-5 * scale, (err, b.abs().max().item(), scale)
     # gibbs_gd: one alpha on every replica, moved from 0.7
     assert torch.equal(r0["alpha"], r1["alpha"])
     assert abs(r0["alpha"].item() - 0.7) > 0.0
