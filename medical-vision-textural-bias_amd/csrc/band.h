@@ -109,6 +109,7 @@ struct BandMidArgs {
   int p0[TB_MAX_BATCH];  // g.cat: the first V point row (pair) of each sample of the launch
   int16_t pkd[TB_MAX_BATCH * BAND_MAX_PTS];  // g.cat: kd of the launch's points in row order
   void* T16;        // g.cat: synthesis-table fragments for pass C' (written by k_band_tab16)
+  uint32_t* mm;     // g.cat: per-sample min/max keys, initialised here for pass C''s atomics (or null)
   const float* tds; // g.cat: [D/2 + 1][2][NCOL] folded synthesis table (plan table)
   BatchOps ops;
   uint32_t* cnt;    // pass C''s arrival counter, zeroed here (B' runs before every C')

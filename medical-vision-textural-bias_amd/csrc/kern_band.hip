@@ -462,6 +462,8 @@ __global__ __launch_bounds__(64 * BAND_HC_NW) void k_band_hcol(BandMidArgs) {
   cf* P = a.P + (int64_t)bc * H * BAND_FWD_SEGS * ncol;
   constexpr int NT = 64 * BAND_HC_NW;
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && a.cnt) *a.cnt = 0u;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && a.mm && tid < 2 * (a.nbc / a.C))  // pass C''s key atomics start here
+    a.mm[2 * (a.bc0 / a.C) + tid] = (tid & 1) ? 0u : 0xffffffffu;
   for (int hh = tid; hh < H; hh += NT) tw[hh] = ld2(a.pl.tw[0] + hh);
   if (tid < BAND_HC_CB) Pb[H * BAND_HC_CB + tid] = make_float2(0.f, 0.f);
   {  // stage: lane -> (h offset tid >> 4, column tid & 15); UR slab rows x 3 slots in flight
@@ -1036,54 +1038,6 @@ __device__ void band_tab16(const BandMidArgs& a, int t) {
   T[(cc * 2 + 1) * 64 + lane] = fl;
 }
 
-// Per-sample min/max keys without a launch of their own: every workgroup of pass C' counts itself
-// in after its partials are stored (store_partial / arrive_last, kernels.h); the last one to arrive
-// reduces the launch's partials as k_band_minmax does.
-template <int NT>
-__device__ void band_minmax_last_t(const BandInvArgs& a, char* smem) {
-  __shared__ int last;
-  drain_vmem();     // this wave's store_partial calls have completed ...
-  __syncthreads();  // ... for every wave before the count-in
-  if (threadIdx.x == 0) last = arrive_last(a.cnt, gridDim.x);
-  __syncthreads();
-  if (!last) return;
-  float* red = reinterpret_cast<float*>(smem);
-  const int ntw = (a.pl.W + 31) / 32, nb = a.nbc / a.C;
-  const int64_t n = (int64_t)a.C * a.pl.H * ntw;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int b = 0; b < nb; ++b) {
-    const float2* p = a.mmp + (int64_t)b * n;
-    float lo = 3.402823466e38f, hi = -3.402823466e38f;
-    for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * NT) {
-      float2 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = i0 + u * NT < n ? load_partial(p + i0 + u * NT) : make_float2(lo, hi);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        lo = fminf(lo, v[u].x);
-        hi = fmaxf(hi, v[u].y);
-      }
-    }
-    lo = wave_min(lo);
-    hi = wave_max(hi);
-    if (lane == 0) {
-      red[wid] = lo;
-      red[NT / 64 + wid] = hi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int w = 1; w < NT / 64; ++w) {
-        lo = fminf(lo, red[w]);
-        hi = fmaxf(hi, red[NT / 64 + w]);
-      }
-      const int sb = a.bc0 / a.C + b;
-      a.mm[2 * sb] = f2key(lo);
-      a.mm[2 * sb + 1] = f2key(hi);
-    }
-    __syncthreads();
-  }
-}
-
 #ifndef TB_INV16_WPE
 #define TB_INV16_WPE 4  // waves per SIMD the VT = 1 split-f16 kernel is compiled for (register budget)
 #endif
@@ -1168,6 +1122,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
   const int nunit = nslab * ntw;
   const int per = (nunit + (int)gridDim.x - 1) / (int)gridDim.x;
   const int ub = (int)blockIdx.x * per, ue = ub + per < nunit ? ub + per : nunit;
+  __shared__ uint32_t kmm[2 * TB_MAX_BATCH];  // this workgroup's per-sample (min, max) keys
+  if (tid < 2 * TB_MAX_BATCH) kmm[tid] = (tid & 1) ? 0u : 0xffffffffu;
+  __syncthreads();
   for (int c0 = ub; c0 < ue;) {
     const int s0 = c0 / ntw;
     const int slast = (ue - 1) / ntw;
@@ -1404,20 +1361,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(VT == 1
           }
         }
       }
-      if (a.mm) {
+      if (a.mm) {  // the unit's (min, max) into the workgroup's per-sample keys (LDS atomics)
         lo = wave_min(lo);
         hi = wave_max(hi);
         if (lane == 0) {
-          if (a.cnt)
-            store_partial(a.mmp + (int64_t)slab * ntw + tw_, make_float2(lo, hi));
-          else
-            a.mmp[(int64_t)slab * ntw + tw_] = make_float2(lo, hi);
+          const int sl = bcl / a.C;  // sample of the launch
+          atomicMin(&kmm[2 * sl], f2key(lo));
+          atomicMax(&kmm[2 * sl + 1], f2key(hi));
         }
       }
     }
     c0 = c1;
   }
-  if (a.mm && a.cnt) band_minmax_last_t<NT>(a, smem);
+  // one device-scope atomic pair per (workgroup, sample) onto the keys pass B' initialised: no partials,
+  // no last-arriver reduction in the kernel's tail (round 5's hand-off cost C' ~3 us at its end)
+  __syncthreads();
+  if (a.mm && (int)threadIdx.x < a.nbc / a.C && kmm[2 * threadIdx.x] != 0xffffffffu) {
+    const int sk = a.bc0 / a.C + (int)threadIdx.x;
+    atomicMin(&a.mm[2 * sk], kmm[2 * threadIdx.x]);
+    atomicMax(&a.mm[2 * sk + 1], kmm[2 * threadIdx.x + 1]);
+  }
 }
 
 // per-sample keys of the slab partials: one workgroup per sample

@@ -825,6 +825,7 @@ static int run_band(const tb_plan* p, const float* x, const int64_t* xs, float* 
     ma.T16 = ws + wl.off_t16;
     ma.tds = p->tds;
     ma.cnt = reinterpret_cast<uint32_t*>(ws + wl.off_cnt);
+    ma.mm = g.cat ? minmax : nullptr;
     TB_HIP(tb::launch_band_mid(ma, st));
   }
   {
