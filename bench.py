@@ -115,7 +115,7 @@ def parse():
 
 
 # traffic_<config or chain>.json (scripts/make_traffic.py), newest round first
-TRAFFIC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r5", "r4", "r3")]
+TRAFFIC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r6", "r5", "r4", "r3")]
 
 
 def pmc_traffic(kernel: str, launch_bytes: int, key: str = "c3"):

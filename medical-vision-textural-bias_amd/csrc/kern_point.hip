@@ -361,6 +361,7 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
   __syncthreads();
   float* yb = a.y + (int64_t)bc * a.ysbc;
   const bool vout = (a.ysw & 3) == 0 && (a.ysh & 3) == 0 && (reinterpret_cast<uintptr_t>(yb) & 15) == 0;
+  const bool vfull = vout && (ncol & 3) == 0;
   const int nrow = W * NQ;
   const int64_t nall = (int64_t)H * nrow;
   using QW = QuadWalk<PT_QU>;
@@ -386,14 +387,16 @@ __global__ __launch_bounds__(POINT_NT) void k_point_apply(PointArgs) {
           v[j] += rr.x * tj.x - rr.y * tj.y;
         }
       }
+      float vl[4], vh[4];  // columns past D (the zero padding) left out of the min / max
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (d0 + j < D) {
-          lo = fminf(lo, v[j]);
-          hi = fmaxf(hi, v[j]);
-        }
+      for (int j = 0; j < 4; ++j) {
+        vl[j] = d0 + j < D ? v[j] : 3.402823466e38f;
+        vh[j] = d0 + j < D ? v[j] : -3.402823466e38f;
+      }
+      lo = min3_raw(min3_raw(lo, vl[0], vl[1]), vl[2], vl[3]);
+      hi = max3_raw(max3_raw(hi, vh[0], vh[1]), vh[2], vh[3]);
       float* yr = yb + ((uint32_t)h * (uint32_t)a.ysh + (uint32_t)w * (uint32_t)a.ysw);
-      if (vout && d0 + 4 <= ncol) {
+      if (vfull) {  // wave-uniform: every quad of the stored row is whole
         st_stream<TB_NT_STORES>(reinterpret_cast<tb_f4v*>(yr + d0), tb_f4v{v[0], v[1], v[2], v[3]});
       } else {
 #pragma unroll

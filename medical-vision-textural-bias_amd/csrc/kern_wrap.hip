@@ -15,6 +15,7 @@
 #include <map>
 #include <mutex>
 
+
 namespace tb {
 
 namespace {
@@ -193,24 +194,22 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
     const int bc = a.bc0 + bcl, sl = bcl / a.C;
     const int nrow = Wh - 4 * gq < 4 ? Wh - 4 * gq : 4;
     const float w00 = wts[sl][0], w10 = wts[sl][1], w01 = wts[sl][2], w11 = wts[sl][3];
-    // the H / W 2-tap combine at load time (it commutes with T_d; 4 FMAs per voxel)
+    // the H / W 2-tap combine at load time (it commutes with T_d; 4 FMAs per voxel, as packed f32 pairs)
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-      const float4 x0 = v[0][i], x1 = v[1][i], x2 = v[2][i], x3 = v[3][i];
-      float4 y0, y1, y2, y3;
-#define TB_WRAP_COMB(cmp)                                                   \
-  y0.cmp = w00 * x0.cmp + w10 * x1.cmp + w01 * x2.cmp + w11 * x3.cmp;       \
-  y1.cmp = w10 * x0.cmp + w00 * x1.cmp + w11 * x2.cmp + w01 * x3.cmp;       \
-  y2.cmp = w01 * x0.cmp + w11 * x1.cmp + w00 * x2.cmp + w10 * x3.cmp;       \
-  y3.cmp = w11 * x0.cmp + w01 * x1.cmp + w10 * x2.cmp + w00 * x3.cmp;       \
-  mx = fmaxf(mx, fmaxf(fmaxf(fabsf(y0.cmp), fabsf(y1.cmp)), fmaxf(fabsf(y2.cmp), fabsf(y3.cmp))));
-      TB_WRAP_COMB(x) TB_WRAP_COMB(y) TB_WRAP_COMB(z) TB_WRAP_COMB(w)
-#undef TB_WRAP_COMB
-      v[0][i] = y0;
-      v[1][i] = y1;
-      v[2][i] = y2;
-      v[3][i] = y3;
+      const f32x4v x0 = {v[0][i].x, v[0][i].y, v[0][i].z, v[0][i].w}, x1 = {v[1][i].x, v[1][i].y, v[1][i].z, v[1][i].w};
+      const f32x4v x2 = {v[2][i].x, v[2][i].y, v[2][i].z, v[2][i].w}, x3 = {v[3][i].x, v[3][i].y, v[3][i].z, v[3][i].w};
+      const f32x4v y0 = w00 * x0 + w10 * x1 + w01 * x2 + w11 * x3;
+      const f32x4v y1 = w10 * x0 + w00 * x1 + w11 * x2 + w01 * x3;
+      const f32x4v y2 = w01 * x0 + w11 * x1 + w00 * x2 + w10 * x3;
+      const f32x4v y3 = w11 * x0 + w01 * x1 + w10 * x2 + w00 * x3;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) mx = max3_abs(max3_abs(mx, y0[c], y1[c]), y2[c], y3[c]);
+      v[0][i] = make_float4(y0[0], y0[1], y0[2], y0[3]);
+      v[1][i] = make_float4(y1[0], y1[1], y1[2], y1[3]);
+      v[2][i] = make_float4(y2[0], y2[1], y2[2], y2[3]);
+      v[3][i] = make_float4(y3[0], y3[1], y3[2], y3[3]);
     }
     // per-unit power of two: max |scaled| < 2^14 (f16 hi parts in range, lo parts normal)
     int ex;
@@ -222,43 +221,47 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
       for (int i = 0; i < NF; ++i) {
         const int f = lane + 64 * i;
         if (f < D) {  // 4 f < 4 D: inside the role's 4-row chunk
-          const float4 s4 = v[r][i];
-          *reinterpret_cast<float4*>(stg + r * a.RS + 4 * f) = make_float4(s4.x * sx, s4.y * sx, s4.z * sx, s4.w * sx);
+          const f32x4v s4 = f32x4v{v[r][i].x, v[r][i].y, v[r][i].z, v[r][i].w} * sx;
+          *reinterpret_cast<f32x4v*>(stg + r * a.RS + 4 * f) = s4;
         }
       }
     // the wave's next unit: its loads fly during this unit's products and stores
     if (u + WRAP_NT / 64 < ue) load_unit(u + WRAP_NT / 64, v);
-    // ---- T_d: Y^T = K^T X^T in split f16
-    f32x4v acc[NTO];
-#pragma unroll
-    for (int t = 0; t < NTO; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    // ---- T_d: Y^T = K^T X^T in split f16.  K is Toeplitz: the A fragment of (k-step s, tile t) is the
+    // table at 16 j, j = 2 s + NTO - 1 - t.  The tiles are done in two halves of NTH (20 accumulator
+    // registers live, not 40 -- at 3 waves per SIMD a spill reload here waited out the next unit's
+    // loads); per half each distinct fragment is read from LDS once and used for every (s, t) on its
+    // diagonal against the B fragments of all KS k-steps held in registers (per tile the s order, and so
+    // the sums, are those of an s-outer loop).
     const bool rowok = g < nrow;
-#pragma unroll 1
+    h16x8 bh[KS], bl[KS];
+    // k-steps inside D for every row of a full unit read without predicates (wave-uniform test); the
+    // rest compare against a per-unit opaque limit (loop-invariant compares would be hoisted out of the
+    // unit loop as 2 SGPRs of lane mask each, spilled to VGPR lanes)
+    int lim = rowok ? D - 8 * kb : 0;
+    asm volatile("" : "+v"(lim));
+#pragma unroll
     for (int s = 0; s < KS; ++s) {
       float xv[8];
+      if (nrow == 4 && 32 * s + 32 <= D) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[j] = (rowok && 32 * s + 8 * kb + j < D) ? xrd[32 * s + j] : 0.f;
-      h16x8 bh, bl;
+        for (int j = 0; j < 8; ++j) xv[j] = xrd[32 * s + j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = 32 * s + j < lim ? xrd[32 * s + j] : 0.f;
+      }
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {  // packed conversions: v_cvt_pk_f16_f32
         const f32x2v p = {xv[j], xv[j + 1]};
         const h16x2v h = __builtin_convertvector(p, h16x2v);
         const h16x2v l = __builtin_convertvector(p - __builtin_convertvector(h, f32x2v), h16x2v);
-        bh[j] = h[0];
-        bh[j + 1] = h[1];
-        bl[j] = l[0];
-        bl[j + 1] = l[1];
-      }
-#pragma unroll
-      for (int t = 0; t < NTO; ++t) {
-        const h16x8 kh = *reinterpret_cast<const h16x8*>(thp + 32 * s + 16 * (NTO - 1 - t));
-        const h16x8 kl = *reinterpret_cast<const h16x8*>(thp + 8 * L + 32 * s + 16 * (NTO - 1 - t));
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, bl, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, bh, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, bh, acc[t], 0, 0, 0);
+        bh[s][j] = h[0];
+        bh[s][j + 1] = h[1];
+        bl[s][j] = l[0];
+        bl[s][j + 1] = l[1];
       }
     }
-    // ---- epilogue: output row n, columns 16 t + 4 kb + 0..3 (zero past D), per-sample min/max
+    // ---- epilogue setup: output row n, columns 16 t + 4 kb + 0..3 (zero past D), per-sample min/max
     if (sl != cur) {  // wave-uniform
       if (cur >= 0) {
         const float l2 = wave_min(lo), h2 = wave_max(hi);
@@ -278,36 +281,66 @@ __global__ __launch_bounds__(WRAP_NT) __attribute__((amdgpu_waves_per_eu(NTO <= 
     asm volatile("" : "+v"(dq), "+v"(nq));
     const int dqr = rowok ? dq : -(1 << 20), nqr = rowok ? nq : -(1 << 20);
     const bool full = nrow == 4;
-#pragma unroll
-    for (int t = 0; t < NTO; ++t) {
-      if (16 * t >= ncolo) break;  // wave-uniform
+    int Dv = D, nco = ncolo;  // per-unit copies: the tiles' uniform tests are not hoisted (and spilled) either
+    asm volatile("" : "+s"(Dv), "+s"(nco));
+    auto store_tile = [&](int t, const f32x4v& av) {
+      if (16 * t >= nco) return;  // wave-uniform
       const int d0 = 16 * t + 4 * kb;
       float o[4];
-      if (full && 16 * t + 16 <= D) {  // wave-uniform fast path
+      if (full && 16 * t + 16 <= Dv) {  // wave-uniform fast path
+        const f32x4v ov = av * inv;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = acc[t][r] * inv;
-        lo = fminf(lo, fminf(fminf(o[0], o[1]), fminf(o[2], o[3])));
-        hi = fmaxf(hi, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+        for (int r = 0; r < 4; ++r) o[r] = ov[r];
+        lo = min3_raw(min3_raw(lo, o[0], o[1]), o[2], o[3]);
+        hi = max3_raw(max3_raw(hi, o[0], o[1]), o[2], o[3]);
         if (vst) {
-          *reinterpret_cast<float4*>(yrow + d0) = make_float4(o[0], o[1], o[2], o[3]);
-          continue;
+          *reinterpret_cast<f32x4v*>(yrow + d0) = ov;
+          return;
         }
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          o[r] = 16 * t + r < dq ? acc[t][r] * inv : 0.f;
+          o[r] = 16 * t + r < dq ? av[r] * inv : 0.f;
           const bool in = 16 * t + r < dqr;
           lo = fminf(lo, in ? o[r] : FLT_MAX);
           hi = fmaxf(hi, in ? o[r] : -FLT_MAX);
         }
       }
-      if (vst && 16 * t + 16 <= ncolo) {  // wave-uniform: the whole tile inside the stored row
-        if (rowok) *reinterpret_cast<float4*>(yrow + d0) = make_float4(o[0], o[1], o[2], o[3]);
+      if (vst && 16 * t + 16 <= nco) {  // wave-uniform: the whole tile inside the stored row
+        if (rowok) *reinterpret_cast<f32x4v*>(yrow + d0) = f32x4v{o[0], o[1], o[2], o[3]};
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (16 * t + r < nqr) yrow[d0 + r] = o[r];
       }
+    };
+    constexpr int NTH = NTO / 2;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int t0 = NTH * hf;
+      __builtin_amdgcn_sched_barrier(0);  // the halves are not interleaved by the scheduler
+      f32x4v acc[NTH];
+#pragma unroll
+      for (int i = 0; i < NTH; ++i) acc[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 2 * KS + NTO - 2; ++j) {
+        if (j < NTO - t0 - NTH || j > 2 * KS - 2 + NTO - 1 - t0) continue;  // no tile of this half (compile-time)
+        const h16x8 kh = *reinterpret_cast<const h16x8*>(thp + 16 * j);
+        const h16x8 kl = *reinterpret_cast<const h16x8*>(thp + 8 * L + 16 * j);
+        // the three split products of the diagonal's pairs interleaved (consecutive MFMAs on different
+        // accumulators); per accumulator the order kh bl, kl bh, kh bh is kept
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const int t = NTO - 1 - (j - 2 * s);
+            if (t < t0 || t >= t0 + NTH) continue;  // compile-time
+            acc[t - t0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(p == 1 ? kl : kh, p == 0 ? bl[s] : bh[s],
+                                                                 acc[t - t0], 0, 0, 0);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < NTH; ++i) store_tile(t0 + i, acc[i]);
     }
   }
   if (!a.mm) return;

@@ -141,6 +141,26 @@ __device__ __forceinline__ float wave_max(float v) {
   return wave_reduce(v, [](float x, float y) { return fmaxf(x, y); });
 }
 
+// Three-operand min / max (v_min3_f32 / v_max3_f32) without the canonicalising v_max_f32 x, x, x that
+// fminf / fmaxf put on every operand the compiler cannot prove canonical (loop-carried running values,
+// packed-math results): one instruction per two values folded in.  For the running min / max of
+// arithmetic results (a quiet NaN operand is ignored, as by fminf).  max3_abs folds |b|, |c| in.
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max3_abs(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // block min/max -> atomic order-preserving keys (uses the first 2*NT/64 floats of smem after a barrier)
 template <int NT>
 __device__ __forceinline__ void block_minmax_atomic(float lo, float hi, float* red, uint32_t* mm) {

@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-close}; mkdir -p $O
 run() { local n=$1; shift; timeout -k 10 600 python3 -u bench.py "$@" > $O/$n.json 2> $O/$n.err || { echo "$n failed"; tail -5 $O/$n.err; exit 1; }; cut -c1-220 $O/$n.json; }
 run bench_c3
-run bench_c2 --config c2 --no-cpu-baseline
+run bench_c2 --config c2
 run bench_c5 --config c5 --no-cpu-baseline
 run filter_c3 --filter-only --steps 20 --warmup 3 --no-cpu-baseline
 for cfg in c3 c2; do
