@@ -301,6 +301,8 @@ __global__ __launch_bounds__(NT) void k_conv3d_wgrad_mz(WgArgs a) {
 // (16x16x4 f32: rows m, columns c) into 27 accumulators per wave; the waves split the positions and
 // meet in LDS at the end, one float atomic per dW entry per block.  The next plane's slabs are loaded
 // into registers while the current plane's MFMAs run (one barrier per z step).
+constexpr size_t ZM_RED_BYTES = (size_t)27 * 2 * 4 * 64 * 4;  // k_conv3d_wgrad_zm end reduction
+
 struct ZmArgs {
   const float* G;
   const float* X;
@@ -311,8 +313,12 @@ struct ZmArgs {
   int mtiles, ctiles;
 };
 
-template <int YB, int WV>  // WV: most float4 per row (W <= 4 WV)
-__global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
+// NW waves share the block's ring (8: two per SIMD at one block per CU): the row's k-steps are split
+// over NW / YB waves; at the end the waves hand their sums down two at a time through a 2-wave LDS
+// image (55.3 KB, inside the ring's allocation), then one atomic per dW entry per block.
+template <int YB, int WV, int NW>  // WV: most float4 per row (W <= 4 WV)
+__global__ __launch_bounds__(64 * NW) void k_conv3d_wgrad_zm(ZmArgs a) {
+  constexpr int NT = 64 * NW;
   constexpr int NXR = YB + 2;  // staged X rows
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -331,18 +337,18 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
   const int mv = min(16, a.M - m0), cv = min(16, a.Cc - c0);
   const int y0 = yb * YB;
   const int z0 = zs * a.zlen, z1 = min(D, z0 + a.zlen);
-  for (int i = tid; i < 4 * GS + 2 * XS; i += 256) smem[i] = 0.f;  // halos, pads, absent rows stay 0
+  for (int i = tid; i < 4 * GS + 2 * XS; i += NT) smem[i] = 0.f;  // halos, pads, absent rows stay 0
   const int64_t plane = (int64_t)H * W;
   const float* Gb = a.G + ((int64_t)n * a.M + m0) * D * plane;
   const float* Xb = a.X + ((int64_t)n * a.Cc + c0) * D * plane;
   // staging items, fixed per thread for the whole march: global offset within a plane (-1: none)
   // and LDS offset within a slab -- X (c, r, q) with row y0 - 1 + r in range, G (m, yy, q)
   const int W4v = W >> 2;
-  constexpr int NXL = (16 * NXR * WV + 255) / 256, NGL = (16 * YB * WV + 255) / 256;
+  constexpr int NXL = (16 * NXR * WV + NT - 1) / NT, NGL = (16 * YB * WV + NT - 1) / NT;
   int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
 #pragma unroll
   for (int j = 0; j < NXL; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NT * j;
     const int q = i % W4v, t = i / W4v, r = t % NXR, c = t / NXR;
     const int y = y0 - 1 + r;
     const bool ok = c < cv && y >= 0 && y < H;
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NT * j;
     const int q = i % W4v, t = i / W4v, yy = t % YB, m = t / YB;
     const int y = y0 + yy;
     const bool ok = m < mv && y < H;
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
     const float* xb = xsl + (zi & 1) * XS + boff;
     // this wave's k-steps: row yy = wave % YB, x0 over part wave / YB of the row (4 / YB parts);
     // the next k-step's 12 operands are read under the current one's 27 MFMAs (2x unrolled, clamped)
-    const int yy = wave % YB, np = 4 / YB, part = wave / YB;
+    const int yy = wave % YB, np = NW / YB, part = wave / YB;
     const int kb = (kpr * part) / np, ke = (kpr * (part + 1)) / np;
     auto ld = [&](int k, float (&av)[3], float (&bv)[9]) {
       const int kk = k < ke ? k : ke - 1;
@@ -458,20 +464,38 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm(ZmArgs a) {
       if (k < ke) mm(a0, b0);
     }
   }
-  // the waves' sums meet in LDS (the ring is free after this barrier), one atomic per entry
-  __syncthreads();
-  float* red = smem;  // [27][4 waves][4 rr][64 lanes]
+  // the waves' sums meet in LDS two at a time (the ring is free after the first barrier)
+  float* red = smem;  // [27][2 waves][4 rr][64 lanes]
 #pragma unroll
-  for (int j = 0; j < 27; ++j)
+  for (int hw = NW - 2; hw >= 2; hw -= 2) {  // waves hw, hw + 1 hand their sums to hw - 2, hw - 1
+    __syncthreads();
+    if (wave >= hw && wave < hw + 2) {
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[((j * 4 + wave) * 4 + rr) * 64 + lane] = acc[j][rr];
+      for (int j = 0; j < 27; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) red[((j * 2 + wave - hw) * 4 + rr) * 64 + lane] = acc[j][rr];
+    }
+    __syncthreads();
+    if (wave >= hw - 2 && wave < hw) {
+#pragma unroll
+      for (int j = 0; j < 27; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[j][rr] += red[((j * 2 + wave - hw + 2) * 4 + rr) * 64 + lane];
+    }
+  }
   __syncthreads();
-  for (int e = tid; e < 27 * 4 * 64; e += 256) {  // e = (j, rr, lane)
+  if (wave < 2) {
+#pragma unroll
+    for (int j = 0; j < 27; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[((j * 2 + wave) * 4 + rr) * 64 + lane] = acc[j][rr];
+  }
+  __syncthreads();
+  for (int e = tid; e < 27 * 4 * 64; e += NT) {  // e = (j, rr, lane)
     const int ln = e & 63, rr = (e >> 6) & 3, j = e >> 8;
     const int m = (ln >> 4) * 4 + rr, c = ln & 15;
     if (m >= mv || c >= cv) continue;
-    const float v = red[((j * 4 + 0) * 4 + rr) * 64 + ln] + red[((j * 4 + 1) * 4 + rr) * 64 + ln] +
-                    red[((j * 4 + 2) * 4 + rr) * 64 + ln] + red[((j * 4 + 3) * 4 + rr) * 64 + ln];
+    const float v = red[((j * 2 + 0) * 4 + rr) * 64 + ln] + red[((j * 2 + 1) * 4 + rr) * 64 + ln];
     atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], v);
   }
 }
@@ -1139,21 +1163,15 @@ bool use_zm(int M, int Cc, int stride, int Do, int Ho, int Wo, int Di, int Hi, i
 int zm_setup(ZmArgs& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, int H, int W, int ncu) {
   a.N = N; a.M = M; a.Cc = Cc; a.D = D; a.H = H; a.W = W;
   a.W4 = W;  // W % 4 == 0
-  constexpr int yb_env = 0;  // rows per block: the first tiling that fits (below)
   a.PX = ((W + 3 + 1) / 2) * 2;  // cols 0..W + 2 (data at 2..W + 1), even (8-B stores)
   a.YB = 0;
-  for (int yb : {4, 2}) {
-    if (yb_env && yb != yb_env) continue;
+  for (int yb : {4, 2}) {  // rows per block: the first tiling that fits
     const int ms = pad_mod32(yb * a.W4, 2), rx = pad_mod32((yb + 2) * a.PX, 2);
     const size_t bytes = (size_t)4 * (4 * 16 * ms + 2 * 16 * rx);
-    if (bytes <= 163840 && bytes >= (size_t)27 * 4 * 4 * 64 * 4) {
+    if (bytes <= 163840) {
       a.YB = yb; a.MS = ms; a.RX = rx;
-      lds = bytes;
-      break;
-    }
-    if (bytes <= 163840) {  // the end's reduction needs 110.6 KB
-      a.YB = yb; a.MS = ms; a.RX = rx;
-      lds = (size_t)27 * 4 * 4 * 64 * 4;
+      lds = bytes > ZM_RED_BYTES ? bytes : ZM_RED_BYTES;  // the end's 2-wave reduction image: 55.3 KB
+      if (lds < 81920 + 16) lds = 81920 + 16;  // one block per CU (two 4-wave blocks measured slower: 212 -> 281 us at 32 -> 32)
       break;
     }
   }
@@ -1161,15 +1179,15 @@ int zm_setup(ZmArgs& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, in
   a.nyb = (H + a.YB - 1) / a.YB;
   a.mtiles = (M + 15) / 16;
   a.ctiles = (Cc + 15) / 16;
-  // z segments: one block per CU at a time (the ring fills the LDS), so the launch takes
-  // ceil(blocks / CUs) rounds of zlen + 2 plane steps (two ring-fill planes per segment): the
-  // segment length minimising that
+  // z segments: the launch takes ceil(blocks / (CUs x blocks per CU)) rounds of zlen + 2 plane steps
+  // (two ring-fill planes per segment): the segment length minimising that
+  const int per_cu = 1;
   const int base = N * a.nyb * a.mtiles * a.ctiles;
   int best = 1 << 30;
   a.zlen = D;
   for (int zl = D; zl >= 4 || zl == D; --zl) {
     const int zs = (D + zl - 1) / zl;
-    const int rounds = (base * zs + ncu - 1) / ncu;
+    const int rounds = (base * zs + ncu * per_cu - 1) / (ncu * per_cu);
     const int cost = rounds * (zl + 2);
     if (cost < best) {
       best = cost;
@@ -1182,13 +1200,15 @@ int zm_setup(ZmArgs& a, size_t& lds, dim3& grid, int N, int M, int Cc, int D, in
   return TB_OK;
 }
 
+// 8 waves per block (one block per CU: two waves per SIMD; 4-wave blocks two per CU measured slower,
+// 4-wave blocks one per CU 7 -- 20 us slower per call)
 int launch_zm(const ZmArgs& a, size_t lds, dim3 grid, hipStream_t st) {
-  auto kern = a.W <= 40 ? (a.YB == 4 ? k_conv3d_wgrad_zm<4, 10> : k_conv3d_wgrad_zm<2, 10>)
-                        : (a.YB == 4 ? k_conv3d_wgrad_zm<4, 20> : k_conv3d_wgrad_zm<2, 20>);
+  auto kern = a.W > 40 ? (a.YB == 4 ? k_conv3d_wgrad_zm<4, 20, 8> : k_conv3d_wgrad_zm<2, 20, 8>)
+                       : (a.YB == 4 ? k_conv3d_wgrad_zm<4, 10, 8> : k_conv3d_wgrad_zm<2, 10, 8>);
   const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 

@@ -80,15 +80,12 @@ struct StripSrc {
 //   other even D -- pitch D + 1, element-wise.
 template <int DC>
 struct Strip {
-  // Every lane issues all FWD_PF loads (indices past the strip clamped to its last vector): conditional
-  // loads leave the compiler unable to count the loads issued after an older one, so a later wait for
-  // that older load (pass A''s W twiddles) became vmcnt(3) -- waiting out this prefetch as well.
   __device__ __forceinline__ static void load(f32x4 (&v)[FWD_PF], const StripSrc& s, int lane) {
     const f32x4* s4 = reinterpret_cast<const f32x4*>(s.src - s.off);
 #pragma unroll
     for (int u = 0; u < FWD_PF; ++u) {
       const int q = lane + 64 * u;
-      v[u] = __builtin_nontemporal_load(s4 + (q < s.nq ? q : s.nq - 1));
+      if (q < s.nq) v[u] = __builtin_nontemporal_load(s4 + q);
     }
   }
   // returns the strip's row-0 pointer in LDS
@@ -286,13 +283,7 @@ __global__ __launch_bounds__(BAND_NT) __attribute__((amdgpu_waves_per_eu(NT2 * K
     __builtin_amdgcn_wave_barrier();
     // 2. the next strip's loads fly while this one is computed
     const uint32_t tn = t + 1;
-    if (F16) {  // issued on every path (past the wave's last strip: every lane re-reads one vector), so the
-                // W product's wait for this strip's twiddles counts these 10 younger loads -- a conditional
-                // block here turned that wait into vmcnt(3), i.e. a wait for the whole prefetch
-      const bool more = tn < t1;
-      if (more) ss = strip_src(tn);
-      Strip<DC>::load(pf, ss, more && !(diag & 1) ? lane : 0);
-    } else if (tn < t1) {
+    if (tn < t1) {
       ss = strip_src(tn);
       if (pre && !(diag & 1)) Strip<DC>::load(pf, ss, lane);
     }
