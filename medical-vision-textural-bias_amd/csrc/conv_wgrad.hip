@@ -517,8 +517,10 @@ struct Zm2Args {
   int mtiles, ctiles;  // m-tiles of 32 (pairs), c-tiles of 16
 };
 
-template <int YB, int WV>  // output rows per block, Wo <= 4 WV
-__global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
+// NW = 8 waves (two per SIMD at one block per CU): m-tile = wave & 1, k-step parity = wave >> 1 of NW / 2
+template <int YB, int WV, int NW>  // output rows per block, Wo <= 4 WV
+__global__ __launch_bounds__(64 * NW) void k_conv3d_wgrad_zm2(Zm2Args a) {
+  constexpr int NT = 64 * NW, P = NW / 2;
   constexpr int NXR = 2 * YB + 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -536,16 +538,16 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   const int m0 = 32 * mt, c0 = 16 * ct;
   const int mv = min(32, a.M - m0), cv = min(16, a.Cc - c0);
   const int z0 = zs * a.zlen, z1 = min(Do, z0 + a.zlen);
-  for (int i = tid; i < 2 * GS + 5 * XS; i += 256) smem[i] = 0.f;
+  for (int i = tid; i < 2 * GS + 5 * XS; i += NT) smem[i] = 0.f;
   const int64_t iplane = (int64_t)Hi * Wi, oplane = (int64_t)Ho * Wo;
   const float* Gb = a.G + ((int64_t)n * a.M + m0) * Do * oplane;
   const float* Xb = a.X + ((int64_t)n * a.Cc + c0) * Di * iplane;
   const int Wi4 = Wi >> 2, Wo4 = Wo >> 2;
-  constexpr int NXL = (16 * NXR * 2 * WV + 255) / 256, NGL = (32 * YB * WV + 255) / 256;
+  constexpr int NXL = (16 * NXR * 2 * WV + NT - 1) / NT, NGL = (32 * YB * WV + NT - 1) / NT;
   int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
 #pragma unroll
   for (int j = 0; j < NXL; ++j) {  // (c, r, q): input row 2 y0 - 1 + r
-    const int i = tid + 256 * j;
+    const int i = tid + NT * j;
     const int q = i % Wi4, t = i / Wi4, r = t % NXR, c = t / NXR;
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < cv && yi >= 0 && yi < Hi;
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {  // (m, yy, q): output row y0 + yy
-    const int i = tid + 256 * j;
+    const int i = tid + NT * j;
     const int q = i % Wo4, t = i / Wo4, yy = t % YB, m = t / YB;
     const bool ok = m < mv && y0 + yy < Ho;
     gg[j] = ok ? (int)(((int64_t)m * Do) * oplane / 4 + ((y0 + yy) * Wo + 4 * q) / 4) : -1;
@@ -644,25 +646,35 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
       float a0, a1, b0[27], b1[27];
       ld(par, a0, b0);
       int k = par;
-      for (; k + 2 < nk; k += 4) {
-        ld(k + 2, a1, b1);
+      for (; k + P < nk; k += 2 * P) {
+        ld(k + P, a1, b1);
         mm(a0, b0);
-        ld(k + 4, a0, b0);
+        ld(k + 2 * P, a0, b0);
         mm(a1, b1);
       }
       if (k < nk) mm(a0, b0);
     }
   }
-  // partner waves (same m-tile, other parity) meet in LDS; waves 0 / 1 add and store
-  __syncthreads();
+  // partner waves (same m-tile, other parities) hand their sums down to parity 0 one parity at a time
+  // through LDS; parity 0 stores
   float* red = smem;  // [2 m-tiles][27][4 rr][64 lanes]
-  if (par == 1) {
 #pragma unroll
-    for (int j = 0; j < 27; ++j)
+  for (int src = P - 1; src >= 1; --src) {
+    __syncthreads();
+    if (par == src) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) red[((mtl * 27 + j) * 4 + rr) * 64 + lane] = acc[j][rr];
+      for (int j = 0; j < 27; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) red[((mtl * 27 + j) * 4 + rr) * 64 + lane] = acc[j][rr];
+    }
+    __syncthreads();
+    if (par == 0) {
+#pragma unroll
+      for (int j = 0; j < 27; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[j][rr] += red[((mtl * 27 + j) * 4 + rr) * 64 + lane];
+    }
   }
-  __syncthreads();
   if (par == 0) {
     const int c = li;
 #pragma unroll
@@ -670,9 +682,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zm2(Zm2Args a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int m = 16 * mtl + lk * 4 + rr;
-        if (m < mv && c < cv)
-          atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j],
-                    acc[j][rr] + red[((mtl * 27 + j) * 4 + rr) * 64 + lane]);
+        if (m < mv && c < cv) atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], acc[j][rr]);
       }
   }
 }
@@ -1245,7 +1255,7 @@ int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do,
   a.mtiles = (M + 31) / 32;
   a.ctiles = (Cc + 15) / 16;
   const int base = N * a.nyb * a.mtiles * a.ctiles;
-  const int per_cu = (int)(163840 / lds) < 2 ? 1 : 2;
+  const int per_cu = 1;  // 8-wave blocks: two waves per SIMD already
   int best = 1 << 30;
   a.zlen = Do;
   for (int zl = Do; zl >= 1; --zl) {
@@ -1263,12 +1273,12 @@ int zm2_setup(Zm2Args& a, size_t& lds, dim3& grid, int N, int M, int Cc, int Do,
 }
 
 int launch_zm2(const Zm2Args& a, size_t lds, dim3 grid, hipStream_t st) {
-  auto kern = a.YB == 2 ? (a.Wo <= 20 ? k_conv3d_wgrad_zm2<2, 5> : k_conv3d_wgrad_zm2<2, 10>)
-                        : (a.Wo <= 20 ? k_conv3d_wgrad_zm2<1, 5> : k_conv3d_wgrad_zm2<1, 10>);
+  auto kern = a.YB == 2 ? (a.Wo <= 20 ? k_conv3d_wgrad_zm2<2, 5, 8> : k_conv3d_wgrad_zm2<2, 10, 8>)
+                        : (a.Wo <= 20 ? k_conv3d_wgrad_zm2<1, 5, 8> : k_conv3d_wgrad_zm2<1, 10, 8>);
   const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
