@@ -703,8 +703,10 @@ struct Zf2Args {
   int mtiles;  // blocks of MT m-tiles
 };
 
-template <int YB, int MT, int WV>  // rows per block, 16-row m-tiles per block, Wo <= 4 WV
-__global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
+// NW = 8 waves (two per SIMD at one block per CU; the loads of twice as many waves in flight)
+template <int YB, int MT, int WV, int NW>  // rows per block, 16-row m-tiles per block, Wo <= 4 WV
+__global__ __launch_bounds__(64 * NW) void k_conv3d_wgrad_zf2(Zf2Args a) {
+  constexpr int NT = 64 * NW;
   constexpr int NXR = 2 * YB + 1;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -721,16 +723,16 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
   const int m0 = 16 * MT * mt, mv = min(16 * MT, a.M - m0);
   const int y0 = yb * YB;
   const int z0 = zs * a.zlen, z1 = min(Do, z0 + a.zlen);
-  for (int i = tid; i < 2 * GS + 5 * XS; i += 256) smem[i] = 0.f;
+  for (int i = tid; i < 2 * GS + 5 * XS; i += NT) smem[i] = 0.f;
   const int64_t iplane = (int64_t)Hi * Wi, oplane = (int64_t)Ho * Wo;
   const float* Gb = a.G + ((int64_t)n * a.M + m0) * Do * oplane;
   const float* Xb = a.X + (int64_t)n * Cc * Di * iplane;
   const int Wi4 = Wi >> 2, Wo4 = Wo >> 2;
-  constexpr int NXL = (5 * NXR * 2 * WV + 255) / 256, NGL = (16 * MT * YB * WV + 255) / 256;
+  constexpr int NXL = (5 * NXR * 2 * WV + NT - 1) / NT, NGL = (16 * MT * YB * WV + NT - 1) / NT;
   int xg[NXL], xl[NXL], gg[NGL], gl[NGL];
 #pragma unroll
   for (int j = 0; j < NXL; ++j) {  // (c, r, q)
-    const int i = tid + 256 * j;
+    const int i = tid + NT * j;
     const int q = i % Wi4, t = i / Wi4, r = t % NXR, c = t / NXR;
     const int yi = 2 * y0 - 1 + r;
     const bool ok = c < Cc && yi >= 0 && yi < Hi;
@@ -739,7 +741,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
   }
 #pragma unroll
   for (int j = 0; j < NGL; ++j) {  // (m, yy, q)
-    const int i = tid + 256 * j;
+    const int i = tid + NT * j;
     const int q = i % Wo4, t = i / Wo4, yy = t % YB, m = t / YB;
     const int y = y0 + yy;
     const bool ok = m < mv && y < Ho;
@@ -808,9 +810,9 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
     const float* ga = gsl + (z & 1) * GS + li * a.MS + lk;
     const float* xp[3] = {xsl + ((2 * z - 1 + 5) % 5) * XS + boff, xsl + ((2 * z) % 5) * XS + boff,
                           xsl + ((2 * z + 1) % 5) * XS + boff};
-    // this wave's k-steps: rows yy = wave, wave + 4, ... (YB = 4: one row; YB < 4: x parts of a row);
+    // this wave's k-steps: rows yy = wave, wave + NW, ... (YB >= NW), else x parts of row wave % YB;
     // the next k-step's operands are read under the current one's MFMAs (2x unrolled, clamped)
-    const int np = YB >= 4 ? 1 : 4 / YB, yy0 = YB >= 4 ? wave : wave % YB, part = YB >= 4 ? 0 : wave / YB;
+    const int np = YB >= NW ? 1 : NW / YB, yy0 = YB >= NW ? wave : wave % YB, part = YB >= NW ? 0 : wave / YB;
     const int kb = (Wo4 * part) / np, ke = (Wo4 * (part + 1)) / np;
     auto ld = [&](int yy, int k, float (&av)[MT], float (&bv)[9]) {
       const int x0 = 4 * (k < ke ? k : ke - 1);
@@ -827,7 +829,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[j], acc[t][j], 0, 0, 0);
     };
-    for (int yy = yy0; yy < YB; yy += 4) {
+    for (int yy = yy0; yy < YB; yy += NW) {
       if (kb >= ke) break;
       float a0[MT], a1[MT], b0[9], b1[9];
       ld(yy, kb, a0, b0);
@@ -841,23 +843,23 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf2(Zf2Args a) {
       if (k < ke) mm(a0, b0);
     }
   }
-  // the four waves' sums meet in LDS, one atomic per entry
+  // the waves' sums meet in LDS, one atomic per entry
   __syncthreads();
-  float* red = smem;  // [MT][9][4 waves][4 rr][64]
+  float* red = smem;  // [MT][9][NW waves][4 rr][64]
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int j = 0; j < 9; ++j)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) red[(((t * 9 + j) * 4 + wave) * 4 + rr) * 64 + lane] = acc[t][j][rr];
+      for (int rr = 0; rr < 4; ++rr) red[(((t * 9 + j) * NW + wave) * 4 + rr) * 64 + lane] = acc[t][j][rr];
   __syncthreads();
-  for (int e = tid; e < MT * 9 * 4 * 64; e += 256) {  // e = ((t, j), rr, lane)
+  for (int e = tid; e < MT * 9 * 4 * 64; e += NT) {  // e = ((t, j), rr, lane)
     const int ln = e & 63, rr = (e >> 6) & 3, tj = e >> 8, t = tj / 9, j = tj - 9 * t;
     const int m = 16 * t + (ln >> 4) * 4 + rr, col = ln & 15;
     if (m >= mv || col >= 3 * Cc) continue;
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) v += red[((tj * 4 + w) * 4 + rr) * 64 + ln];
+    for (int w = 0; w < NW; ++w) v += red[((tj * NW + w) * 4 + rr) * 64 + ln];
     const int c = col / 3, tx = col - 3 * c;
     atomicAdd(&a.dW[((int64_t)(m0 + m) * Cc + c) * 27 + j * 3 + tx], v);  // j = (tz, ty)
   }
@@ -1297,7 +1299,7 @@ int zf2_setup(Zf2Args& a, int& MT, size_t& lds, dim3& grid, int N, int M, int Cc
   a.YB = 0;
   for (int yb : {4, 2, 1}) {
     const int rx = pad_mod32((2 * yb + 1) * a.PX, 8), ms = pad_mod32(yb * Wo, 2);
-    const size_t ring = (size_t)4 * (2 * 16 * MT * ms + 5 * Cc * rx), red = (size_t)4 * MT * 9 * 4 * 4 * 64;
+    const size_t ring = (size_t)4 * (2 * 16 * MT * ms + 5 * Cc * rx), red = (size_t)4 * MT * 9 * 8 * 4 * 64;
     const size_t need = ring > red ? ring : red;
     if (need <= 163840) {
       a.YB = yb; a.RX = rx; a.MS = ms;
@@ -1327,11 +1329,11 @@ int zf2_setup(Zf2Args& a, int& MT, size_t& lds, dim3& grid, int N, int M, int Cc
 
 template <int YB, int MT>
 int launch_zf2_t(const Zf2Args& a, size_t lds, dim3 grid, hipStream_t st) {
-  auto kern = a.Wo <= 40 ? k_conv3d_wgrad_zf2<YB, MT, 10> : k_conv3d_wgrad_zf2<YB, MT, 20>;
+  auto kern = a.Wo <= 40 ? k_conv3d_wgrad_zf2<YB, MT, 10, 8> : k_conv3d_wgrad_zf2<YB, MT, 20, 8>;
   const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   if (attr != hipSuccess) return TB_ERR_HIP;
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 int launch_zf2(const Zf2Args& a, int MT, size_t lds, dim3 grid, hipStream_t st) {
