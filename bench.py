@@ -414,6 +414,15 @@ def main():
             "filter_passes": passes,
             "filter_ms_per_step": round(sum(ms) / stat_steps, 4),
         }
+        if args.config == "c3" and not layer_model and not args.filter_only:
+            from texbias.train import step_conv_flops
+            fl = step_conv_flops(lambda: reference_model(C, 3), (B, C, H, W, D + pad))
+            tfs = fl / (elapsed / args.steps) / 1e12
+            line["unet_compute"] = {"analytic_tflop_per_step": round(fl / 1e12, 4), "tflop_s": round(tfs, 2),
+                                    "peak_f32_matrix_tflop_s": 157.3, "frac": round(tfs / 157.3, 4),
+                                    "note": "per rank: the U-Net's conv layers (fwd + weight grad + input grad except "
+                                            "the network input's), texbias.train.step_conv_flops / measured step time "
+                                            "(the whole step, filter chain included)"}
         if args.config == "c5":
             from texbias.dcgan import step_flops
             fl = step_flops() * B  # per rank and step (analytic: 3x forward per backward pass)

@@ -48,6 +48,35 @@ def reference_model(in_channels: int = 4, out_channels: int = 3) -> UNet:
                 strides=(2, 2, 2, 2), num_res_units=2)
 
 
+def step_conv_flops(model_fn, input_shape) -> int:
+    """Analytic FLOPs of one train step's convolutions (measurement, not used by training): the model built
+    by ``model_fn()`` on the meta device, one forward over ``input_shape`` recording every Conv3d /
+    ConvTranspose3d's multiply-adds (Conv3d: output elements x Cin x k^3; ConvTranspose3d: input elements x
+    Cout x k^3); per layer 2 x MACs for the forward, the weight gradient and -- unless its input is the
+    network input -- the input gradient.  Norms, activations, the loss and Adam are left out (< 1 %)."""
+    import math
+
+    import torch.nn as nn
+    with torch.device("meta"):
+        m = model_fn()
+    total = 0
+
+    def hook(mod, inp, out):
+        nonlocal total
+        k = math.prod(mod.kernel_size)
+        macs = inp[0].numel() * mod.out_channels * k if isinstance(mod, nn.ConvTranspose3d) else \
+            out.numel() * mod.in_channels * k
+        total += 2 * macs * (3 if inp[0].requires_grad else 2)
+
+    hs = [c.register_forward_hook(hook) for c in m.modules() if isinstance(c, (nn.Conv3d, nn.ConvTranspose3d))]
+    try:
+        m(torch.empty(tuple(input_shape), device="meta"))
+    finally:
+        for h in hs:
+            h.remove()
+    return total
+
+
 class TrainStep:
     """model / loss / optimizer of the reference, optionally wrapped in DDP."""
 
