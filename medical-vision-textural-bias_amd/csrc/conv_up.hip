@@ -1154,8 +1154,8 @@ static int mfma_call(const float* x, const float* W, const float* bias, const fl
   if (!x || !W || !y || N < 1 || D < 1 || H < 1 || Wd < 1) return TB_ERR_INVALID_ARG;
   if ((C != 32 && C != 64) || Wd % 4 != 0 || Wd > 64 || (reinterpret_cast<uintptr_t>(x) & 15) != 0)
     return TB_ERR_UNSUPPORTED_SIZE;
-  // 4 waves with 5 chains each (TEXBIAS_CONVMFMA_NT=512: 8 waves, two per role on alternate tiles with
-  // 3 chains -- measured slower here, 245 vs 211 us at 32 -> 32, unlike k_conv3d_fwd16).  (Persistent step
+  // 4 waves with 5 chains each (8 waves, two per role on alternate tiles with 3 chains, measured
+  // slower here, 245 vs 211 us at 32 -> 32, unlike k_conv3d_fwd16).  (Persistent step
   // shares as in k_conv3d_fwd16 measured no gain at 32 -> 32, 186 vs 184 us, and the loop they need cost
   // the 64 -> 64 kernel 107 -> 144 us: not used.)
   constexpr int NTv = 256;  // only the measured best (256 threads) is instantiated

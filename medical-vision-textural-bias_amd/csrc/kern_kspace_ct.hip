@@ -210,9 +210,9 @@ bool kspace_ct_supported(int H) {
   return false;
 }
 
-// the paired kernel when every tile is full and rows stay 16-B aligned.  Tile width (TEXBIAS_KSPACE_T2):
-// 16 columns on 128-thread workgroups by default (4 per CU by LDS: 196 us per C3 launch), 32 on
-// 256 threads (2 per CU: 206 us), or 8 on 64 threads
+// the paired kernel when every tile is full and rows stay 16-B aligned.  Tile width: 16 columns on
+// 128-thread workgroups (4 per CU by LDS: 196 us per C3 launch; measured against 32 columns on 256
+// threads, 2 per CU: 206 us, and 8 on 64 threads)
 static bool use_pair(int ncols) {
   return ncols % ct::kCtTileT2 == 0;
 }
@@ -222,7 +222,7 @@ static int pair_tile() {
 
 int kspace_ct_tile(int ncols) { return use_pair(ncols) ? pair_tile() : ct::kCtTileT; }
 
-// persistent pass B (TEXBIAS_KSPACE_PERSIST=0: the one-tile-per-workgroup grid)
+// persistent pass B (measured against the one-tile-per-workgroup grid)
 static bool use_persist() {
   return true;
 }
@@ -243,7 +243,7 @@ static int kspace_occupancy(K kern, int nt, size_t lds) {
 bool kspace_ct_persistent(int ncols) { return use_pair(ncols) && use_persist() && pair_tile() == 16; }
 
 // the launch's programs all of one mask-op kind -> pass B's unrolled middle phase
-// (TEXBIAS_KSPACE_MASK=0: always the generic one)
+// (else the generic one)
 static int launch_mask_kind(const KspaceArgs& a) {
   if (a.nbc < 1) return ct::MASK_GENERIC;
   const int s0 = a.cofs / a.C, s1 = (a.cofs + a.nbc - 1) / a.C;

@@ -474,10 +474,9 @@ extern "C" int tb_debug_slab_prof_clear() {
 }
 #endif
 
-// threads per workgroup: 768 (3 waves per SIMD) by default; TEXBIAS_CT_NT=512 selects 512 (tuning).
-// TEXBIAS_CT_FUSE (bit 1: forward, bit 2: inverse; default 2) selects the fused DU / RE phase
-// variant (slab_ct.h) at 512 threads for plans with odd R0 and D: it holds two butterflies'
-// inputs across a barrier, which fits the register file only at 2 waves per SIMD.
+// threads per workgroup: 768 (3 waves per SIMD; measured against 512).  The fused DU / RE phase variant
+// (slab_ct.h) is used for the inverse pass only (bit 2): it holds two butterflies' inputs across a
+// barrier, which fits the register file only at 2 waves per SIMD.
 static int ct_nt() {
   return 768;
 }
@@ -492,7 +491,7 @@ bool slab_ct_supported(int W, int D) {
   return false;
 }
 
-// 16-B staged loads when the slabs are contiguous and 16-B aligned (TEXBIAS_SLAB_RAW16=0: off)
+// 16-B staged loads when the slabs are contiguous and 16-B aligned
 static bool raw16_ok(const SlabFwdArgs& a) {
   return a.sw == a.pl.D && a.sh % 4 == 0 && a.sbc % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
          (a.pl.W * a.pl.D) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.S) & 15) == 0;
@@ -543,9 +542,9 @@ bool slab_half_supported(int W, int D) {
   return false;
 }
 
-// TEXBIAS_HALF_CFG / TEXBIAS_HALF_CFG_INV (tuning, passes A / C): 0 = 256 threads with the fused DU / RE
-// phase, 1 = 256 threads unfused, 2 = 512 threads unfused, 3 = 768 threads unfused.  Measured on the
-// gibbs-aug C3 chain (A / C us): 0: 220 / 207, 1: 224 / 211, 2: 184 / 167, 3: 224 / 151 -> A 2, C 3.
+// half-unit configurations (passes A / C): 0 = 256 threads with the fused DU / RE phase, 1 = 256 threads
+// unfused, 2 = 512 threads unfused, 3 = 768 threads unfused.  Measured on the gibbs-aug C3 chain
+// (A / C us): 0: 220 / 207, 1: 224 / 211, 2: 184 / 167, 3: 224 / 151 -> A 2, C 3.
 static int half_cfg() { return 2; }
 static int half_cfg_inv() { return 3; }
 

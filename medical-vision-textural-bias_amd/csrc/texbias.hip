@@ -506,7 +506,7 @@ static bool g_half = [] {
 }();
 static bool use_half(const tb_plan* p) { return g_half && use_ct_slab(p) && p->ct_half; }
 
-// channel-volumes per A -> B -> C chain (TEXBIAS_CHUNK_BC; 0 = all, the default).  Chunks of
+// channel-volumes per A -> B -> C chain (tb_set_chain_chunk; 0 = all, the default).  Chunks of
 // 2..4 channel-volumes keep the spectrum within the Infinity Cache between passes, but measured
 // slower at C3 (0.99 / 0.94 / 0.89 vs 0.85 ms per step: the passes are latency-bound, not
 // HBM-bound, and smaller launches leave more of the chip idle in their tails).
@@ -876,8 +876,7 @@ static int run_generic(const tb_plan* p, const float* x, const int64_t* xs, floa
   return TB_OK;
 }
 
-// Samples per chain of the closed-form route's three launches (TEXBIAS_POINT_CHUNK, 0 = the whole
-// launch group): per-sample chains would let k_point_apply re-read a 142 MB sample from the Infinity
+// Samples per chain of the closed-form route's three launches (0 = the whole launch group): per-sample chains would let k_point_apply re-read a 142 MB sample from the Infinity
 // Cache, but cost more in launches and smaller grids than they saved.
 static int point_chunk(const tb_plan* p, int C) {
   (void)p;
