@@ -167,6 +167,18 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
                         int Hi, int Wi, int stride, int pad, void* stream);
 
 /*
+ * The same weight gradient with a caller-owned workspace (device, `ws_bytes` from
+ * tb_conv3d_wgrad_ws_bytes for the same sizes): the z-marching kernels then write one partial dW tile
+ * per workgroup into `ws` and a reduction kernel sums them in workgroup order (deterministic) -- the
+ * contended float atomics of tb_conv3d_wgrad_f32 cost up to 3/4 of those kernels' time.  `ws` NULL or
+ * too small: tb_conv3d_wgrad_f32.  tb_conv3d_wgrad_ws_bytes returns 0 where no partial path exists.
+ */
+int64_t tb_conv3d_wgrad_ws_bytes(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride,
+                                 int pad);
+int tb_conv3d_wgrad_ws_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo,
+                           int Di, int Hi, int Wi, int stride, int pad, void* ws, size_t ws_bytes, void* stream);
+
+/*
  * The tiling tb_conv3d_wgrad_f32 chooses for these sizes, without launching anything (host only):
  * cfg[0] = SEG (64-column row segments staged per wave, 1..4), cfg[1] = TX (1: 16 input channels x
  * 27 tap accumulators; 3: (channel, tx) columns for <= 5 channels), cfg[2] = YB (output rows per

@@ -307,6 +307,7 @@ struct ZmArgs {
   const float* G;
   const float* X;
   float* dW;
+  float* part;  // non-null: per-workgroup partial tiles [tile][block][16 m][16 c][27] instead of atomics
   int N, M, Cc, D, H, W;       // G and X both [N][.][D][H][W] (stride 1, padding 1)
   int YB, nyb, ZS, zlen;       // rows per block, row blocks, z segments, planes per segment
   int MS, RX, PX, W4;          // LDS pitches (floats): G channel, X channel, X row; k-step row length
@@ -491,12 +492,47 @@ __global__ __launch_bounds__(64 * NW) void k_conv3d_wgrad_zm(ZmArgs a) {
       for (int rr = 0; rr < 4; ++rr) red[((j * 2 + wave) * 4 + rr) * 64 + lane] = acc[j][rr];
   }
   __syncthreads();
+  float* pt = a.part ? a.part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (16 * 16 * 27) : nullptr;
   for (int e = tid; e < 27 * 4 * 64; e += NT) {  // e = (j, rr, lane)
     const int ln = e & 63, rr = (e >> 6) & 3, j = e >> 8;
     const int m = (ln >> 4) * 4 + rr, c = ln & 15;
-    if (m >= mv || c >= cv) continue;
     const float v = red[((j * 2 + 0) * 4 + rr) * 64 + ln] + red[((j * 2 + 1) * 4 + rr) * 64 + ln];
-    atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], v);
+    if (pt) {
+      pt[(m * 16 + c) * 27 + j] = v;  // the whole tile (zeros past mv, cv: those G / X rows were staged as 0)
+    } else if (m < mv && c < cv) {
+      atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], v);
+    }
+  }
+}
+
+// dW from per-workgroup partial tiles part[tile][nblk][TM m][TC c][27], summed in block order: 64 entries x
+// 16 block groups per 1024-thread workgroup (each thread ~nblk / 16 independent loads in flight), the groups
+// met in LDS.  grid (ceil(TM TC 27 / 64), tiles); tile -> (mt, ct) = (tile / ctiles, tile % ctiles).
+__global__ __launch_bounds__(1024) void k_wgrad_reduce(const float* __restrict__ part, float* __restrict__ dW, int nblk,
+                                                       int TM, int TC, int ctiles, int M, int Cc) {
+  __shared__ float red[16][64];
+  const int tid = (int)threadIdx.x, el = tid & 63, bg = tid >> 6;
+  const int TE = TM * TC * 27, tile = (int)blockIdx.y;
+  const int e = (int)blockIdx.x * 64 + el;
+  const float* src = part + (int64_t)tile * nblk * TE + (e < TE ? e : 0);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = bg;
+  for (; b + 48 < nblk; b += 64) {
+    s0 += src[(int64_t)b * TE];
+    s1 += src[(int64_t)(b + 16) * TE];
+    s2 += src[(int64_t)(b + 32) * TE];
+    s3 += src[(int64_t)(b + 48) * TE];
+  }
+  for (; b < nblk; b += 16) s0 += src[(int64_t)b * TE];
+  red[bg][el] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (bg == 0 && e < TE) {
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) v += red[g][el];
+    const int mt = tile / ctiles, ct = tile - mt * ctiles;
+    const int m = e / (TC * 27), r = e - m * (TC * 27), c = r / 27, j = r - c * 27;
+    if (mt * TM + m < M && ct * TC + c < Cc) dW[((int64_t)(mt * TM + m) * Cc + ct * TC + c) * 27 + j] = v;
   }
 }
 
@@ -1488,6 +1524,46 @@ int tb_conv3d_wgrad_f32(const float* G, const float* X, float* dW, int N, int M,
   }
   if (stride == 1) return TX == 1 ? launch_seg<1, 1>(a, seg, by, lds, st) : launch_seg<1, 3>(a, seg, by, lds, st);
   return TX == 1 ? launch_seg<2, 1>(a, seg, by, lds, st) : launch_seg<2, 3>(a, seg, by, lds, st);
+}
+
+static int wgrad_ncu() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
+    return c;
+  }();
+  return n;
+}
+
+int64_t tb_conv3d_wgrad_ws_bytes(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride,
+                                 int pad) {
+  if (pad != 1 || N < 1 || !use_zm(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, nullptr, nullptr)) return 0;
+  ZmArgs z{};
+  size_t lds = 0;
+  dim3 grid;
+  if (zm_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, wgrad_ncu()) != TB_OK) return 0;
+  return (int64_t)grid.x * grid.y * 16 * 16 * 27 * 4;
+}
+
+int tb_conv3d_wgrad_ws_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo,
+                           int Di, int Hi, int Wi, int stride, int pad, void* ws, size_t ws_bytes, void* stream) {
+  if (!G || !X || !dW) return TB_ERR_INVALID_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (ws && pad == 1 && N >= 1 && use_zm(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {
+    ZmArgs z{};
+    size_t lds = 0;
+    dim3 grid;
+    if (zm_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, wgrad_ncu()) == TB_OK &&
+        ws_bytes >= (size_t)grid.x * grid.y * 16 * 16 * 27 * 4 && (reinterpret_cast<uintptr_t>(ws) & 3) == 0) {
+      z.G = G; z.X = X; z.dW = dW; z.part = static_cast<float*>(ws);
+      const int rc = launch_zm(z, lds, grid, st);
+      if (rc != TB_OK) return rc;
+      hipLaunchKernelGGL(k_wgrad_reduce, dim3((16 * 16 * 27 + 63) / 64, grid.y), dim3(1024), 0, st,
+                         static_cast<const float*>(ws), dW, (int)grid.x, 16, 16, z.ctiles, M, Cc);
+      return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+    }
+  }
+  return tb_conv3d_wgrad_f32(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad, stream);
 }
 
 // The tiling tb_conv3d_wgrad_f32 would choose (no launch): cfg = {SEG, TX, YB, chunks, LDS bytes}.

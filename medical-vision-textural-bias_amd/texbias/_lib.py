@@ -42,6 +42,8 @@ def _proto(L):
         "tb_kspace_logabs_sum_f32": (I, [P, P, P, P, SZ, I, I, P, P, P]),
         "tb_conv3d_wgrad_f32": (I, [P, P, P] + [I] * 11 + [P]),
         "tb_conv3d_wgrad_config": (I, [I] * 11 + [P]),
+        "tb_conv3d_wgrad_ws_bytes": (I64, [I] * 11),
+        "tb_conv3d_wgrad_ws_f32": (I, [P, P, P] + [I] * 11 + [P, SZ, P]),
         "tb_instnorm_prelu_workspace_bytes": (SZ, [I64]),
         "tb_instnorm_prelu_fwd_f32": (I, [P, P, P, P, P, I64, I64, F, P, SZ, P]),
         "tb_instnorm_prelu_bwd_f32": (I, [P, P, P, P, P, P, P, I64, I64, P, SZ, P]),

@@ -33,8 +33,15 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+@functools.lru_cache(maxsize=256)
+def _wgrad_ws_bytes(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad) -> int:
+    return int(lib().tb_conv3d_wgrad_ws_bytes(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad))
+
+
 def wgrad(G: torch.Tensor, X: torch.Tensor, w_shape, stride: int, pad: int) -> torch.Tensor:
-    """dW[m][c][k^3] = corr(G, X) -- see tb_conv3d_wgrad_f32 (include/texbias.h)."""
+    """dW[m][c][k^3] = corr(G, X) -- see tb_conv3d_wgrad_f32 / tb_conv3d_wgrad_ws_f32 (include/texbias.h): with a
+    workspace from the caching allocator the z-marching kernels write per-workgroup partial tiles that one
+    reduction sums in order, instead of contended float atomics."""
     G = G.contiguous()
     X = X.contiguous()
     N, M = G.shape[:2]
@@ -42,9 +49,12 @@ def wgrad(G: torch.Tensor, X: torch.Tensor, w_shape, stride: int, pad: int) -> t
     dW = torch.empty((M, Cc, 3, 3, 3), dtype=torch.float32, device=G.device)
     Do, Ho, Wo = G.shape[2:]
     Di, Hi, Wi = X.shape[2:]
+    nb = _wgrad_ws_bytes(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad)
+    ws = torch.empty(max(nb, 4), dtype=torch.uint8, device=G.device) if nb > 0 else None
     with torch.cuda.device(G.device):
-        check(lib().tb_conv3d_wgrad_f32(G.data_ptr(), X.data_ptr(), dW.data_ptr(), N, M, Cc, Do, Ho, Wo, Di, Hi, Wi,
-                                        stride, pad, _stream(G)), "tb_conv3d_wgrad_f32")
+        check(lib().tb_conv3d_wgrad_ws_f32(G.data_ptr(), X.data_ptr(), dW.data_ptr(), N, M, Cc, Do, Ho, Wo, Di, Hi, Wi,
+                                           stride, pad, ws.data_ptr() if ws is not None else None, nb,
+                                           _stream(G)), "tb_conv3d_wgrad_ws_f32")
     return dW.view(w_shape)
 
 

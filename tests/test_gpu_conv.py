@@ -141,3 +141,37 @@ def test_small_conv_direct(conv, cin, cout, shape):
     torch.testing.assert_close(gxo, gxr, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gbo, gbr, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gwo, gwr, rtol=1e-4, atol=1e-3 * gwr.abs().max().item())
+
+
+@pytest.mark.parametrize("M,Cc,shape", [(16, 16, (2, 12, 10, 40)), (32, 32, (1, 9, 13, 20)), (24, 40, (1, 7, 6, 16)),
+                                        (64, 64, (2, 5, 7, 12)), (16, 16, (2, 20, 24, 80))])
+def test_wgrad_partial_tiles_match_atomics(conv, M, Cc, shape):
+    """tb_conv3d_wgrad_ws_f32 (per-workgroup partial tiles + an ordered reduction) against
+    tb_conv3d_wgrad_f32 (float atomics) on the z-marching shapes: the same sums in another order
+    (max |d| <= 1e-5 max |dW|), bitwise repeatable, and a too-small workspace falls back to the atomics."""
+    from texbias._lib import lib
+    torch.manual_seed(5)
+    N = shape[0]
+    G = torch.randn((N, M) + shape[1:], device="cuda")
+    X = torch.randn((N, Cc) + shape[1:], device="cuda")
+    dims = (N, M, Cc) + shape[1:] + shape[1:] + (1, 1)
+    nb = int(lib().tb_conv3d_wgrad_ws_bytes(*dims))
+    assert nb > 0
+    st = torch.cuda.current_stream().cuda_stream
+    ref = torch.empty((M, Cc, 27), device="cuda")
+    assert lib().tb_conv3d_wgrad_f32(G.data_ptr(), X.data_ptr(), ref.data_ptr(), *dims, st) == 0
+    outs = []
+    for _ in range(2):
+        ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        out = torch.empty_like(ref)
+        assert lib().tb_conv3d_wgrad_ws_f32(G.data_ptr(), X.data_ptr(), out.data_ptr(), *dims, ws.data_ptr(), nb, st) == 0
+        outs.append(out)
+    small = torch.empty_like(ref)
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    assert lib().tb_conv3d_wgrad_ws_f32(G.data_ptr(), X.data_ptr(), small.data_ptr(), *dims, ws.data_ptr(), nb - 4,
+                                        st) == 0
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    assert (outs[0] - ref).abs().max().item() <= 1e-5 * scale
+    assert torch.equal(outs[0], outs[1])
+    assert (small - ref).abs().max().item() <= 1e-5 * scale
