@@ -547,6 +547,7 @@ struct Zm2Args {
   const float* G;
   const float* X;
   float* dW;
+  float* part;  // non-null: per-workgroup partial tiles (k_wgrad_reduce) instead of atomics
   int N, M, Cc, Do, Ho, Wo, Di, Hi, Wi;
   int ZS, zlen, YB, nyb;
   int MS, RX, PX;
@@ -713,12 +714,14 @@ __global__ __launch_bounds__(64 * NW) void k_conv3d_wgrad_zm2(Zm2Args a) {
   }
   if (par == 0) {
     const int c = li;
+    float* pt = a.part ? a.part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (32 * 16 * 27) : nullptr;
 #pragma unroll
     for (int j = 0; j < 27; ++j)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int m = 16 * mtl + lk * 4 + rr;
-        if (m < mv && c < cv) atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], acc[j][rr]);
+        if (pt) pt[(m * 16 + c) * 27 + j] = acc[j][rr];  // the whole [32][16][27] tile (zeros past mv, cv)
+        else if (m < mv && c < cv) atomicAdd(&a.dW[((int64_t)(m0 + m) * a.Cc + (c0 + c)) * 27 + j], acc[j][rr]);
       }
   }
 }
@@ -733,6 +736,7 @@ struct Zf2Args {
   const float* G;
   const float* X;
   float* dW;
+  float* part;  // non-null: per-workgroup partial tiles (k_wgrad_reduce) instead of atomics
   int N, M, Cc, Do, Ho, Wo, Di, Hi, Wi;
   int YB, nyb, ZS, zlen;
   int MS, RX, PX;
@@ -889,15 +893,17 @@ __global__ __launch_bounds__(64 * NW) void k_conv3d_wgrad_zf2(Zf2Args a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) red[(((t * 9 + j) * NW + wave) * 4 + rr) * 64 + lane] = acc[t][j][rr];
   __syncthreads();
+  float* pt = a.part ? a.part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (16 * MT * Cc * 27) : nullptr;
   for (int e = tid; e < MT * 9 * 4 * 64; e += NT) {  // e = ((t, j), rr, lane)
     const int ln = e & 63, rr = (e >> 6) & 3, tj = e >> 8, t = tj / 9, j = tj - 9 * t;
     const int m = 16 * t + (ln >> 4) * 4 + rr, col = ln & 15;
-    if (m >= mv || col >= 3 * Cc) continue;
+    if ((!pt && m >= mv) || col >= 3 * Cc) continue;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[((tj * NW + w) * 4 + rr) * 64 + ln];
     const int c = col / 3, tx = col - 3 * c;
-    atomicAdd(&a.dW[((int64_t)(m0 + m) * Cc + c) * 27 + j * 3 + tx], v);  // j = (tz, ty)
+    if (pt) pt[(m * Cc + c) * 27 + j * 3 + tx] = v;  // the whole [16 MT][Cc][27] tile (zeros past mv)
+    else atomicAdd(&a.dW[((int64_t)(m0 + m) * Cc + c) * 27 + j * 3 + tx], v);  // j = (tz, ty)
   }
 }
 
@@ -912,6 +918,7 @@ struct Zf1Args {
   const float* G;
   const float* X;
   float* dW;
+  float* part;  // non-null: per-workgroup partial tiles (k_wgrad_reduce) instead of atomics
   int N, M, Cc, D, H, W;
   int YB, nyb, ZS, zlen;
   int GR, GM, GS;  // G: row pitch, channel pitch, slot pitch (floats)
@@ -1066,6 +1073,7 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf1(Zf1Args a) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) red[((t * 4 + wave) * 4 + rr) * 64 + lane] = acc[0][t][rr] + acc[1][t][rr];
   __syncthreads();
+  float* pt = a.part ? a.part + (int64_t)blockIdx.x * (M * Cc * 27) : nullptr;
   for (int e = tid; e < 2 * 4 * 64; e += 256) {  // e = (t, rr, lane)
     const int ln = e & 63, rr = (e >> 6) & 3, t = e >> 8;
     const int r = 16 * t + 4 * (ln >> 4) + rr, col = ln & 15;
@@ -1074,7 +1082,8 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad_zf1(Zf1Args a) {
     const int tz = (r / 3) % 3, ty = r % 3, tx = col - 3 * c;
     const float v = red[((t * 4 + 0) * 4 + rr) * 64 + ln] + red[((t * 4 + 1) * 4 + rr) * 64 + ln] +
                     red[((t * 4 + 2) * 4 + rr) * 64 + ln] + red[((t * 4 + 3) * 4 + rr) * 64 + ln];
-    atomicAdd(&a.dW[((int64_t)m * Cc + c) * 27 + tz * 9 + ty * 3 + tx], v);
+    if (pt) pt[(m * Cc + c) * 27 + tz * 9 + ty * 3 + tx] = v;  // every (m < M, c < Cc) entry once
+    else atomicAdd(&a.dW[((int64_t)m * Cc + c) * 27 + tz * 9 + ty * 3 + tx], v);
   }
 }
 
@@ -1535,35 +1544,66 @@ static int wgrad_ncu() {
   return n;
 }
 
-int64_t tb_conv3d_wgrad_ws_bytes(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride,
-                                 int pad) {
-  if (pad != 1 || N < 1 || !use_zm(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, nullptr, nullptr)) return 0;
-  ZmArgs z{};
+// The z-marching route tb_conv3d_wgrad_f32 takes for these sizes, set up for partial tiles: the partial
+// tile of each workgroup is TM x TC x 27 floats (k_wgrad_reduce), `blocks` workgroups per tile.
+struct ZRoute {
+  int kind = 0;  // 0: none (the general kernel, atomics), 1 zm, 2 zm2, 3 zf1, 4 zf2
+  ZmArgs zm{};
+  Zm2Args zm2{};
+  Zf1Args zf1{};
+  Zf2Args zf2{};
+  int MT = 1;
   size_t lds = 0;
   dim3 grid;
-  if (zm_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, wgrad_ncu()) != TB_OK) return 0;
-  return (int64_t)grid.x * grid.y * 16 * 16 * 27 * 4;
+  int TM = 0, TC = 0, ctiles = 1;
+  size_t bytes() const { return kind ? (size_t)grid.x * grid.y * TM * TC * 27 * 4 : 0; }
+};
+
+static ZRoute zroute(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride, int pad,
+                     const void* G, const void* X) {
+  ZRoute r;
+  if (pad != 1 || N < 1) return r;
+  const int ncu = wgrad_ncu();
+  if (use_zm(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X) &&
+      zm_setup(r.zm, r.lds, r.grid, N, M, Cc, Do, Ho, Wo, ncu) == TB_OK) {
+    r.kind = 1, r.TM = 16, r.TC = 16, r.ctiles = r.zm.ctiles;
+  } else if (use_zm2(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X) &&
+             zm2_setup(r.zm2, r.lds, r.grid, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, ncu) == TB_OK) {
+    r.kind = 2, r.TM = 32, r.TC = 16, r.ctiles = r.zm2.ctiles;
+  } else if (use_zf1(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X) &&
+             zf1_setup(r.zf1, r.lds, r.grid, N, M, Cc, Do, Ho, Wo, ncu) == TB_OK) {
+    r.kind = 3, r.TM = M, r.TC = Cc, r.ctiles = 1;
+  } else if (use_zf2(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X) &&
+             zf2_setup(r.zf2, r.MT, r.lds, r.grid, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, ncu) == TB_OK) {
+    r.kind = 4, r.TM = 16 * r.MT, r.TC = Cc, r.ctiles = 1;
+  }
+  return r;
+}
+
+int64_t tb_conv3d_wgrad_ws_bytes(int N, int M, int Cc, int Do, int Ho, int Wo, int Di, int Hi, int Wi, int stride,
+                                 int pad) {
+  return (int64_t)zroute(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad, nullptr, nullptr).bytes();
 }
 
 int tb_conv3d_wgrad_ws_f32(const float* G, const float* X, float* dW, int N, int M, int Cc, int Do, int Ho, int Wo,
                            int Di, int Hi, int Wi, int stride, int pad, void* ws, size_t ws_bytes, void* stream) {
   if (!G || !X || !dW) return TB_ERR_INVALID_ARG;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (ws && pad == 1 && N >= 1 && use_zm(M, Cc, stride, Do, Ho, Wo, Di, Hi, Wi, G, X)) {
-    ZmArgs z{};
-    size_t lds = 0;
-    dim3 grid;
-    if (zm_setup(z, lds, grid, N, M, Cc, Do, Ho, Wo, wgrad_ncu()) == TB_OK &&
-        ws_bytes >= (size_t)grid.x * grid.y * 16 * 16 * 27 * 4 && (reinterpret_cast<uintptr_t>(ws) & 3) == 0) {
-      z.G = G; z.X = X; z.dW = dW; z.part = static_cast<float*>(ws);
-      const int rc = launch_zm(z, lds, grid, st);
-      if (rc != TB_OK) return rc;
-      hipLaunchKernelGGL(k_wgrad_reduce, dim3((16 * 16 * 27 + 63) / 64, grid.y), dim3(1024), 0, st,
-                         static_cast<const float*>(ws), dW, (int)grid.x, 16, 16, z.ctiles, M, Cc);
-      return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
-    }
+  ZRoute r = zroute(N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad, G, X);
+  if (!ws || !r.kind || ws_bytes < r.bytes() || (reinterpret_cast<uintptr_t>(ws) & 3) != 0)
+    return tb_conv3d_wgrad_f32(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad, stream);
+  float* part = static_cast<float*>(ws);
+  int rc = TB_OK;
+  switch (r.kind) {
+    case 1: r.zm.G = G, r.zm.X = X, r.zm.dW = dW, r.zm.part = part; rc = launch_zm(r.zm, r.lds, r.grid, st); break;
+    case 2: r.zm2.G = G, r.zm2.X = X, r.zm2.dW = dW, r.zm2.part = part; rc = launch_zm2(r.zm2, r.lds, r.grid, st); break;
+    case 3: r.zf1.G = G, r.zf1.X = X, r.zf1.dW = dW, r.zf1.part = part; rc = launch_zf1(r.zf1, r.lds, r.grid, st); break;
+    default: r.zf2.G = G, r.zf2.X = X, r.zf2.dW = dW, r.zf2.part = part; rc = launch_zf2(r.zf2, r.MT, r.lds, r.grid, st); break;
   }
-  return tb_conv3d_wgrad_f32(G, X, dW, N, M, Cc, Do, Ho, Wo, Di, Hi, Wi, stride, pad, stream);
+  if (rc != TB_OK) return rc;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((r.TM * r.TC * 27 + 63) / 64, r.grid.y), dim3(1024), 0, st,
+                     static_cast<const float*>(part), dW, (int)r.grid.x, r.TM, r.TC, r.ctiles, M, Cc);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 
 // The tiling tb_conv3d_wgrad_f32 would choose (no launch): cfg = {SEG, TX, YB, chunks, LDS bytes}.

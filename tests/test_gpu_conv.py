@@ -143,18 +143,21 @@ def test_small_conv_direct(conv, cin, cout, shape):
     torch.testing.assert_close(gwo, gwr, rtol=1e-4, atol=1e-3 * gwr.abs().max().item())
 
 
-@pytest.mark.parametrize("M,Cc,shape", [(16, 16, (2, 12, 10, 40)), (32, 32, (1, 9, 13, 20)), (24, 40, (1, 7, 6, 16)),
-                                        (64, 64, (2, 5, 7, 12)), (16, 16, (2, 20, 24, 80))])
-def test_wgrad_partial_tiles_match_atomics(conv, M, Cc, shape):
+@pytest.mark.parametrize("M,Cc,N,gsp,xsp,stride", [
+    (16, 16, 2, (12, 10, 40), (12, 10, 40), 1), (32, 32, 1, (9, 13, 20), (9, 13, 20), 1),
+    (24, 40, 1, (7, 6, 16), (7, 6, 16), 1), (64, 64, 2, (5, 7, 12), (5, 7, 12), 1), (16, 16, 2, (20, 24, 80), (20, 24, 80), 1),
+    (32, 16, 2, (6, 8, 12), (12, 16, 24), 2), (64, 32, 1, (5, 7, 20), (10, 14, 40), 2),       # k_conv3d_wgrad_zm2
+    (3, 3, 2, (10, 12, 40), (10, 12, 40), 1), (2, 5, 1, (7, 9, 16), (7, 9, 16), 1),          # k_conv3d_wgrad_zf1
+    (32, 4, 2, (6, 8, 12), (12, 16, 24), 2), (16, 3, 1, (5, 6, 20), (10, 12, 40), 2)])        # k_conv3d_wgrad_zf2
+def test_wgrad_partial_tiles_match_atomics(conv, M, Cc, N, gsp, xsp, stride):
     """tb_conv3d_wgrad_ws_f32 (per-workgroup partial tiles + an ordered reduction) against
-    tb_conv3d_wgrad_f32 (float atomics) on the z-marching shapes: the same sums in another order
+    tb_conv3d_wgrad_f32 (float atomics) on every z-marching route: the same sums in another order
     (max |d| <= 1e-5 max |dW|), bitwise repeatable, and a too-small workspace falls back to the atomics."""
     from texbias._lib import lib
     torch.manual_seed(5)
-    N = shape[0]
-    G = torch.randn((N, M) + shape[1:], device="cuda")
-    X = torch.randn((N, Cc) + shape[1:], device="cuda")
-    dims = (N, M, Cc) + shape[1:] + shape[1:] + (1, 1)
+    G = torch.randn((N, M) + gsp, device="cuda")
+    X = torch.randn((N, Cc) + xsp, device="cuda")
+    dims = (N, M, Cc) + gsp + xsp + (stride, 1)
     nb = int(lib().tb_conv3d_wgrad_ws_bytes(*dims))
     assert nb > 0
     st = torch.cuda.current_stream().cuda_stream
