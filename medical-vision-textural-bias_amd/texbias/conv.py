@@ -110,6 +110,16 @@ def weight_grad(gy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int,
     return gw
 
 
+# reduction length (positions) from which the z-marching weight gradients (partial tiles, no atomics) take a
+# layer whatever its channel counts -- measured: 1 gives C3 156.7 vols/s but the 128 x 128 x 64 crop 516 (its
+# deep layers are better on CK), 0 (off) 155.4 / 551, 20000 156.5 / 551
+ZMARCH_MIN_POS = 20000
+
+
+def pos_of(x: torch.Tensor, out_spatial, transposed: bool) -> int:
+    return x.shape[0] * math.prod(out_spatial if not transposed else x.shape[2:])
+
+
 def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, padding, transposed: bool,
                        output_padding=(0, 0, 0)) -> bool:
     if not custom_backward_applies(x, w):
@@ -117,14 +127,21 @@ def fast_wgrad_applies(x: torch.Tensor, w: torch.Tensor, out_spatial, stride, pa
     if tuple(w.shape[2:]) != (3, 3, 3) or len(set(stride)) != 1 or stride[0] not in (1, 2) or padding[0] != 1 or \
             len(set(padding)) != 1:
         return False
+    s = stride[0]
+    if transposed:  # G = x [N, Cin, ...], X = grad of the output [N, Cout, (n - 1) s + 1 + output_padding]
+        g_shape = tuple(x.shape)
+        x_shape = (x.shape[0], w.shape[1]) + tuple((n - 1) * s + 1 + op for n, op in zip(x.shape[2:], output_padding))
+    else:
+        g_shape, x_shape = (x.shape[0], w.shape[0]) + tuple(out_spatial), tuple(x.shape)
+    # the z-marching kernels (partial tiles, no atomics) take any reduction length; the general split-K
+    # kernel only long ones
+    if ZMARCH_MIN_POS and pos_of(x, out_spatial, transposed) >= ZMARCH_MIN_POS and \
+            _wgrad_ws_bytes(*g_shape[:2], x_shape[1], *g_shape[2:], *x_shape[2:], s, 1) > 0:
+        return True
     pos = x.shape[0] * math.prod(out_spatial if not transposed else x.shape[2:])
     if pos < MIN_K_PER_OUTPUT * w.shape[0] * w.shape[1] * 27 // 16:
         return False
-    s = stride[0]
-    if transposed:  # G = x [N, Cin, ...], X = grad of the output [N, Cout, (n - 1) s + 1 + output_padding]
-        hi = tuple((n - 1) * s + 1 + op for n, op in zip(x.shape[2:], output_padding))
-        return _wgrad_tiles(tuple(x.shape), (x.shape[0], w.shape[1]) + hi, s)
-    return _wgrad_tiles((x.shape[0], w.shape[0]) + tuple(out_spatial), tuple(x.shape), s)
+    return _wgrad_tiles(g_shape, x_shape, s)
 
 
 GEMM = os.environ.get("TEXBIAS_CONVGEMM", "1") != "0"
