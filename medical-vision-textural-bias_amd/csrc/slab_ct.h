@@ -583,9 +583,11 @@ TB_HD void c_twiddle_half(const v2* lds, v2* r, int e, int it) {
   for (int q = 0; q < P::Q1; ++q) r[q] = cmulc(r[q], te[blk + P::Q0 * q]);
 }
 
-// Slab shapes (W, D) with a compile-time plan in the device library
-#define TB_CT_SLAB_SHAPES(X) X(240, 155) X(128, 128) X(128, 64)
-// ... of which these run as half units (split spectrum; W/2 two-stage, half slab <= 80 KB of LDS)
+// Slab shapes (W, D) whose whole-slab passes have a compile-time plan in the device library
+#define TB_CT_SLAB_SHAPES(X) X(128, 128) X(128, 64)
+// Slab shapes that run as half units (split spectrum; W/2 two-stage, half slab <= 80 KB of LDS).  Their
+// whole-slab compiled kernels were dropped in round 6 (a 150 KB slab per CU spilled 104-400 B/lane and ran
+// 1.3x slower than the half units): with half units off they take the run-time-planned passes.
 #define TB_CT_HALF_SHAPES(X) X(240, 155)
 
 }  // namespace ct

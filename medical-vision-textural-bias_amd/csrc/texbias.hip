@@ -355,9 +355,10 @@ int tb_plan_create(int H, int W, int D, tb_plan** out) {
   // compile-time slab plan: same shape and therefore the same radix order as the runtime plan
   p->ct_slab = !p->generic && tb::slab_ct_supported(W, D);
   p->ct_tile = !p->generic && tb::kspace_ct_supported(H);
-  p->ct_half = p->ct_slab && tb::slab_half_supported(W, D) && tb::kspace_half_supported(H, W, D);
+  p->ct_half = !p->generic && tb::slab_half_supported(W, D) && tb::kspace_half_supported(H, W, D);
   const SlabGeo sg = slab_geo(W, D);
   if ((size_t)sg.total_cf * 8 > (size_t)p->lds_max) p->generic = true;  // slab above the LDS: fallback too
+  if (p->generic) p->ct_slab = p->ct_half = false;
   // device tables: tw[H], tw[W], tw[D] (cf) + rev_d[D], irev_h[H], irev_w[W] (int)
   const size_t ncf = (size_t)H + W + D, nint = (size_t)D + H + W;
   const size_t bytes = ncf * sizeof(cf) + nint * sizeof(int);
@@ -504,7 +505,7 @@ static bool g_half = [] {
   const char* e = std::getenv("TEXBIAS_HALF");
   return !(e && e[0] == '0');
 }();
-static bool use_half(const tb_plan* p) { return g_half && use_ct_slab(p) && p->ct_half; }
+static bool use_half(const tb_plan* p) { return g_half && g_compiled_plans && p->ct_half; }
 
 // channel-volumes per A -> B -> C chain (tb_set_chain_chunk; 0 = all, the default).  Chunks of
 // 2..4 channel-volumes keep the spectrum within the Infinity Cache between passes, but measured

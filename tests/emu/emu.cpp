@@ -132,7 +132,7 @@ void ct_tile_run(int H, const tb_plan_dev& pl, v2* lds, v2* S, int bc, int tile,
 }
 
 // the device library's shapes plus small test shapes (odd/even D, composite and prime radices)
-#define TB_EMU_CT_SHAPES(X) TB_CT_SLAB_SHAPES(X) X(24, 35) X(20, 28)
+#define TB_EMU_CT_SHAPES(X) TB_CT_SLAB_SHAPES(X) X(240, 155) X(24, 35) X(20, 28)  // (240, 155): host-only since round 6
 
 bool ct_has(int W, int D) {
 #define TB_X(w, d) if (W == w && D == d) return true;

@@ -4,7 +4,7 @@ Fourier.shift_fourier / inv_shift_fourier (filters_and_operators.py:594-632) for
 programs that the band / closed-form / wrap routes do not take (RandGibbsNoised augmentation, the
 device-alpha GibbsNoiseLayer, high-pass disks, mixed programs).
 
-Tolerances: half units vs the whole-slab compiled passes (tb_set_half_units(0)) max|d| / max|y| <= 2e-6;
+Tolerances: half units vs the whole-slab run-time-planned passes (tb_set_half_units(0)) max|d| / max|y| <= 2e-6;
 vs the numpy oracle <= 1e-5 (north_star); zero padding exact; per-sample min/max keys bit-exact
 against the output.
 """
