@@ -347,8 +347,9 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
  * contiguous C S), the ResidualUnit's sum fused into the forward store (y = prelu(norm(x)) + res; res
  * may be NULL), and in the backward the preceding convolution's bias gradient dbias[c] = sum over n and
  * voxels of dx, taken in float64 from the backward statistics as -rstd mean(g z) sum(z) (the exact value
- * is zero: the norm removes a bias; NULL: not computed), and the PReLU weight gradient dw (NULL: not
- * computed).  No accumulator memsets and no float atomics: every block stores partial sums, reduced in
+ * is zero: the norm removes a bias; NULL: not computed), dysum[c] = sum over n and voxels of dy (the
+ * bias gradient of a residual convolution summed into the same output, out of the same sweep; NULL: not
+ * computed), and the PReLU weight gradient dw (NULL: not computed).  No accumulator memsets and no float atomics: every block stores partial sums, reduced in
  * block order (forward: by every apply block; backward: one block per instance) -- results are
  * deterministic; two launches forward, three backward.  `counters`: DEVICE
  * uint32[tb_adn_counters(N, C)], zero before the first call, left zero by every call (one set per
@@ -360,8 +361,9 @@ int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const flo
                    float* rstd, const float* prelu_w, int64_t N, int64_t C, int64_t S, float eps, void* ws,
                    size_t ws_bytes, uint32_t* counters, void* stream);
 int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, float* dx, int64_t dxsn,
-                   const float* mean, const float* rstd, const float* prelu_w, float* dw, float* dbias, int64_t N,
-                   int64_t C, int64_t S, void* ws, size_t ws_bytes, uint32_t* counters, void* stream);
+                   const float* mean, const float* rstd, const float* prelu_w, float* dw, float* dbias,
+                   float* dysum, int64_t N, int64_t C, int64_t S, void* ws, size_t ws_bytes, uint32_t* counters,
+                   void* stream);
 
 /*
  * GPU-side BraTS preprocessing of B resident raw volumes img [B][C][H0][W0][D0] and

@@ -14,6 +14,8 @@
 // Statistics: biased variance, rstd = 1/sqrt(var + eps) (torch.nn.functional.instance_norm).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "texbias.h"
 
 namespace {
@@ -61,6 +63,14 @@ __device__ __forceinline__ Chunk chunk_of(int64_t S) {
   return Chunk{nc * S, b, e};
 }
 
+// Statistics sweeps load their chunk with every index clamped to the chunk's last float4, so that all
+// VPT loads are issued before the first use, and zero the out-of-range lanes afterwards with a select.
+// (`in ? p[i] : 0` compiled to a branch per load with its own s_waitcnt: one load in flight per wave,
+// ~4 TB/s on the C3 statistics sweeps against 6 TB/s for the apply sweeps.)
+__device__ __forceinline__ float4 zero_unless(bool in, float4 v) {
+  return in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __device__ __forceinline__ void stats_of(double s1, double s2, int64_t S, float eps, float& mean, float& rstd) {
   const double m = s1 / (double)S;
   double var = s2 / (double)S - m * m;
@@ -86,10 +96,11 @@ __global__ __launch_bounds__(NT) void k_in_stats(const float* __restrict__ x, do
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       const int i = threadIdx.x + k * NT;
-      v[k] = i < n4 ? p[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k] = p[i < n4 ? i : n4 - 1];
     }
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
+      v[k] = zero_unless((int)threadIdx.x + k * NT < n4, v[k]);
       const double a = v[k].x, b = v[k].y, e = v[k].z, f = v[k].w;
       s1 += (a + b) + (e + f);
       s2 += (a * a + b * b) + (e * e + f * f);
@@ -119,10 +130,13 @@ __global__ __launch_bounds__(NT) void k_channel_sum(const float* __restrict__ x,
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       const int i = threadIdx.x + k * NT;
-      v[k] = i < n4 ? p[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k] = p[i < n4 ? i : n4 - 1];
     }
 #pragma unroll
-    for (int k = 0; k < VPT; ++k) s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    for (int k = 0; k < VPT; ++k) {
+      v[k] = zero_unless((int)threadIdx.x + k * NT < n4, v[k]);
+      s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
   } else {
     for (int64_t i = c.begin + threadIdx.x; i < c.end; i += NT) s1 += x[c.base + i];
   }
@@ -275,12 +289,12 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_stats(const float* __restri
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const int i = threadIdx.x + (h * U + k) * NT;
-        const bool ok = i < n4;
-        vx[k] = ok ? px[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        vg[k] = ok ? pg[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        vx[k] = px[i < n4 ? i : n4 - 1];
+        vg[k] = pg[i < n4 ? i : n4 - 1];
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
+        vg[k] = zero_unless((int)threadIdx.x + (h * U + k) * NT < n4, vg[k]);  // g = 0: no contribution
         visit(vx[k].x, vg[k].x);
         visit(vx[k].y, vg[k].y);
         visit(vx[k].z, vg[k].z);
@@ -385,8 +399,9 @@ struct AdnArgs {
   const float* aw;
   float* dw;
   float* dbias;
-  double* part;   // [NC][nblk][2 | 4]: block partials (forward: sum x, x^2; backward: g, g z, dy z [z<=0], z)
-  double* inst;   // [NC][4]: per-instance results (backward: mg, mgz, sa, the bias-gradient share)
+  float* dysum;   // backward: per-channel sum over n and voxels of dy (the residual conv's bias gradient)
+  double* part;   // [NC][nblk][2 | 5]: block partials (forward: sum x, x^2; backward: g, g z, dy z [z<=0], z, dy)
+  double* inst;   // [NC][5]: per-instance results (backward: mg, mgz, sa, the bias-gradient share, sum dy)
   uint32_t* cnt;  // [2 NC + C + 1]
   int64_t S;
   int C, NC, nblk;  // nblk: statistics partials per instance (blocks of the statistics sweeps)
@@ -472,10 +487,11 @@ __global__ __launch_bounds__(NT) void k_adn_stats(const AdnArgs a) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       const int i = threadIdx.x + k * NT;
-      v[k] = i < n4 ? reinterpret_cast<const float4*>(xp)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[k] = reinterpret_cast<const float4*>(xp)[i < n4 ? i : n4 - 1];
     }
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
+      v[k] = zero_unless((int)threadIdx.x + k * NT < n4, v[k]);
       const double p = v[k].x, q = v[k].y, r = v[k].z, t = v[k].w;
       s1 += (p + q) + (r + t);
       s2 += (p * p + q * q) + (r * r + t * t);
@@ -546,15 +562,19 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
   const int nc = blockIdx.y;
   const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
   const double md = mean, rd = rstd;
-  double s1 = 0.0, s2 = 0.0, sa = 0.0, sz = 0.0;
+  // Per voxel only float64 sums of x-moments (the z-centred sums follow per block, exactly in exact
+  // arithmetic): P1 = sum dy, P2 = sum dy x over z > 0; N1, N2 the same over z <= 0; X = sum x.  Then
+  // s1 = sum g = P1 + a N1, s2 = sum g z = rd (P2 + a N2 - md s1), sa = sum_{z<=0} dy z = rd (N2 - md N1),
+  // sz = sum z = rd (X - n md): 3 conversions + 5 float64 adds / FMAs per voxel instead of ~11 + selects.
+  double P1 = 0.0, P2 = 0.0, N1 = 0.0, N2 = 0.0, X = 0.0;
   auto visit = [&](float xv, float gv, bool in = true) {  // (in: a real voxel, not a zero-padded lane)
     const bool pos = (xv - mean) * rstd > 0.f;
-    const double z = ((double)xv - md) * rd;
-    const double g = pos ? (double)gv : (double)aw * (double)gv;
-    s1 += g;
-    s2 += g * z;
-    sa += pos ? 0.0 : (double)gv * z;
-    sz += in ? z : 0.0;
+    const double x = in ? xv : 0.f, dp = pos ? gv : 0.f, dn = pos ? 0.f : gv;
+    P1 += dp;
+    N1 += dn;
+    P2 += dp * x;
+    N2 += dn * x;
+    X += x;
   };
   const int64_t b = (int64_t)blockIdx.x * CHUNK;
   const int64_t e = b + CHUNK < a.S ? b + CHUNK : a.S;
@@ -563,57 +583,68 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
   if (a.vec) {
     const int n4 = (int)((e - b) >> 2);
     constexpr int U = VPT / 2;
+    auto sweep = [&](auto full) {  // full: every lane of the chunk is a voxel (no masking selects)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float4 vx[U], vg[U];
+      for (int h = 0; h < 2; ++h) {
+        float4 vx[U], vg[U];
 #pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const int i = threadIdx.x + (h * U + k) * NT;
-        const bool ok = i < n4;
-        vx[k] = ok ? reinterpret_cast<const float4*>(xp)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        vg[k] = ok ? reinterpret_cast<const float4*>(gp)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < U; ++k) {
+          const int i = threadIdx.x + (h * U + k) * NT;
+          vx[k] = reinterpret_cast<const float4*>(xp)[decltype(full)::value || i < n4 ? i : n4 - 1];
+          vg[k] = reinterpret_cast<const float4*>(gp)[decltype(full)::value || i < n4 ? i : n4 - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          const bool in = decltype(full)::value || (int)threadIdx.x + (h * U + k) * NT < n4;
+          vg[k] = zero_unless(in, vg[k]);  // g = 0 adds nothing to P, N; `in` masks X
+          visit(vx[k].x, vg[k].x, in);
+          visit(vx[k].y, vg[k].y, in);
+          visit(vx[k].z, vg[k].z, in);
+          visit(vx[k].w, vg[k].w, in);
+        }
       }
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const bool in = (int)threadIdx.x + (h * U + k) * NT < n4;
-        visit(vx[k].x, vg[k].x, in);
-        visit(vx[k].y, vg[k].y, in);
-        visit(vx[k].z, vg[k].z, in);
-        visit(vx[k].w, vg[k].w, in);
-      }
-    }
+    };
+    if (n4 == VPT * NT)
+      sweep(std::true_type{});
+    else
+      sweep(std::false_type{});
   } else {
     for (int64_t i = threadIdx.x; i < e - b; i += NT) visit(xp[i], gp[i]);
   }
-  double in[4] = {s1, s2, sa, sz}, tot[4];
-  block_sum<4>(in, tot);
-  if (threadIdx.x < 4) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 4 + threadIdx.x] = tot[threadIdx.x];
+  double in[5] = {P1, P2, N1, N2, X}, bs[5];
+  block_sum<5>(in, bs);
+  const double s1 = bs[0] + (double)aw * bs[2];
+  const double tot[5] = {s1, rd * (bs[1] + (double)aw * bs[3] - md * s1), rd * (bs[3] - md * bs[2]),
+                         rd * (bs[4] - (double)(e - b) * md), bs[0] + bs[2]};
+  if (threadIdx.x < 5) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 5 + threadIdx.x] = tot[threadIdx.x];
 }
 
 // one block per instance: mg, mgz, the instance's PReLU term and its share of the producing conv's bias
 // gradient, sum_voxels dx = rstd (sum g - S mg - mgz sum z) = -rstd mgz sum z (float64, from this sweep:
-// no store-pass partials and no separate finalize); the last instance block to finish sums the PReLU
-// weight gradient over the instances and the bias gradient over the samples (in order)
+// no store-pass partials and no separate finalize), and sum dy; the last instance block to finish sums the
+// PReLU weight gradient over the instances and the bias gradient and dy sum over the samples (in order)
 __global__ __launch_bounds__(NT) void k_adn_fin_bwd(const AdnArgs a) {
   const int nc = blockIdx.x;
-  double all[4];
-  reduce_partials<4>(a.part + (int64_t)nc * a.nblk * 4, a.nblk, all);
+  double all[5];
+  reduce_partials<5>(a.part + (int64_t)nc * a.nblk * 5, a.nblk, all);
   const double mgz = all[1] / (double)a.S;
-  double res[4] = {all[0] / (double)a.S, mgz, all[2], -(double)a.rstd[nc] * mgz * all[3]};
-  if (!publish_last<4>(res, a.inst, nc, a.cnt, a.NC)) return;
+  double res[5] = {all[0] / (double)a.S, mgz, all[2], -(double)a.rstd[nc] * mgz * all[3], all[4]};
+  if (!publish_last<5>(res, a.inst, nc, a.cnt, a.NC)) return;
   if (a.dw) {
     double v[1] = {0.0}, sw[1];
-    for (int i = threadIdx.x; i < a.NC; i += NT) v[0] += load_d(a.inst + 4 * i + 2);
+    for (int i = threadIdx.x; i < a.NC; i += NT) v[0] += load_d(a.inst + 5 * i + 2);
     block_sum<1>(v, sw);
     if (threadIdx.x == 0) *a.dw = (float)sw[0];
   }
-  if (a.dbias) {
-    const int N = a.NC / a.C;
-    for (int c = threadIdx.x; c < a.C; c += NT) {
-      double v = 0.0;
-      for (int n = 0; n < N; ++n) v += load_d(a.inst + 4 * (n * a.C + c) + 3);
-      a.dbias[c] = (float)v;
+  const int N = a.NC / a.C;
+  for (int c = threadIdx.x; c < a.C; c += NT) {
+    double v = 0.0, u = 0.0;
+    for (int n = 0; n < N; ++n) {
+      v += load_d(a.inst + 5 * (n * a.C + c) + 3);
+      u += load_d(a.inst + 5 * (n * a.C + c) + 4);
     }
+    if (a.dbias) a.dbias[c] = (float)v;
+    if (a.dysum) a.dysum[c] = (float)u;
   }
 }
 
@@ -622,7 +653,7 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
   const int nc = blockIdx.y;
   const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
   const double md = mean, rd = rstd;
-  const double mg = load_d(a.inst + 4 * nc), mgz = load_d(a.inst + 4 * nc + 1);
+  const double mg = load_d(a.inst + 5 * nc), mgz = load_d(a.inst + 5 * nc + 1);
   auto f = [&](float xv, float gv) {
     const bool pos = (xv - mean) * rstd > 0.f;
     const double z = ((double)xv - md) * rd;
@@ -828,7 +859,7 @@ inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintp
 
 size_t tb_adn_workspace_bytes(int64_t N, int64_t C, int64_t S) {
   const int64_t NC = N * C, nb = adn_nblk(S);
-  return (size_t)(NC * nb * 4 + NC * 4 + 64) * sizeof(double);
+  return (size_t)(NC * nb * 5 + NC * 5 + 64) * sizeof(double);
 }
 
 int64_t tb_adn_counters(int64_t N, int64_t C) { return 1 + 0 * N * C; }
@@ -856,8 +887,9 @@ int tb_adn_fwd_f32(const float* x, int64_t xsn, float* y, int64_t ysn, const flo
 }
 
 int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, float* dx, int64_t dxsn,
-                   const float* mean, const float* rstd, const float* prelu_w, float* dw, float* dbias, int64_t N,
-                   int64_t C, int64_t S, void* ws, size_t ws_bytes, uint32_t* counters, void* stream) {
+                   const float* mean, const float* rstd, const float* prelu_w, float* dw, float* dbias,
+                   float* dysum, int64_t N, int64_t C, int64_t S, void* ws, size_t ws_bytes, uint32_t* counters,
+                   void* stream) {
   if (!x || !dy || !dx || !mean || !rstd || !prelu_w || !ws || !counters || N < 1 || C < 1 || S < 1 ||
       N * C > 65535)
     return TB_ERR_INVALID_ARG;
@@ -865,9 +897,9 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
   AdnArgs a{};
   a.x = x, a.dy = dy, a.y = dx;
   a.xsn = xsn > 0 ? xsn : C * S, a.dysn = dysn > 0 ? dysn : C * S, a.ysn = dxsn > 0 ? dxsn : C * S;
-  a.mean = const_cast<float*>(mean), a.rstd = const_cast<float*>(rstd), a.aw = prelu_w, a.dw = dw, a.dbias = dbias;
+  a.mean = const_cast<float*>(mean), a.rstd = const_cast<float*>(rstd), a.aw = prelu_w, a.dw = dw, a.dbias = dbias, a.dysum = dysum;
   a.part = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  a.inst = a.part + N * C * adn_nblk(S) * 4;
+  a.inst = a.part + N * C * adn_nblk(S) * 5;
   a.cnt = counters;
   a.S = S, a.C = (int)C, a.NC = (int)(N * C), a.nblk = adn_nblk(S);
   a.vec = S % 4 == 0 && a.xsn % 4 == 0 && a.ysn % 4 == 0 && a.dysn % 4 == 0 && al16(x) && al16(dy) && al16(dx);

@@ -51,7 +51,7 @@ def _proto(L):
         "tb_adn_workspace_bytes": (SZ, [I64, I64, I64]),
         "tb_adn_counters": (I64, [I64, I64]),
         "tb_adn_fwd_f32": (I, [P, I64, P, I64, P, I64, P, P, P, I64, I64, I64, F, P, SZ, P, P]),
-        "tb_adn_bwd_f32": (I, [P, I64, P, I64, P, I64, P, P, P, P, P, I64, I64, I64, P, SZ, P, P]),
+        "tb_adn_bwd_f32": (I, [P, I64, P, I64, P, I64, P, P, P, P, P, P, I64, I64, I64, P, SZ, P, P]),
         "tb_conv3d_small_f32": (I, [P, P, P, P] + [I] * 6 + [P]),
         "tb_conv3d_small_add_f32": (I, [P, P, P, P, P] + [I] * 6 + [P]),
         "tb_conv3d_fwd16_add_f32": (I, [P, P, P, P, P] + [I] * 4 + [P]),

@@ -84,9 +84,12 @@ def adn_forward(x: torch.Tensor, w: torch.Tensor, eps: float, res: Optional[torc
 
 
 def adn_backward(x: torch.Tensor, dy: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, w: torch.Tensor,
-                 need_w: bool = True, need_bias: bool = False, dx_out: Optional[torch.Tensor] = None):
+                 need_w: bool = True, need_bias: bool = False, dx_out: Optional[torch.Tensor] = None,
+                 dysum_out: Optional[torch.Tensor] = None):
     """(dx, dw or None, dbias or None): the ADN's input gradient, its PReLU weight gradient and the
-    bias gradient of the convolution that produced x (dx summed over n and the voxels)."""
+    bias gradient of the convolution that produced x (dx summed over n and the voxels).  ``dysum_out``
+    (float32 [C], optional) receives dy summed over n and the voxels out of the same sweep (the bias
+    gradient of a residual convolution added to this block's output)."""
     x = _plain(x)
     dy = _plain(dy)
     N, C = x.shape[:2]
@@ -101,7 +104,8 @@ def adn_backward(x: torch.Tensor, dy: torch.Tensor, mean: torch.Tensor, rstd: to
         check(lib().tb_adn_bwd_f32(x.data_ptr(), _sn(x, S), dy.data_ptr(), _sn(dy, S), dx.data_ptr(), _sn(dx, S),
                                    mean.data_ptr(), rstd.data_ptr(), w.detach().data_ptr(),
                                    dw.data_ptr() if dw is not None else None,
-                                   db.data_ptr() if db is not None else None, N, C, S, ws.data_ptr(), nb,
+                                   db.data_ptr() if db is not None else None,
+                                   dysum_out.data_ptr() if dysum_out is not None else None, N, C, S, ws.data_ptr(), nb,
                                    cnt.data_ptr(), _stream(x)), "tb_adn_bwd_f32")
     if dw is not None:
         dw = dw.view(w.shape)

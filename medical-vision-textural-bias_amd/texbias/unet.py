@@ -144,7 +144,9 @@ class _StackedUnitFn(torch.autograd.Function):
         c, r_st, r1, has_b0, has_b1 = ctx.cfg
         n = ctx.needs_input_grad
         g = g.contiguous()
-        dz1, da1, db1 = adn_backward(z1, g, m1, s1, a1w, need_w=n[8], need_bias=has_b1)
+        # the residual conv's bias gradient (g summed over n and the voxels) out of the ADN's statistics sweep
+        dbr = torch.empty(c, dtype=g.dtype, device=g.device) if has_b0 and n[4] else None
+        dz1, da1, db1 = adn_backward(z1, g, m1, s1, a1w, need_w=n[8], need_bias=has_b1, dysum_out=dbr)
         da0 = r1.input_grad(dz1, a0, w1)
         gw1 = r1.weight_grad(dz1, a0, w1) if n[6] else None
         dy2 = torch.empty_like(y2)
@@ -153,7 +155,6 @@ class _StackedUnitFn(torch.autograd.Function):
                                     dx_out=dy2[:, :c])
         gx = r_st.input_grad(dy2, x, w_st) if n[0] else None
         gw_st = r_st.weight_grad(dy2, x, w_st) if (n[1] or n[3]) else None
-        dbr = _conv.channel_sum(g) if has_b0 and n[4] else None
         return (gx, gw_st[:c] if gw_st is not None else None, db0, gw_st[c:] if gw_st is not None else None, dbr,
                 dw0a, gw1, db1 if n[7] else None, da1, None, None)
 

@@ -108,6 +108,11 @@ def test_adn_strided_residual_bias(gpu, shape):
     torch.testing.assert_close(db.double(), dx.double().sum(dim=(0, 2, 3, 4)), rtol=0, atol=tol)
     dx2, dw2, db2 = adn_backward(z, g, mean, rstd, w, need_w=True, need_bias=True)
     assert torch.equal(dx2, dx) and torch.equal(dw2, dw) and torch.equal(db2, db)
+    # the residual conv's bias gradient out of the same sweep: dy summed over n and the voxels (float64 sums)
+    ds = torch.full((C,), float("nan"), device=gpu)
+    dx3, _, _ = adn_backward(z, g, mean, rstd, w, need_w=False, need_bias=False, dysum_out=ds)
+    assert torch.equal(dx3, dx)
+    torch.testing.assert_close(ds.double(), g.double().sum(dim=(0, 2, 3, 4)), rtol=1e-6, atol=1e-6)
     y2, m2, s2 = adn_forward(z, w, 1e-5, res=r)
     assert torch.equal(y2, y) and torch.equal(m2, mean) and torch.equal(s2, rstd)
     from texbias.norm import counters
