@@ -350,8 +350,8 @@ int tb_instnorm_prelu_bwd_f32(const float* x, const float* dy, const float* mean
  * is zero: the norm removes a bias; NULL: not computed), dysum[c] = sum over n and voxels of dy (the
  * bias gradient of a residual convolution summed into the same output, out of the same sweep; NULL: not
  * computed), and the PReLU weight gradient dw (NULL: not computed).  No accumulator memsets and no float atomics: every block stores partial sums, reduced in
- * block order (forward: by every apply block; backward: one block per instance) -- results are
- * deterministic; two launches forward, three backward.  `counters`: DEVICE
+ * block order (by every apply block) -- results are
+ * deterministic; two launches forward, two backward.  `counters`: DEVICE
  * uint32[tb_adn_counters(N, C)], zero before the first call, left zero by every call (one set per
  * stream); ws: tb_adn_workspace_bytes(N, C, S) bytes of device scratch.
  */

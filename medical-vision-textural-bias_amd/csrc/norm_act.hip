@@ -181,15 +181,24 @@ __global__ __launch_bounds__(NT) void k_dice_sums(const float* __restrict__ x, c
     const float4* px = reinterpret_cast<const float4*>(x + c.base + c.begin);
     const float4* pt = reinterpret_cast<const float4*>(t + c.base + c.begin);
     const int n4 = (int)((c.end - c.begin) >> 2);
-#pragma unroll 4
-    for (int k = 0; k < VPT; ++k) {
-      const int i = threadIdx.x + k * NT;
-      if (i < n4) {
-        const float4 xv = px[i], tv = pt[i];
-        add1(xv.x, tv.x);
-        add1(xv.y, tv.y);
-        add1(xv.z, tv.z);
-        add1(xv.w, tv.w);
+    constexpr int U = VPT / 2;  // two halves of 2 x 8 float4, every load issued before the first use
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 xv[U], tv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int i = threadIdx.x + (h * U + k) * NT;
+        xv[k] = px[i < n4 ? i : n4 - 1];
+        tv[k] = pt[i < n4 ? i : n4 - 1];
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if ((int)threadIdx.x + (h * U + k) * NT < n4) {
+          add1(xv[k].x, tv[k].x);
+          add1(xv[k].y, tv[k].y);
+          add1(xv[k].z, tv[k].z);
+          add1(xv[k].w, tv[k].w);
+        }
       }
     }
   } else {
@@ -381,13 +390,14 @@ __global__ __launch_bounds__(NT) void k_in_prelu_bwd_apply(const float* __restri
 // The same arithmetic as K1-K4 with (a) per-sample batch strides, so that an ADN can read a channel slice
 // of a wider tensor (the stacked unit + residual convolution of a strided ResidualUnit) and write into
 // one; (b) the residual sum fused into the forward store; (c) the preceding convolution's bias gradient
-// (dx summed over n and the voxels) out of the backward's store pass; (d) no accumulator memsets and no
-// float atomics: every block stores its partial sums and a one-block-per-instance finalize kernel sums
-// them in block order (deterministic).  (A last-arriving-block reduction inside the sweep kernels --
+// (dx summed over n and the voxels) out of the backward's statistics sweep; (d) no accumulator memsets and
+// no float atomics: every statistics block stores its partial sums and every apply block sums its
+// instance's partials in block order (deterministic; round 6 folded the backward's one-block-per-instance
+// finalize launch into the apply as well).  (A last-arriving-block reduction inside the sweep kernels --
 // partial store, vmcnt drain, counter atomic at the end of every block -- measured 57.6 vs 36 us per
 // backward statistics sweep: the drain serialises each block's tail.)  The PReLU weight gradient, a sum
-// over instances, is taken by the last finalize block through one counter (a caller-owned uint32, zero
-// before the first call and left zero).
+// over instances, is taken by the last of the NC (0, nc) apply blocks through one counter (a caller-owned
+// uint32, zero before the first call and left zero).
 struct AdnArgs {
   const float* x;
   const float* dy;
@@ -619,15 +629,13 @@ __global__ __launch_bounds__(NT) void k_adn_bwd_stats(const AdnArgs a) {
   if (threadIdx.x < 5) a.part[((int64_t)nc * a.nblk + blockIdx.x) * 5 + threadIdx.x] = tot[threadIdx.x];
 }
 
-// one block per instance: mg, mgz, the instance's PReLU term and its share of the producing conv's bias
-// gradient, sum_voxels dx = rstd (sum g - S mg - mgz sum z) = -rstd mgz sum z (float64, from this sweep:
-// no store-pass partials and no separate finalize), and sum dy; the last instance block to finish sums the
-// PReLU weight gradient over the instances and the bias gradient and dy sum over the samples (in order)
-__global__ __launch_bounds__(NT) void k_adn_fin_bwd(const AdnArgs a) {
-  const int nc = blockIdx.x;
-  double all[5];
-  reduce_partials<5>(a.part + (int64_t)nc * a.nblk * 5, a.nblk, all);
-  const double mgz = all[1] / (double)a.S;
+// Every apply block first sums its instance's statistics partials (the same fixed-order reduction in
+// every block, as in the forward: no separate finalize launch) into mg = mean(g), mgz = mean(g z); block
+// (0, nc) publishes the instance's PReLU term, its share of the producing conv's bias gradient,
+// sum_voxels dx = rstd (sum g - S mg - mgz sum z) = -rstd mgz sum z (float64, from the statistics sweep:
+// no store-pass partials), and its dy sum; the last instance to publish sums the PReLU weight gradient
+// over the instances and the bias gradient and dy sum over the samples (in order).
+__device__ __forceinline__ void adn_bwd_finish(const AdnArgs& a, int nc, const double (&all)[5], double mgz) {
   double res[5] = {all[0] / (double)a.S, mgz, all[2], -(double)a.rstd[nc] * mgz * all[3], all[4]};
   if (!publish_last<5>(res, a.inst, nc, a.cnt, a.NC)) return;
   if (a.dw) {
@@ -648,12 +656,14 @@ __global__ __launch_bounds__(NT) void k_adn_fin_bwd(const AdnArgs a) {
   }
 }
 
-// dx = rstd (g - mg - z mgz); dbias[c] = sum over n and voxels of dx (partials + per-channel counter)
 __global__ __launch_bounds__(NT) void k_adn_bwd_apply(const AdnArgs a) {
   const int nc = blockIdx.y;
   const float mean = a.mean[nc], rstd = a.rstd[nc], aw = *a.aw;
   const double md = mean, rd = rstd;
-  const double mg = load_d(a.inst + 5 * nc), mgz = load_d(a.inst + 5 * nc + 1);
+  double all[5];
+  reduce_partials<5>(a.part + (int64_t)nc * a.nblk * 5, a.nblk, all);
+  const double mg = all[0] / (double)a.S, mgz = all[1] / (double)a.S;
+  if (blockIdx.x == 0) adn_bwd_finish(a, nc, all, mgz);
   auto f = [&](float xv, float gv) {
     const bool pos = (xv - mean) * rstd > 0.f;
     const double z = ((double)xv - md) * rd;
@@ -906,7 +916,6 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)adn_nblk(S), (unsigned)a.NC);
   hipLaunchKernelGGL(k_adn_bwd_stats, dim3((unsigned)a.nblk, (unsigned)a.NC), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(k_adn_fin_bwd, dim3((unsigned)a.NC), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(k_adn_bwd_apply, grid, dim3(NT), 0, st, a);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
