@@ -115,7 +115,7 @@ class _StackedUnitFn(torch.autograd.Function):
     a0 = ADN0(unit0), out = ADN1(conv1(a0)) + residual."""
 
     @staticmethod
-    def forward(ctx, x, w0, b0, wr, br, a0w, w1, b1, a1w, unit, eps):
+    def forward(ctx, x, w0, b0, wr, br, a0w, w1, b1, a1w, unit, eps, skip):
         c = w0.shape[0]
         w_st = _adjacent(w0, wr)
         if w_st is None:
@@ -136,6 +136,7 @@ class _StackedUnitFn(torch.autograd.Function):
         out, m1, s1 = adn_forward(z1, a1w, eps, res=res)
         ctx.save_for_backward(x, w_st, a0w, w1, a1w, y2, a0, z1, m0, s0, m1, s1)
         ctx.cfg = (c, r_st, r1, b0 is not None, b1 is not None)
+        ctx.skip = skip
         return out
 
     @staticmethod
@@ -143,20 +144,24 @@ class _StackedUnitFn(torch.autograd.Function):
         x, w_st, a0w, w1, a1w, y2, a0, z1, m0, s0, m1, s1 = ctx.saved_tensors
         c, r_st, r1, has_b0, has_b1 = ctx.cfg
         n = ctx.needs_input_grad
-        g = g.contiguous()
+        dy2 = torch.empty_like(y2)
+        gs = ctx.skip.pop("g", None)
+        if gs is not None:  # the skip concatenation's share of this output's gradient, summed straight into
+            g = torch.add(g, gs, out=dy2[:, c:])  # the residual conv's half of the stacked output gradient
+        else:
+            g = g.contiguous()
+            dy2[:, c:].copy_(g)                               # the residual conv's output gradient
         # the residual conv's bias gradient (g summed over n and the voxels) out of the ADN's statistics sweep
         dbr = torch.empty(c, dtype=g.dtype, device=g.device) if has_b0 and n[4] else None
         dz1, da1, db1 = adn_backward(z1, g, m1, s1, a1w, need_w=n[8], need_bias=has_b1, dysum_out=dbr)
         da0 = r1.input_grad(dz1, a0, w1)
         gw1 = r1.weight_grad(dz1, a0, w1) if n[6] else None
-        dy2 = torch.empty_like(y2)
-        dy2[:, c:].copy_(g)                                   # the residual conv's output gradient
         _, dw0a, db0 = adn_backward(y2[:, :c], da0, m0, s0, a0w, need_w=n[5], need_bias=has_b0,
                                     dx_out=dy2[:, :c])
         gx = r_st.input_grad(dy2, x, w_st) if n[0] else None
         gw_st = r_st.weight_grad(dy2, x, w_st) if (n[1] or n[3]) else None
         return (gx, gw_st[:c] if gw_st is not None else None, db0, gw_st[c:] if gw_st is not None else None, dbr,
-                dw0a, gw1, db1 if n[7] else None, da1, None, None)
+                dw0a, gw1, db1 if n[7] else None, da1, None, None, None)
 
 
 class ADN(nn.Sequential):
@@ -239,8 +244,11 @@ class ResidualUnit(nn.Module):
                     and isinstance(u0.conv, Conv3d) and _fusable(x, u0.conv, u0.adn) and _fusable(x, r, None) and \
                     _fusable(x, u1.conv, u1.adn) and (r.bias is None) == (u0.conv.bias is None) and \
                     u0.adn.N.eps == u1.adn.N.eps and r.padding_mode == "zeros":
-                return _StackedUnitFn.apply(x, u0.conv.weight, u0.conv.bias, r.weight, r.bias, u0.adn.A.weight,
-                                            u1.conv.weight, u1.conv.bias, u1.adn.A.weight, self, u0.adn.N.eps)
+                skip = {}
+                y = _StackedUnitFn.apply(x, u0.conv.weight, u0.conv.bias, r.weight, r.bias, u0.adn.A.weight,
+                                         u1.conv.weight, u1.conv.bias, u1.adn.A.weight, self, u0.adn.N.eps, skip)
+                y._tb_skip = skip  # a skip concatenation of y hands its gradient share over (_SkipCatFn)
+                return y
         if isinstance(self.residual, nn.Identity) and len(units) == 1 and hasattr(units[0], "adn"):
             out = self.__dict__.pop("_tb_out", None)
             if out is not None and tuple(out.shape) != tuple(x.shape[:1]) + (units[0].conv.out_channels,) + \
@@ -312,18 +320,25 @@ def _alias(buf: torch.Tensor, c0: int, c1: int) -> torch.Tensor:
 
 
 class _SkipCatFn(torch.autograd.Function):
-    """cat([x, s], 1) where s already sits in channels [c, c + cs) of ``buf``: only x is copied."""
+    """cat([x, s], 1) where s already sits in channels [c, c + cs) of ``buf``: only x is copied.  When x
+    comes from a stacked ResidualUnit (``skip``: its hand-over dict), x's gradient share g[:, :c] is handed
+    to that unit's backward, which sums it with the submodule's share straight into its stacked output
+    gradient (no autograd accumulation pass, no copy); autograd runs this backward before the submodule's
+    and the unit's, since both need the gradient of s first."""
 
     @staticmethod
-    def forward(ctx, x, s, buf):
+    def forward(ctx, x, s, buf, skip=None):
         c = x.shape[1]
         _alias(buf, 0, c).copy_(x)
-        ctx.c = c
+        ctx.c, ctx.skip = c, skip
         return _alias(buf, 0, buf.shape[1])
 
     @staticmethod
     def backward(ctx, g):
-        return g[:, :ctx.c], g[:, ctx.c:], None
+        if ctx.skip is not None and ctx.needs_input_grad[0]:
+            ctx.skip["g"] = g[:, :ctx.c]
+            return None, g[:, ctx.c:], None, None
+        return g[:, :ctx.c], g[:, ctx.c:], None, None
 
 
 class SkipConnection(nn.Module):
@@ -354,7 +369,7 @@ class SkipConnection(nn.Module):
             finally:
                 ru.__dict__.pop("_tb_out", None)
             if s.data_ptr() == tail.data_ptr() and s.shape == tail.shape:
-                return _SkipCatFn.apply(x, s, buf)
+                return _SkipCatFn.apply(x, s, buf, getattr(x, "_tb_skip", None))
             return torch.cat([x, s], dim=1)
         return torch.cat([x, self.submodule(x)], dim=1)
 
