@@ -366,6 +366,20 @@ int tb_adn_bwd_f32(const float* x, int64_t xsn, const float* dy, int64_t dysn, f
                    void* stream);
 
 /*
+ * One Adam step over nt float32 tensors on the device, torch.optim.Adam semantics (L2 weight decay added
+ * to the gradient; amsgrad: the denominator from the running maximum of exp_avg_sq), the reference's
+ * optimizer (stylized_gibbs12p5.py:203-205: Adam(params, 1e-4, weight_decay=1e-5, amsgrad=True)).  The
+ * pointer arrays are HOST arrays of DEVICE pointers; step[i] is tensor i's DEVICE float32 step count,
+ * already incremented for this step (as torch's fused / capturable Adam keeps it); numel[i] (host) its
+ * element count.  max_exp_avg_sq may be NULL without amsgrad.  Tensors are cut into 4096-element
+ * chunks, up to 32 tensors per launch (csrc/optim.hip, k_adam).  Graph-capturable.
+ */
+int tb_adam_f32(int nt, float* const* param, const float* const* grad, float* const* exp_avg,
+                float* const* exp_avg_sq, float* const* max_exp_avg_sq, const float* const* step,
+                const int64_t* numel, double lr, double beta1, double beta2, double eps, double weight_decay,
+                int amsgrad, void* stream);
+
+/*
  * GPU-side BraTS preprocessing of B resident raw volumes img [B][C][H0][W0][D0] and
  * label maps lab [B][H0][W0][D0] (float class ids, as LoadImaged gives them; may be NULL when
  * out_lab is NULL), per sample b with params[b] drawn on the host:

@@ -20,6 +20,7 @@ from typing import Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from . import optim as _optim
 from .losses import DiceLoss
 from .unet import UNet, pack_parameters
 
@@ -100,6 +101,9 @@ class TrainStep:
             self.model = model
         self.loss_fn = DiceLoss(to_onehot_y=False, sigmoid=True, squared_pred=True)
         opt_kw = dict(lr=1e-4, weight_decay=1e-5, amsgrad=True)
+        if device.type == "cuda" and _optim.ENABLED:  # one texbias launch (csrc/optim.hip); capturable
+            self.opt = _optim.Adam(self.model.parameters(), **opt_kw)
+            return
         if device.type == "cuda":
             opt_kw["fused"] = True
             if capturable:
