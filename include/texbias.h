@@ -222,6 +222,11 @@ int tb_dice_loss_bwd_f32(const double* sums, const float* gloss, float* gsums, i
  * -- replaces ATen's generic reduction in the U-Net backward (stylized_gibbs12p5.py:232-243).
  */
 int tb_channel_sum_f32(const float* x, float* out, int64_t N, int64_t C, int64_t S, void* stream);
+/* The same without float atomics: float64 block partials in ws (tb_channel_sum_ws_bytes(N, C, S) bytes of
+ * device scratch) summed per channel in block order -- deterministic; two launches. */
+size_t tb_channel_sum_ws_bytes(int64_t N, int64_t C, int64_t S);
+int tb_channel_sum_ws_f32(const float* x, float* out, int64_t N, int64_t C, int64_t S, void* ws, size_t ws_bytes,
+                          void* stream);
 
 /*
  * Direct 3x3x3 convolution, stride 1, padding 1, for Cin, Cout <= 4 (the U-Net's full-resolution

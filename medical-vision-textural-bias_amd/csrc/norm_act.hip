@@ -481,6 +481,46 @@ __device__ __forceinline__ void reduce_partials(const double* part, int n, doubl
   block_sum<K>(v, out);
 }
 
+// The same channel sums without float atomics (every block of one channel had added its partial to one
+// address: ~1,100 contended atomics per channel at the U-Net's full resolution): each block stores its
+// float64 partial, then one block per channel sums them over the samples and blocks in order
+// (deterministic).
+__global__ __launch_bounds__(NT) void k_channel_part(const float* __restrict__ x, double* __restrict__ part,
+                                                     int64_t S, int vec) {
+  const Chunk c = chunk_of(S);
+  float s1 = 0.f;
+  if (vec) {
+    const float4* p = reinterpret_cast<const float4*>(x + c.base + c.begin);
+    const int n4 = (int)((c.end - c.begin) >> 2);
+    float4 v[VPT];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int i = threadIdx.x + k * NT;
+      v[k] = p[i < n4 ? i : n4 - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      v[k] = zero_unless((int)threadIdx.x + k * NT < n4, v[k]);
+      s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+  } else {
+    for (int64_t i = c.begin + threadIdx.x; i < c.end; i += NT) s1 += x[c.base + i];
+  }
+  double in[1] = {(double)s1}, tot[1];
+  block_sum<1>(in, tot);
+  if (threadIdx.x == 0) part[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = tot[0];
+}
+
+__global__ __launch_bounds__(NT) void k_channel_fin(const double* __restrict__ part, float* __restrict__ out, int N,
+                                                    int C, int nblk) {
+  const int c = (int)blockIdx.x;
+  double v[1] = {0.0}, tot[1];
+  for (int n = 0; n < N; ++n)
+    for (int i = threadIdx.x; i < nblk; i += NT) v[0] += part[((int64_t)n * C + c) * nblk + i];
+  block_sum<1>(v, tot);
+  if (threadIdx.x == 0) out[c] = (float)tot[0];
+}
+
 __device__ __forceinline__ int64_t inst_base(int nc, int C, int64_t sn, int64_t S) {
   return (int64_t)(nc / C) * sn + (int64_t)(nc % C) * S;
 }
@@ -805,6 +845,23 @@ int tb_channel_sum_f32(const float* x, float* out, int64_t N, int64_t C, int64_t
   const int vec = (S % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) ? 1 : 0;
   const dim3 grid((unsigned)((S + CHUNK - 1) / CHUNK), (unsigned)(N * C));
   hipLaunchKernelGGL(k_channel_sum, grid, dim3(NT), 0, st, x, out, S, (int)C, vec);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+size_t tb_channel_sum_ws_bytes(int64_t N, int64_t C, int64_t S) {
+  return (size_t)(N * C * ((S + CHUNK - 1) / CHUNK)) * sizeof(double);
+}
+
+int tb_channel_sum_ws_f32(const float* x, float* out, int64_t N, int64_t C, int64_t S, void* ws, size_t ws_bytes,
+                          void* stream) {
+  if (!x || !out || !ws || N < 1 || C < 1 || S < 1 || N * C > 65535) return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb_channel_sum_ws_bytes(N, C, S)) return TB_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int vec = (S % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) ? 1 : 0;
+  const int nblk = (int)((S + CHUNK - 1) / CHUNK);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(k_channel_part, dim3((unsigned)nblk, (unsigned)(N * C)), dim3(NT), 0, st, x, part, S, vec);
+  hipLaunchKernelGGL(k_channel_fin, dim3((unsigned)C), dim3(NT), 0, st, part, out, (int)N, (int)C, nblk);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 

@@ -48,6 +48,8 @@ def _proto(L):
         "tb_instnorm_prelu_fwd_f32": (I, [P, P, P, P, P, I64, I64, F, P, SZ, P]),
         "tb_instnorm_prelu_bwd_f32": (I, [P, P, P, P, P, P, P, I64, I64, P, SZ, P]),
         "tb_channel_sum_f32": (I, [P, P, I64, I64, I64, P]),
+        "tb_channel_sum_ws_bytes": (SZ, [I64, I64, I64]),
+        "tb_channel_sum_ws_f32": (I, [P, P, I64, I64, I64, P, SZ, P]),
         "tb_adn_workspace_bytes": (SZ, [I64, I64, I64]),
         "tb_adam_f32": (I, [I, P, P, P, P, P, P, P] + [C.c_double] * 5 + [I, P]),
         "tb_adn_counters": (I64, [I64, I64]),

@@ -70,13 +70,17 @@ def wgrad_config(g_shape, x_shape, stride: int, pad: int = 1) -> dict:
 
 
 def channel_sum(g: torch.Tensor) -> torch.Tensor:
-    """g [N, C, *spatial] -> [C]: sum over N and the spatial axes (tb_channel_sum_f32)."""
+    """g [N, C, *spatial] -> [C]: sum over N and the spatial axes (tb_channel_sum_ws_f32: float64 block
+    partials summed in block order -- deterministic, no float atomics)."""
     g = g.contiguous()
     N, Cc = g.shape[:2]
+    S = g[0, 0].numel()
     out = torch.empty(Cc, dtype=torch.float32, device=g.device)
+    nb = int(lib().tb_channel_sum_ws_bytes(N, Cc, S))
+    ws = torch.empty(nb, dtype=torch.uint8, device=g.device)
     with torch.cuda.device(g.device):
-        check(lib().tb_channel_sum_f32(g.data_ptr(), out.data_ptr(), N, Cc, g[0, 0].numel(), _stream(g)),
-              "tb_channel_sum_f32")
+        check(lib().tb_channel_sum_ws_f32(g.data_ptr(), out.data_ptr(), N, Cc, S, ws.data_ptr(), nb, _stream(g)),
+              "tb_channel_sum_ws_f32")
     return out
 
 

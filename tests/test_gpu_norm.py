@@ -146,3 +146,16 @@ def test_skip_buffer_matches_cat(gpu, monkeypatch):
     assert abs(l1.item() - l2.item()) <= 1e-6
     for a, b in zip(g1, g2):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * max(b.abs().max().item(), 1e-3))
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 240, 240, 160), (2, 16, 20, 24, 16), (1, 5, 33, 31, 7)])
+def test_channel_sum_partials(gpu, shape):
+    """texbias.conv.channel_sum (a conv's bias gradient: float64 block partials summed in block order)
+    against float64 sums; bit-identical on a second call."""
+    from texbias.conv import channel_sum
+    torch.manual_seed(3)
+    g = torch.randn(shape, device=gpu) + 0.25
+    a = channel_sum(g)
+    ref = g.double().sum(dim=(0, 2, 3, 4))
+    torch.testing.assert_close(a.double(), ref, rtol=1e-6, atol=1e-6 * math.sqrt(g[:, 0].numel()))
+    assert torch.equal(channel_sum(g), a)
