@@ -196,6 +196,11 @@ int tb_conv3d_wgrad_config(int N, int M, int Cc, int Do, int Ho, int Wo, int Di,
  */
 int tb_dice_sums_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, int sigmoid, int squared,
                      void* stream);
+/* The same sums without float atomics: float64 block partials in ws (tb_dice_sums_ws_bytes(NC, S) bytes of
+ * device scratch) summed per instance in block order -- deterministic; two launches. */
+size_t tb_dice_sums_ws_bytes(int64_t NC, int64_t S);
+int tb_dice_sums_ws_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, int sigmoid, int squared,
+                        void* ws, size_t ws_bytes, void* stream);
 /*
  * Dice METRIC statistics of the reference's evaluation loop (source_code/utils.py:313-411:
  * Activations(sigmoid=True) + AsDiscrete(threshold 0.5) then DiceMetric(include_background)):

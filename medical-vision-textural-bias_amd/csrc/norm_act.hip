@@ -481,6 +481,65 @@ __device__ __forceinline__ void reduce_partials(const double* part, int n, doubl
   block_sum<K>(v, out);
 }
 
+// Dice statistics without float atomics (k_dice_sums adds every block's three sums to its instance's
+// doubles: ~560 contended atomics per address at the U-Net's output): float64 block partials
+// [NC][nblk][3], then one block per instance sums them in block order (deterministic; the same 103-105 us
+// per C3 call as the atomic version -- and as with the hardware exp / reciprocal sigmoid, so neither the
+// atomics nor the sigmoid's ~30 VALU ops per voxel set this sweep's time).
+__global__ __launch_bounds__(NT) void k_dice_part(const float* __restrict__ x, const float* __restrict__ t,
+                                                  double* __restrict__ part, int64_t S, int flags, int vec) {
+  const Chunk c = chunk_of(S);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  auto add1 = [&](float xv, float tv) {
+    float p = (flags & 1) ? sigm(xv) : xv;
+    a0 += tv * p;
+    if (flags & 2) {
+      a1 += tv * tv;
+      a2 += p * p;
+    } else {
+      a1 += tv;
+      a2 += p;
+    }
+  };
+  if (vec) {
+    const float4* px = reinterpret_cast<const float4*>(x + c.base + c.begin);
+    const float4* pt = reinterpret_cast<const float4*>(t + c.base + c.begin);
+    const int n4 = (int)((c.end - c.begin) >> 2);
+    constexpr int U = VPT / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 xv[U], tv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int i = threadIdx.x + (h * U + k) * NT;
+        xv[k] = px[i < n4 ? i : n4 - 1];
+        tv[k] = pt[i < n4 ? i : n4 - 1];
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if ((int)threadIdx.x + (h * U + k) * NT < n4) {
+          add1(xv[k].x, tv[k].x);
+          add1(xv[k].y, tv[k].y);
+          add1(xv[k].z, tv[k].z);
+          add1(xv[k].w, tv[k].w);
+        }
+      }
+    }
+  } else {
+    for (int64_t i = c.begin + threadIdx.x; i < c.end; i += NT) add1(x[c.base + i], t[c.base + i]);
+  }
+  double in[3] = {(double)a0, (double)a1, (double)a2}, tot[3];
+  block_sum<3>(in, tot);
+  if (threadIdx.x < 3) part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 3 + threadIdx.x] = tot[threadIdx.x];
+}
+
+__global__ __launch_bounds__(NT) void k_dice_fin(const double* __restrict__ part, double* __restrict__ sums, int nblk) {
+  const int nc = (int)blockIdx.x;
+  double all[3];
+  reduce_partials<3>(part + (int64_t)nc * nblk * 3, nblk, all);
+  if (threadIdx.x < 3) sums[3 * (int64_t)nc + threadIdx.x] = all[threadIdx.x];
+}
+
 // The same channel sums without float atomics (every block of one channel had added its partial to one
 // address: ~1,100 contended atomics per channel at the U-Net's full resolution): each block stores its
 // float64 partial, then one block per channel sums them over the samples and blocks in order
@@ -845,6 +904,24 @@ int tb_channel_sum_f32(const float* x, float* out, int64_t N, int64_t C, int64_t
   const int vec = (S % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) ? 1 : 0;
   const dim3 grid((unsigned)((S + CHUNK - 1) / CHUNK), (unsigned)(N * C));
   hipLaunchKernelGGL(k_channel_sum, grid, dim3(NT), 0, st, x, out, S, (int)C, vec);
+  return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
+}
+
+size_t tb_dice_sums_ws_bytes(int64_t NC, int64_t S) {
+  return (size_t)(NC * ((S + CHUNK - 1) / CHUNK) * 3) * sizeof(double);
+}
+
+int tb_dice_sums_ws_f32(const float* x, const float* t, double* sums, int64_t NC, int64_t S, int sigmoid, int squared,
+                        void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !t || !sums || !ws || NC < 1 || S < 1 || NC > 65535) return TB_ERR_INVALID_ARG;
+  if (ws_bytes < tb_dice_sums_ws_bytes(NC, S)) return TB_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int vec = (S % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  const int nblk = (int)((S + CHUNK - 1) / CHUNK);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(k_dice_part, dim3((unsigned)nblk, (unsigned)NC), dim3(NT), 0, st, x, t, part, S,
+                     (sigmoid ? 1 : 0) | (squared ? 2 : 0), vec);
+  hipLaunchKernelGGL(k_dice_fin, dim3((unsigned)NC), dim3(NT), 0, st, part, sums, nblk);
   return hipGetLastError() == hipSuccess ? TB_OK : TB_ERR_HIP;
 }
 

@@ -71,6 +71,8 @@ def _proto(L):
         "tb_conv3d_gemm_f32": (I, [I, P, I64, P, P, P, I64, P, I64] + [I] * 8 + [P, SZ, P]),
         "tb_conv3d_gemm_config": (I, [I] * 9 + [P]),
         "tb_dice_sums_f32": (I, [P, P, P, I64, I64, I, I, P]),
+        "tb_dice_sums_ws_bytes": (SZ, [I64, I64]),
+        "tb_dice_sums_ws_f32": (I, [P, P, P, I64, I64, I, I, P, SZ, P]),
         "tb_dice_sums_bwd_f32": (I, [P, P, P, P, I64, I64, I, I, P]),
         "tb_dice_metric_sums_f32": (I, [P, P, P, I64, I64, P]),
         "tb_dice_loss_f32": (I, [P, P, I64, I64, I, I, F, F, P]),

@@ -3,7 +3,7 @@ squared_pred=True)`` (e.g. stylized_gibbs12p5.py:201), MONAI 0.5 semantics: per 
 ``1 - (2 sum(p t) + 1e-5) / (sum(t^2) + sum(p^2) + 1e-5)`` over the spatial axes, p = sigmoid(x),
 mean-reduced.  Parity with MONAI is unpinned (MONAI is absent in this image); the formula is
 MONAI's published one.  On HIP tensors the three per-instance sums come from one fused sweep
-(``tb_dice_sums_f32``, float64 accumulation) with a fused backward (``tb_dice_sums_bwd_f32``), and the
+(``tb_dice_sums_ws_f32``, float64 block partials summed in block order: deterministic) with a fused backward (``tb_dice_sums_bwd_f32``), and the
 finalize (the formula and its reduction, forward and backward) is one launch each way
 (``tb_dice_loss_f32`` / ``tb_dice_loss_bwd_f32``).
 """
@@ -25,6 +25,14 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _dice_sums(x, t, sums, nc: int, S: int, sigmoid: bool, squared: bool, stream: int) -> None:
+    """sums[nc][3] = {sum t p, sum t^2 | t, sum p^2 | p} per instance (tb_dice_sums_ws_f32)."""
+    nb = int(lib().tb_dice_sums_ws_bytes(nc, S))
+    ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    check(lib().tb_dice_sums_ws_f32(x.data_ptr(), t.data_ptr(), sums.data_ptr(), nc, S, int(sigmoid), int(squared),
+                                    ws.data_ptr(), nb, stream), "tb_dice_sums_ws_f32")
+
+
 class _DiceSums(torch.autograd.Function):
     """(x, t) [N, C, *spatial] -> [N, C, 3] float32 sums {t p, t^2 | t, p^2 | p}, p = sigmoid(x)?"""
 
@@ -34,8 +42,7 @@ class _DiceSums(torch.autograd.Function):
         nc, S = x.shape[0] * x.shape[1], math.prod(x.shape[2:])
         sums = torch.empty((x.shape[0], x.shape[1], 3), dtype=torch.float64, device=x.device)
         with torch.cuda.device(x.device):
-            check(lib().tb_dice_sums_f32(x.data_ptr(), t.data_ptr(), sums.data_ptr(), nc, S, int(sigmoid), int(squared),
-                                         _stream(x)), "tb_dice_sums_f32")
+            _dice_sums(x, t, sums, nc, S, sigmoid, squared, _stream(x))
         ctx.save_for_backward(x, t)
         ctx.cfg = (sigmoid, squared)
         return sums.float()
@@ -68,8 +75,7 @@ class _DiceLossFn(torch.autograd.Function):
         loss = torch.empty(oshape, dtype=torch.float32, device=x.device)
         with torch.cuda.device(x.device):
             st = _stream(x)
-            check(lib().tb_dice_sums_f32(x.data_ptr(), t.data_ptr(), sums.data_ptr(), nc, S, int(sigmoid), int(squared),
-                                         st), "tb_dice_sums_f32")
+            _dice_sums(x, t, sums, nc, S, sigmoid, squared, st)
             check(lib().tb_dice_loss_f32(sums.data_ptr(), loss.data_ptr(), nc, Cc, int(batch), red, nr, dr, st),
                   "tb_dice_loss_f32")
         ctx.save_for_backward(x, t, sums)
